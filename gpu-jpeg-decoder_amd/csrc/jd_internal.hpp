@@ -1,0 +1,124 @@
+// jd_internal.hpp — data layout shared by the host runtime and the gfx950 kernels.
+//
+// Everything a kernel reads is described here; see DESIGN.md §4 for the HBM layout of a batch.
+#pragma once
+
+#include <stdint.h>
+
+#include "jd.h"
+
+namespace jd {
+
+// Fast Huffman lookup width: one LDS read resolves every code of <= kLutBits bits (and, when the
+// magnitude bits fit too, the coefficient value).  Longer codes take the canonical slow path.
+constexpr int kLutBits = 10;
+constexpr int kLutSize = 1 << kLutBits;
+
+// Device Huffman table (built on the host from a DHT table, uploaded once, cached by content).
+//   fast[i]: entry for the next kLutBits stream bits = i
+//     bits 0..4  : bits to consume (0 = slow path)
+//     bit  5     : value-complete (magnitude bits already included in the count)
+//     bits 8..15 : symbol (DC: size s; AC: run<<4 | size)
+//     bits 16..31: int16 coefficient value when value-complete
+//   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not
+//                < lim[l-1]) — the canonical DECODE procedure of JPEG Annex F.2.2.3
+//   base[l]    : valptr[l] - mincode[l]
+struct alignas(16) HuffLut {
+    uint32_t fast[kLutSize];
+    uint32_t lim[20];
+    int32_t base[20];
+    uint8_t vals[256];
+};
+static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
+constexpr uint32_t kLutFlagComplete = 32u;
+
+// Maximum Huffman tables a table set (one workgroup of the Huffman kernel) stages into LDS.
+constexpr int kSlotsPerSet = 6;
+
+// Per table set: which cached LUT each slot holds and which slot each component uses.
+struct TableSet {
+    int32_t lut[kSlotsPerSet];  // index into the LUT array (-1 = unused)
+    uint8_t dc_slot[4];
+    uint8_t ac_slot[4];
+};
+
+// Per image of a batch (device array, one entry per decodable image).
+struct alignas(16) ImgDesc {
+    uint64_t jpeg;         // device address of the file bytes
+    uint64_t rgb;          // device address of the H*W*3 uint8 output
+    uint32_t len;          // file length in bytes
+    uint32_t ecs_off;      // first ECS byte
+    uint32_t width, height;
+    uint32_t mcux, mcuy;
+    uint32_t ncomp, hmax, vmax, bpm;  // bpm = blocks per MCU
+    uint32_t block_pattern;           // component of MCU block b at bits 2b..2b+1
+    uint32_t restart_interval;        // MCUs per interval (0 = single segment)
+    uint32_t seg_base, nseg;          // this image's segments in the global segment list
+    uint64_t block_base;              // first global block index
+    uint32_t tableset;
+    uint32_t tile_mcus;               // MCUs per IDCT/colour tile (one MCU row slice)
+    uint32_t tiles_x;                 // tiles per MCU row
+    uint32_t chunk_base, nchunks;     // RST-scan chunks of this image
+    uint32_t status_slot;             // index into the per-image status array
+    uint8_t h[4], v[4];
+    uint16_t qslot[4];                // quant table of each component (index into batch Q array)
+    uint8_t comp_block0[4];           // first MCU block of each component
+    uint32_t pad[1];
+};
+
+// Per-block result of the Huffman kernel (sparse coefficient representation):
+//   x = index of the block's first AC entry in the entry array
+//   y = (number of AC entries << 16) | (uint16)DC   (DC already un-predicted, still quantised)
+// AC entry = (int16 value << 16) | zig-zag index (1..63).
+struct BlockInfo {
+    uint32_t entry_start;
+    uint32_t cnt_dc;
+};
+
+constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
+
+// RST scan geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
+constexpr int kScanThreads = 256;
+constexpr int kScanBytesPerThread = 64;
+constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
+constexpr int kScanCap = kScanChunk / 2;  // a marker takes 2 bytes: a chunk cannot hold more
+
+constexpr int kHuffThreads = 256;
+constexpr int kIdctThreads = 256;
+constexpr int kTileMaxBlocks = 48;  // blocks staged in LDS per IDCT/colour tile
+
+// Per-image status bits written by kernels (atomicOr); host maps them to jd_status.
+constexpr uint32_t kStCorrupt = 1u;      // bad code / overrun / DC range
+constexpr uint32_t kStRstMissing = 2u;   // fewer RST markers than intervals
+constexpr uint32_t kStRstOrder = 4u;     // RSTn numbering wrong
+
+// Kernel launch wrappers (jd_kernels.hip).
+struct BatchDev {
+    const ImgDesc* imgs;
+    uint32_t nimg;
+    const HuffLut* luts;
+    const TableSet* tablesets;
+    const uint16_t* qtabs;        // 64 x uint16 per quant table, zig-zag order
+    // segments
+    const uint32_t* seg_img;      // image of each segment (kInvalidImage = padding)
+    uint32_t* seg_start;          // first byte (relative to the file) of each segment
+    const uint32_t* seg_entry;    // first AC-entry slot of each segment
+    uint32_t nseg;                // including padding, multiple of kHuffThreads
+    const uint32_t* wg_tableset;  // table set of each Huffman workgroup
+    // rst scan
+    const uint32_t* rst_imgs;     // images with restart intervals
+    uint32_t nrst;
+    uint32_t max_chunks;
+    uint32_t* chunk_cnt;
+    uint32_t* chunk_pos;          // kScanCap per chunk
+    uint32_t* ecs_end;            // per image: first terminating marker position
+    // outputs
+    BlockInfo* blocks;
+    uint32_t* entries;
+    uint32_t* status;             // per image
+    unsigned long long* counters; // [0] AC entries written, [1] blocks written
+    uint32_t max_tiles_x;
+    uint32_t max_tile_rows;
+};
+
+}  // namespace jd

@@ -1,0 +1,213 @@
+// jd_parse.cpp — host-side marker parser and Huffman LUT builder.
+//
+// The reference walks a fixed marker sequence (APP0, DQT, DQT, SOF0, 4x DHT, SOS:
+// cpp-decoder/src/parser.cpp:31-101) and maps "first DQT -> Y, second -> chroma" and DHT ids
+// 0x00/0x01/0x10/0x11 positionally.  For the files the reference accepts that is the same as
+// honouring the SOF Tq and SOS Td/Ta selectors, which is what this parser does; it also accepts
+// any marker order, multi-table segments, DRI, fill bytes and 1-component frames, and rejects
+// what the GPU path does not implement with JD_ERR_UNSUPPORTED instead of decoding garbage.
+#include "jd_parse.hpp"
+
+#include <string.h>
+
+namespace jd {
+
+static inline uint32_t be16(const uint8_t* p) { return (uint32_t(p[0]) << 8) | p[1]; }
+
+jd_status parse_jpeg(const uint8_t* d, size_t n, ParsedJpeg* out) {
+    *out = ParsedJpeg();
+    if (!d || n < 4) return JD_ERR_INVALID_ARG;
+    if (d[0] != 0xFF || d[1] != 0xD8) return JD_ERR_CORRUPT;
+    jd_header& h = out->hdr;
+    size_t p = 2;
+    bool have_sof = false;
+    for (;;) {
+        if (p + 2 > n) return JD_ERR_TRUNCATED;
+        if (d[p] != 0xFF) return JD_ERR_CORRUPT;
+        while (p + 1 < n && d[p + 1] == 0xFF) p++;
+        if (p + 2 > n) return JD_ERR_TRUNCATED;
+        const uint8_t m = d[p + 1];
+        p += 2;
+        if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;  // standalone markers
+        if (m == 0xD9) return JD_ERR_CORRUPT;                               // EOI before SOS
+        if (p + 2 > n) return JD_ERR_TRUNCATED;
+        const size_t L = be16(d + p);
+        if (L < 2 || p + L > n) return JD_ERR_TRUNCATED;
+        const uint8_t* s = d + p + 2;
+        const size_t sl = L - 2;
+        switch (m) {
+            case 0xC0:
+            case 0xC1: {  // baseline / extended sequential, Huffman
+                if (sl < 6) return JD_ERR_CORRUPT;
+                if (s[0] != 8) return JD_ERR_UNSUPPORTED;  // 12-bit samples
+                h.height = int(be16(s + 1));
+                h.width = int(be16(s + 3));
+                const int nc = s[5];
+                if (nc != 1 && nc != 3) return JD_ERR_UNSUPPORTED;  // CMYK / 2-component
+                if (sl < 6 + 3 * size_t(nc)) return JD_ERR_CORRUPT;
+                if (h.width == 0 || h.height == 0) return JD_ERR_UNSUPPORTED;  // DNL
+                h.ncomp = nc;
+                for (int c = 0; c < nc; c++) {
+                    out->cid[c] = s[6 + 3 * c];
+                    h.h[c] = s[7 + 3 * c] >> 4;
+                    h.v[c] = s[7 + 3 * c] & 15;
+                    h.tq[c] = s[8 + 3 * c];
+                    if (h.h[c] < 1 || h.h[c] > 4 || h.v[c] < 1 || h.v[c] > 4 || h.tq[c] > 3)
+                        return JD_ERR_CORRUPT;
+                }
+                have_sof = true;
+                break;
+            }
+            case 0xC4: {  // DHT
+                size_t q = 0;
+                while (q < sl) {
+                    if (q + 17 > sl) return JD_ERR_CORRUPT;
+                    const int tc = s[q] >> 4, th = s[q] & 15;
+                    if (tc > 1 || th > 3) return JD_ERR_CORRUPT;
+                    HuffSpec& t = tc ? out->ac[th] : out->dc[th];
+                    t = HuffSpec();
+                    int tot = 0;
+                    for (int l = 1; l <= 16; l++) tot += (t.counts[l] = s[q + l]);
+                    if (tot > 256 || q + 17 + tot > sl) return JD_ERR_CORRUPT;
+                    memcpy(t.vals, s + q + 17, size_t(tot));
+                    t.nvals = tot;
+                    t.present = true;
+                    q += 17 + size_t(tot);
+                }
+                break;
+            }
+            case 0xDB: {  // DQT
+                size_t q = 0;
+                while (q < sl) {
+                    const int pq = s[q] >> 4, tq = s[q] & 15;
+                    if (pq > 1 || tq > 3) return JD_ERR_CORRUPT;
+                    if (q + 1 + 64 * size_t(pq + 1) > sl) return JD_ERR_CORRUPT;
+                    for (int k = 0; k < 64; k++)
+                        out->q[tq][k] = uint16_t(pq ? be16(s + q + 1 + 2 * k) : s[q + 1 + k]);
+                    out->qp[tq] = true;
+                    q += 1 + 64 * size_t(pq + 1);
+                }
+                break;
+            }
+            case 0xDD:  // DRI
+                if (sl < 2) return JD_ERR_CORRUPT;
+                h.restart_interval = int(be16(s));
+                break;
+            case 0xDA: {  // SOS
+                if (!have_sof || sl < 1) return JD_ERR_CORRUPT;
+                const int ns = s[0];
+                if (sl < 4 + 2 * size_t(ns)) return JD_ERR_CORRUPT;
+                if (ns != h.ncomp) return JD_ERR_UNSUPPORTED;  // multi-scan sequential
+                for (int i = 0; i < ns; i++) {
+                    if (s[1 + 2 * i] != out->cid[i]) return JD_ERR_UNSUPPORTED;
+                    out->td[i] = s[2 + 2 * i] >> 4;
+                    out->ta[i] = s[2 + 2 * i] & 15;
+                    if (out->td[i] > 3 || out->ta[i] > 3) return JD_ERR_CORRUPT;
+                    if (!out->dc[out->td[i]].present || !out->ac[out->ta[i]].present)
+                        return JD_ERR_CORRUPT;
+                    if (!out->qp[h.tq[i]]) return JD_ERR_CORRUPT;
+                }
+                if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0)
+                    return JD_ERR_UNSUPPORTED;  // spectral selection / approximation
+                h.ecs_offset = p + L;
+                goto done;
+            }
+            default:
+                if (m >= 0xC2 && m <= 0xCF && m != 0xC8 && m != 0xCC)
+                    return JD_ERR_UNSUPPORTED;  // progressive, lossless, arithmetic
+                break;                          // APPn, COM, DNL, ...: skipped by length
+        }
+        p += L;
+    }
+done:
+    if (h.ncomp == 1) {
+        h.h[0] = h.v[0] = 1;  // non-interleaved scan: MCU = one block
+        h.hmax = h.vmax = 1;
+    } else {
+        h.hmax = h.vmax = 1;
+        for (int c = 0; c < h.ncomp; c++) {
+            if (h.h[c] > h.hmax) h.hmax = h.h[c];
+            if (h.v[c] > h.vmax) h.vmax = h.v[c];
+        }
+        for (int c = 0; c < h.ncomp; c++)
+            if (h.hmax % h.h[c] || h.vmax % h.v[c]) return JD_ERR_UNSUPPORTED;
+    }
+    h.mcux = (h.width + 8 * h.hmax - 1) / (8 * h.hmax);
+    h.mcuy = (h.height + 8 * h.vmax - 1) / (8 * h.vmax);
+    h.blocks_per_mcu = 0;
+    for (int c = 0; c < h.ncomp; c++) h.blocks_per_mcu += h.h[c] * h.v[c];
+    if (h.blocks_per_mcu > 10) return JD_ERR_UNSUPPORTED;
+    if (h.ncomp == 1) {
+        h.subsampling = JD_SS_GRAY;
+    } else if (h.h[1] == h.h[2] && h.v[1] == h.v[2] && h.h[1] == 1 && h.v[1] == 1) {
+        if (h.hmax == 1 && h.vmax == 1) h.subsampling = JD_SS_444;
+        else if (h.hmax == 2 && h.vmax == 1) h.subsampling = JD_SS_422;
+        else if (h.hmax == 2 && h.vmax == 2) h.subsampling = JD_SS_420;
+        else if (h.hmax == 1 && h.vmax == 2) h.subsampling = JD_SS_440;
+        else h.subsampling = JD_SS_OTHER;
+    } else {
+        h.subsampling = JD_SS_OTHER;
+    }
+    return JD_OK;
+}
+
+static inline int extend(int v, int s) {
+    if (s == 0) return 0;
+    const int l = 1 << (s - 1);
+    return v >= l ? v : v - ((l << 1) - 1);
+}
+
+bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
+    memset(lut, 0, sizeof(*lut));
+    int code = 0, k = 0;
+    int codes[256];
+    int lens[256];
+    for (int l = 1; l <= 16; l++) {
+        lut->base[l] = k - code;  // valptr[l] - mincode[l]
+        for (int i = 0; i < h.counts[l]; i++) {
+            if (k >= 256) return false;
+            codes[k] = code++;
+            lens[k] = l;
+            k++;
+        }
+        if (code > (1 << l)) return false;  // over-subscribed
+        lut->lim[l] = uint32_t(code) << (16 - l);
+        code <<= 1;
+    }
+    lut->lim[17] = 0xFFFFFFFFu;  // sentinel: unmatched 16-bit prefix -> corrupt
+    for (int i = 0; i < h.nvals; i++) lut->vals[i] = h.vals[i];
+    for (int i = 0; i < k; i++) {
+        const int l = lens[i];
+        if (l > kLutBits) continue;
+        const int sym = h.vals[i];
+        const int s = is_dc ? sym : (sym & 15);
+        const int shift = kLutBits - l;
+        const int first = codes[i] << shift, last = ((codes[i] + 1) << shift) - 1;
+        for (int idx = first; idx <= last; idx++) {
+            uint32_t e;
+            if (s <= 16 && l + s <= kLutBits) {
+                const int bits = (idx >> (kLutBits - l - s)) & ((1 << s) - 1);
+                const int val = extend(bits, s);
+                e = uint32_t(l + s) | kLutFlagComplete | (uint32_t(sym) << 8) |
+                    (uint32_t(uint16_t(int16_t(val))) << 16);
+            } else {
+                e = uint32_t(l) | (uint32_t(sym) << 8);
+            }
+            lut->fast[idx] = e;
+        }
+    }
+    return true;
+}
+
+uint64_t hash_huff(const HuffSpec& h, bool is_dc) {
+    uint64_t x = 1469598103934665603ull ^ (is_dc ? 0x9e3779b97f4a7c15ull : 0);
+    auto mix = [&](uint8_t b) {
+        x ^= b;
+        x *= 1099511628211ull;
+    };
+    for (int l = 1; l <= 16; l++) mix(h.counts[l]);
+    for (int i = 0; i < h.nvals; i++) mix(h.vals[i]);
+    return x;
+}
+
+}  // namespace jd

@@ -1,0 +1,686 @@
+// jd_runtime.cpp — context, batch planning and the C ABI of libjdamd.so.
+//
+// A batch flows through: host header parse (C++ threads) -> plan (tables de-duplicated, segments,
+// tiles, offsets) -> one H2D copy of the plan -> four kernels on the context stream -> per-image
+// status D2H.  Device buffers are grow-only pools owned by the context, so steady-state batches do
+// no allocation.  Replaces the reference's per-image extract()/allocate()/clean() cycle
+// (cuda-decoder/benchmark_thoughput/benchmark.cu:49-93) which cudaMalloc'ed every image.
+#include <hip/hip_runtime_api.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <array>
+#include <map>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "jd.h"
+#include "jd_internal.hpp"
+#include "jd_kernels.hpp"
+#include "jd_parse.hpp"
+#include "jd_test.h"
+
+using namespace jd;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct CachedLut {
+    HuffSpec spec;
+    bool is_dc;
+};
+
+}  // namespace
+
+struct jd_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    unsigned flags = 0;
+    int parse_threads = 1;
+    std::string last_error;
+
+    // Huffman LUT cache (content-addressed, grows across calls)
+    std::unordered_multimap<uint64_t, int> lut_by_hash;
+    std::vector<CachedLut> lut_specs;
+    std::vector<HuffLut> lut_host;
+    DevBuf lut_dev;
+    size_t lut_dev_count = 0;
+
+    // pools
+    DevBuf plan, chunk_pos, blocks, entries, input, output;
+    PinBuf plan_host, input_host;
+
+    hipEvent_t ev[JD_NUM_KERNELS][2] = {};
+    jd_stats stats{};
+
+    std::vector<ParsedJpeg> parsed;
+    std::vector<jd_status> pst;
+};
+
+namespace {
+
+jd_status hip_fail(jd_ctx* ctx, hipError_t e, const char* what) {
+    if (ctx) ctx->last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return JD_ERR_HIP;
+}
+
+#define HIPCHK(ctx, call)                                         \
+    do {                                                          \
+        hipError_t e_ = (call);                                   \
+        if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);  \
+    } while (0)
+
+hipError_t ensure_dev(DevBuf& b, size_t bytes) {
+    if (bytes <= b.cap) return hipSuccess;
+    const size_t n = std::max(bytes, b.cap + b.cap / 2);
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    hipError_t e = hipMalloc(&b.p, n);
+    if (e == hipSuccess) b.cap = n;
+    return e;
+}
+
+hipError_t ensure_pin(PinBuf& b, size_t bytes) {
+    if (bytes <= b.cap) return hipSuccess;
+    const size_t n = std::max(bytes, b.cap + b.cap / 2);
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    hipError_t e = hipHostMalloc(&b.p, n, hipHostMallocDefault);
+    if (e == hipSuccess) b.cap = n;
+    return e;
+}
+
+int lut_id(jd_ctx* ctx, const HuffSpec& s, bool is_dc) {
+    const uint64_t h = hash_huff(s, is_dc);
+    auto range = ctx->lut_by_hash.equal_range(h);
+    for (auto it = range.first; it != range.second; ++it) {
+        const CachedLut& c = ctx->lut_specs[size_t(it->second)];
+        if (c.is_dc == is_dc && c.spec.nvals == s.nvals && !memcmp(c.spec.counts, s.counts, 17) &&
+            !memcmp(c.spec.vals, s.vals, size_t(s.nvals)))
+            return it->second;
+    }
+    HuffLut lut;
+    if (!build_lut(s, is_dc, &lut)) return -1;
+    const int id = int(ctx->lut_host.size());
+    ctx->lut_host.push_back(lut);
+    ctx->lut_specs.push_back(CachedLut{s, is_dc});
+    ctx->lut_by_hash.emplace(h, id);
+    return id;
+}
+
+jd_status sync_luts(jd_ctx* ctx) {
+    if (ctx->lut_dev_count == ctx->lut_host.size()) return JD_OK;
+    HIPCHK(ctx, ensure_dev(ctx->lut_dev, ctx->lut_host.size() * sizeof(HuffLut)));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->lut_dev.p, ctx->lut_host.data(), ctx->lut_host.size() * sizeof(HuffLut),
+                               hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->lut_dev_count = ctx->lut_host.size();
+    return JD_OK;
+}
+
+void parse_all(jd_ctx* ctx, const jd_item* items, int n) {
+    ctx->parsed.resize(size_t(n));
+    ctx->pst.resize(size_t(n));
+    auto work = [&](int lo, int hi) {
+        for (int i = lo; i < hi; i++) ctx->pst[i] = parse_jpeg(items[i].jpeg, items[i].len, &ctx->parsed[i]);
+    };
+    int nt = std::min(ctx->parse_threads, std::max(1, n / 32));
+    if (nt <= 1) {
+        work(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int per = (n + nt - 1) / nt;
+    for (int t = 0; t < nt; t++) {
+        const int lo = t * per, hi = std::min(n, lo + per);
+        if (lo < hi) th.emplace_back(work, lo, hi);
+    }
+    for (auto& t : th) t.join();
+}
+
+struct Plan {
+    std::vector<ImgDesc> imgs;
+    std::vector<int> item_of_img;
+    std::vector<TableSet> tablesets;
+    std::vector<uint16_t> qtabs;
+    std::vector<uint32_t> seg_img, seg_start, seg_entry, wg_tableset, rst_imgs, ecs_end;
+    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0;
+    uint64_t total_blocks = 0, total_entry_cap = 0;
+    double pixels = 0, ecs_bytes = 0, rst_bytes = 0;
+};
+
+// Largest item prefix [lo, hi) whose sparse-coefficient capacity fits 32-bit entry indices.
+int batch_split(jd_ctx* ctx, int lo, int n) {
+    uint64_t cap = 0;
+    int hi = lo;
+    for (; hi < n; hi++) {
+        if (ctx->pst[hi] != JD_OK) continue;
+        const jd_header& h = ctx->parsed[hi].hdr;
+        const uint64_t blocks = uint64_t(h.mcux) * h.mcuy * h.blocks_per_mcu;
+        if (hi > lo && cap + blocks * 63 > 0xF0000000ull) break;
+        cap += blocks * 63;
+    }
+    return hi;
+}
+
+jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const std::vector<uint64_t>& dev_addr,
+                     const std::vector<uint64_t>& out_addr, Plan& P) {
+    std::map<std::array<int, 7>, int> ts_index;
+    std::map<std::array<uint16_t, 64>, int> q_index;
+    std::vector<int> ts_of_img;
+    for (int it = lo; it < hi; it++) {
+        if (ctx->pst[it] != JD_OK) continue;
+        const ParsedJpeg& pj = ctx->parsed[it];
+        const jd_header& h = pj.hdr;
+        std::array<int, 7> key{};
+        key[0] = h.ncomp;
+        bool ok = true;
+        for (int c = 0; c < h.ncomp; c++) {
+            key[1 + c] = lut_id(ctx, pj.dc[pj.td[c]], true);
+            key[4 + c] = lut_id(ctx, pj.ac[pj.ta[c]], false);
+            if (key[1 + c] < 0 || key[4 + c] < 0) ok = false;
+        }
+        if (!ok) {
+            ctx->pst[it] = JD_ERR_CORRUPT;
+            continue;
+        }
+        auto f = ts_index.find(key);
+        int ts;
+        if (f == ts_index.end()) {
+            TableSet t;
+            for (int s = 0; s < kSlotsPerSet; s++) t.lut[s] = -1;
+            memset(t.dc_slot, 0, sizeof(t.dc_slot));
+            memset(t.ac_slot, 0, sizeof(t.ac_slot));
+            int nslot = 0;
+            auto slot_of = [&](int id) {
+                for (int s = 0; s < nslot; s++)
+                    if (t.lut[s] == id) return s;
+                t.lut[nslot] = id;
+                return nslot++;
+            };
+            for (int c = 0; c < h.ncomp; c++) {
+                t.dc_slot[c] = uint8_t(slot_of(key[1 + c]));
+                t.ac_slot[c] = uint8_t(slot_of(key[4 + c]));
+            }
+            ts = int(P.tablesets.size());
+            P.tablesets.push_back(t);
+            ts_index.emplace(key, ts);
+        } else {
+            ts = f->second;
+        }
+        ImgDesc d;
+        memset(&d, 0, sizeof(d));
+        d.jpeg = dev_addr[it];
+        d.rgb = out_addr[it];
+        d.len = uint32_t(items[it].len);
+        d.ecs_off = uint32_t(h.ecs_offset);
+        d.width = uint32_t(h.width);
+        d.height = uint32_t(h.height);
+        d.mcux = uint32_t(h.mcux);
+        d.mcuy = uint32_t(h.mcuy);
+        d.ncomp = uint32_t(h.ncomp);
+        d.hmax = uint32_t(h.hmax);
+        d.vmax = uint32_t(h.vmax);
+        d.bpm = uint32_t(h.blocks_per_mcu);
+        uint32_t pat = 0, b = 0;
+        for (int c = 0; c < h.ncomp; c++) {
+            d.h[c] = uint8_t(h.h[c]);
+            d.v[c] = uint8_t(h.v[c]);
+            d.comp_block0[c] = uint8_t(b);
+            for (int j = 0; j < h.h[c] * h.v[c]; j++, b++) pat |= uint32_t(c) << (2 * b);
+            std::array<uint16_t, 64> q;
+            memcpy(q.data(), pj.q[h.tq[c]], sizeof(q));
+            auto fq = q_index.find(q);
+            int qi;
+            if (fq == q_index.end()) {
+                qi = int(P.qtabs.size() / 64);
+                P.qtabs.insert(P.qtabs.end(), q.begin(), q.end());
+                q_index.emplace(q, qi);
+            } else {
+                qi = fq->second;
+            }
+            d.qslot[c] = uint16_t(qi);
+        }
+        d.block_pattern = pat;
+        d.restart_interval = uint32_t(h.restart_interval);
+        const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
+        d.nseg = h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
+        d.block_base = P.total_blocks;
+        P.total_blocks += nmcu * uint64_t(h.blocks_per_mcu);
+        d.tableset = uint32_t(ts);
+        d.tile_mcus = std::max(1u, std::min(uint32_t(kTileMaxBlocks) / d.bpm, d.mcux));
+        d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
+        P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.mcuy);
+        d.status_slot = uint32_t(P.imgs.size());
+        if (h.restart_interval && d.nseg > 1) {
+            const uint64_t a0 = (d.jpeg + d.ecs_off) & ~uint64_t(15);
+            const uint64_t span = d.jpeg + d.len - a0;
+            d.nchunks = uint32_t((span + kScanChunk - 1) / kScanChunk);
+            d.chunk_base = P.total_chunks;
+            P.total_chunks += d.nchunks;
+            P.max_chunks = std::max(P.max_chunks, d.nchunks);
+            P.rst_imgs.push_back(uint32_t(P.imgs.size()));
+            P.rst_bytes += double(d.len - d.ecs_off);
+        }
+        P.pixels += double(h.width) * h.height;
+        P.ecs_bytes += double(d.len - d.ecs_off);
+        P.imgs.push_back(d);
+        P.item_of_img.push_back(it);
+        P.ecs_end.push_back(d.len);
+        ts_of_img.push_back(ts);
+    }
+    // segments grouped by table set; each Huffman workgroup sees exactly one table set
+    std::vector<uint32_t> order(P.imgs.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = uint32_t(i);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return ts_of_img[a] < ts_of_img[b]; });
+    uint64_t entry_cursor = 0;
+    for (size_t oi = 0; oi < order.size();) {
+        const int ts = ts_of_img[order[oi]];
+        for (; oi < order.size() && ts_of_img[order[oi]] == ts; oi++) {
+            ImgDesc& d = P.imgs[order[oi]];
+            d.seg_base = uint32_t(P.seg_img.size());
+            const uint32_t nmcu = d.mcux * d.mcuy;
+            for (uint32_t k = 0; k < d.nseg; k++) {
+                const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
+                const uint32_t m1 = d.restart_interval ? std::min(m0 + d.restart_interval, nmcu) : nmcu;
+                P.seg_img.push_back(order[oi]);
+                P.seg_start.push_back(k == 0 ? d.ecs_off : 0u);
+                P.seg_entry.push_back(uint32_t(entry_cursor));
+                entry_cursor += uint64_t(m1 - m0) * d.bpm * 63;
+            }
+        }
+        while (P.seg_img.size() % kHuffThreads) {
+            P.seg_img.push_back(kInvalidImage);
+            P.seg_start.push_back(0);
+            P.seg_entry.push_back(0);
+        }
+        while (P.wg_tableset.size() < P.seg_img.size() / kHuffThreads) P.wg_tableset.push_back(uint32_t(ts));
+    }
+    if (entry_cursor > 0xFFFFFFFFull) return JD_ERR_CAPACITY;
+    P.total_entry_cap = entry_cursor;
+    return JD_OK;
+}
+
+template <typename T>
+size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
+    const size_t off = align_up(blob.size(), 256);
+    blob.resize(off + std::max<size_t>(v.size() * sizeof(T), 16));
+    if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result* results, int rgb_on_device,
+                    hipStream_t s) {
+    // 1. inputs and outputs on the device
+    std::vector<uint64_t> dev_addr(size_t(hi), 0), out_addr(size_t(hi), 0);
+    size_t in_bytes = 0, out_bytes = 0;
+    for (int i = lo; i < hi; i++) {
+        if (ctx->pst[i] != JD_OK) continue;
+        if (!items[i].jpeg_dev) in_bytes += align_up(items[i].len + 64, 256);
+        if (!rgb_on_device) out_bytes += align_up(size_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3, 256);
+    }
+    if (in_bytes) {
+        HIPCHK(ctx, ensure_dev(ctx->input, in_bytes));
+        HIPCHK(ctx, ensure_pin(ctx->input_host, in_bytes));
+        size_t off = 0;
+        for (int i = lo; i < hi; i++) {
+            if (ctx->pst[i] != JD_OK || items[i].jpeg_dev) continue;
+            memcpy(static_cast<uint8_t*>(ctx->input_host.p) + off, items[i].jpeg, items[i].len);
+            dev_addr[i] = reinterpret_cast<uint64_t>(ctx->input.p) + off;
+            off += align_up(items[i].len + 64, 256);
+        }
+        HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, ctx->input_host.p, in_bytes, hipMemcpyHostToDevice, s));
+    }
+    for (int i = lo; i < hi; i++)
+        if (ctx->pst[i] == JD_OK && items[i].jpeg_dev) dev_addr[i] = reinterpret_cast<uint64_t>(items[i].jpeg_dev);
+    if (out_bytes) HIPCHK(ctx, ensure_dev(ctx->output, out_bytes));
+    {
+        size_t off = 0;
+        for (int i = lo; i < hi; i++) {
+            if (ctx->pst[i] != JD_OK) continue;
+            if (rgb_on_device) {
+                out_addr[i] = reinterpret_cast<uint64_t>(items[i].rgb);
+            } else {
+                out_addr[i] = reinterpret_cast<uint64_t>(ctx->output.p) + off;
+                off += align_up(size_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3, 256);
+            }
+        }
+    }
+
+    // 2. plan
+    Plan P;
+    jd_status st = build_plan(ctx, items, lo, hi, dev_addr, out_addr, P);
+    if (st != JD_OK) return st;
+    st = sync_luts(ctx);
+    if (st != JD_OK) return st;
+    const uint32_t nimg = uint32_t(P.imgs.size());
+    if (nimg) {
+        std::vector<uint8_t> blob;
+        const size_t o_imgs = put(blob, P.imgs);
+        const size_t o_ts = put(blob, P.tablesets);
+        const size_t o_q = put(blob, P.qtabs);
+        const size_t o_segimg = put(blob, P.seg_img);
+        const size_t o_segstart = put(blob, P.seg_start);
+        const size_t o_segent = put(blob, P.seg_entry);
+        const size_t o_wgts = put(blob, P.wg_tableset);
+        const size_t o_rst = put(blob, P.rst_imgs);
+        const size_t o_cc = put(blob, std::vector<uint32_t>(P.total_chunks, 0));
+        const size_t o_end = put(blob, P.ecs_end);
+        const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
+        const size_t o_ctr = put(blob, std::vector<unsigned long long>(2, 0));
+        HIPCHK(ctx, ensure_dev(ctx->plan, blob.size()));
+        HIPCHK(ctx, ensure_pin(ctx->plan_host, blob.size()));
+        memcpy(ctx->plan_host.p, blob.data(), blob.size());
+        HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, ctx->plan_host.p, blob.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, ensure_dev(ctx->chunk_pos, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * 4)));
+        HIPCHK(ctx, ensure_dev(ctx->blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
+        HIPCHK(ctx, ensure_dev(ctx->entries, std::max<size_t>(16, P.total_entry_cap * 4)));
+
+        uint8_t* base = static_cast<uint8_t*>(ctx->plan.p);
+        BatchDev b;
+        b.imgs = reinterpret_cast<const ImgDesc*>(base + o_imgs);
+        b.nimg = nimg;
+        b.luts = static_cast<const HuffLut*>(ctx->lut_dev.p);
+        b.tablesets = reinterpret_cast<const TableSet*>(base + o_ts);
+        b.qtabs = reinterpret_cast<const uint16_t*>(base + o_q);
+        b.seg_img = reinterpret_cast<const uint32_t*>(base + o_segimg);
+        b.seg_start = reinterpret_cast<uint32_t*>(base + o_segstart);
+        b.seg_entry = reinterpret_cast<const uint32_t*>(base + o_segent);
+        b.nseg = uint32_t(P.seg_img.size());
+        b.wg_tableset = reinterpret_cast<const uint32_t*>(base + o_wgts);
+        b.rst_imgs = reinterpret_cast<const uint32_t*>(base + o_rst);
+        b.nrst = uint32_t(P.rst_imgs.size());
+        b.max_chunks = P.max_chunks;
+        b.chunk_cnt = reinterpret_cast<uint32_t*>(base + o_cc);
+        b.chunk_pos = static_cast<uint32_t*>(ctx->chunk_pos.p);
+        b.ecs_end = reinterpret_cast<uint32_t*>(base + o_end);
+        b.blocks = static_cast<BlockInfo*>(ctx->blocks.p);
+        b.entries = static_cast<uint32_t*>(ctx->entries.p);
+        b.status = reinterpret_cast<uint32_t*>(base + o_status);
+        b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
+        b.max_tiles_x = P.max_tiles;
+        b.max_tile_rows = 0;
+
+        const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
+        hipError_t (*launch[JD_NUM_KERNELS])(const BatchDev&, hipStream_t) = {launch_rst_scan, launch_rst_index,
+                                                                             launch_huffman, launch_idct_color};
+        const bool active[JD_NUM_KERNELS] = {b.nrst > 0, b.nrst > 0, true, true};
+        for (int k = 0; k < JD_NUM_KERNELS; k++) {
+            if (!active[k]) continue;
+            if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][0], s));
+            HIPCHK(ctx, launch[k](b, s));
+            if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][1], s));
+        }
+        std::vector<uint32_t> status(nimg);
+        unsigned long long ctr[2] = {0, 0};
+        HIPCHK(ctx, hipMemcpyAsync(status.data(), b.status, nimg * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctr, b.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        for (uint32_t i = 0; i < nimg; i++)
+            if (status[i]) ctx->pst[P.item_of_img[i]] = JD_ERR_CORRUPT;
+
+        jd_stats& S = ctx->stats;
+        const double entries = double(ctr[0]);
+        const double blocks = double(P.total_blocks);
+        const double bytes[JD_NUM_KERNELS] = {P.rst_bytes, double(P.total_chunks) * 4 + double(P.seg_img.size()) * 4,
+                                              P.ecs_bytes + blocks * 8 + entries * 4,
+                                              blocks * 8 + entries * 4 + P.pixels * 3};
+        for (int k = 0; k < JD_NUM_KERNELS; k++) {
+            if (!active[k]) continue;
+            S.launches[k]++;
+            S.bytes[k] += bytes[k];
+            if (timing) {
+                float ms = 0;
+                HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev[k][0], ctx->ev[k][1]));
+                S.total_ms[k] += ms;
+            }
+        }
+        S.batches += 1;
+        S.images += nimg;
+        S.pixels += P.pixels;
+        S.ecs_bytes += P.ecs_bytes;
+        S.blocks += blocks;
+        S.segments += double(P.seg_img.size());
+    }
+
+    // 3. results (and host copies when the caller asked for host output)
+    for (int i = lo; i < hi; i++) {
+        results[i].status = ctx->pst[i];
+        results[i].width = ctx->pst[i] == JD_OK || ctx->pst[i] == JD_ERR_CORRUPT ? ctx->parsed[i].hdr.width : 0;
+        results[i].height = ctx->pst[i] == JD_OK || ctx->pst[i] == JD_ERR_CORRUPT ? ctx->parsed[i].hdr.height : 0;
+        if (!rgb_on_device && out_addr[i] && items[i].rgb) {
+            const size_t n = size_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3;
+            HIPCHK(ctx, hipMemcpyAsync(items[i].rgb, reinterpret_cast<void*>(out_addr[i]), n, hipMemcpyDeviceToHost, s));
+        }
+    }
+    if (!rgb_on_device) HIPCHK(ctx, hipStreamSynchronize(s));
+    return JD_OK;
+}
+
+}  // namespace
+
+// ============================================================================================
+// C ABI
+// ============================================================================================
+extern "C" {
+
+int jd_abi_version(void) { return JD_ABI_VERSION; }
+
+const char* jd_status_str(jd_status st) {
+    switch (st) {
+        case JD_OK: return "ok";
+        case JD_ERR_INVALID_ARG: return "invalid argument";
+        case JD_ERR_CORRUPT: return "corrupt stream";
+        case JD_ERR_UNSUPPORTED: return "unsupported JPEG variant";
+        case JD_ERR_TRUNCATED: return "truncated file";
+        case JD_ERR_HIP: return "HIP runtime error";
+        case JD_ERR_NOMEM: return "out of memory";
+        case JD_ERR_CAPACITY: return "batch exceeds capacity";
+        case JD_ERR_IO: return "I/O error";
+    }
+    return "unknown status";
+}
+
+const char* jd_kernel_name(int k) {
+    static const char* names[JD_NUM_KERNELS] = {"k_rst_scan", "k_rst_index", "k_huffman", "k_idct_color"};
+    return (k >= 0 && k < JD_NUM_KERNELS) ? names[k] : "?";
+}
+
+jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
+    if (!out) return JD_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || hip_device < 0 || hip_device >= ndev) return JD_ERR_INVALID_ARG;
+    jd_ctx* ctx = new jd_ctx();
+    ctx->device = hip_device;
+    ctx->flags = opts ? opts->flags : 0u;
+    int pt = opts ? opts->parse_threads : 0;
+    if (pt <= 0) pt = int(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+    ctx->parse_threads = pt;
+    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return JD_ERR_HIP;
+    }
+    for (int k = 0; k < JD_NUM_KERNELS; k++)
+        for (int j = 0; j < 2; j++)
+            if (hipEventCreate(&ctx->ev[k][j]) != hipSuccess) {
+                delete ctx;
+                return JD_ERR_HIP;
+            }
+    *out = ctx;
+    return JD_OK;
+}
+
+jd_status jd_ctx_destroy(jd_ctx* ctx) {
+    if (!ctx) return JD_ERR_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_pos, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output})
+        if (b->p) (void)hipFree(b->p);
+    for (PinBuf* b : {&ctx->plan_host, &ctx->input_host})
+        if (b->p) (void)hipHostFree(b->p);
+    for (int k = 0; k < JD_NUM_KERNELS; k++)
+        for (int j = 0; j < 2; j++)
+            if (ctx->ev[k][j]) (void)hipEventDestroy(ctx->ev[k][j]);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return JD_OK;
+}
+
+jd_status jd_parse(const uint8_t* jpeg, size_t len, jd_header* hdr) {
+    if (!jpeg || !hdr) return JD_ERR_INVALID_ARG;
+    ParsedJpeg* p = new ParsedJpeg();
+    jd_status st = parse_jpeg(jpeg, len, p);
+    *hdr = p->hdr;
+    delete p;
+    return st;
+}
+
+jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results, int rgb_on_device,
+                          void* hip_stream) {
+    if (!ctx || n < 0 || (n > 0 && (!items || !results))) return JD_ERR_INVALID_ARG;
+    for (int i = 0; i < n; i++)
+        if (!items[i].jpeg || items[i].len > 0xFFFFFFF0ull) return JD_ERR_INVALID_ARG;
+    if (hipSetDevice(ctx->device) != hipSuccess) return JD_ERR_HIP;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    parse_all(ctx, items, n);
+    for (int lo = 0; lo < n;) {
+        const int hi = batch_split(ctx, lo, n);
+        jd_status st = run_batch(ctx, items, lo, hi, results, rgb_on_device, s);
+        if (st != JD_OK) return st;
+        lo = hi;
+    }
+    return JD_OK;
+}
+
+jd_status jd_decode(jd_ctx* ctx, const uint8_t* jpeg, size_t len, uint8_t* rgb, int rgb_on_device, int* width,
+                    int* height) {
+    if (!ctx || !jpeg || !rgb) return JD_ERR_INVALID_ARG;
+    jd_item it{jpeg, nullptr, len, rgb};
+    jd_result r{};
+    jd_status st = jd_decode_batch(ctx, &it, 1, &r, rgb_on_device, nullptr);
+    if (st != JD_OK) return st;
+    if (width) *width = r.width;
+    if (height) *height = r.height;
+    return jd_status(r.status);
+}
+
+jd_status jd_decode_file(jd_ctx* ctx, const char* path, uint8_t* rgb, size_t rgb_capacity, int rgb_on_device,
+                         int* width, int* height) {
+    if (!ctx || !path) return JD_ERR_INVALID_ARG;
+    FILE* f = fopen(path, "rb");
+    if (!f) return JD_ERR_IO;
+    std::vector<uint8_t> data;
+    uint8_t tmp[1 << 16];
+    size_t got;
+    while ((got = fread(tmp, 1, sizeof(tmp), f)) > 0) data.insert(data.end(), tmp, tmp + got);
+    fclose(f);
+    jd_header h;
+    jd_status st = jd_parse(data.data(), data.size(), &h);
+    if (st != JD_OK) return st;
+    if (width) *width = h.width;
+    if (height) *height = h.height;
+    if (!rgb) return JD_OK;  // header query
+    if (rgb_capacity < size_t(h.width) * h.height * 3) return JD_ERR_CAPACITY;
+    return jd_decode(ctx, data.data(), data.size(), rgb, rgb_on_device, width, height);
+}
+
+jd_status jd_write_array(const char* path, const uint8_t* rgb, int width, int height) {
+    if (!path || !rgb || width <= 0 || height <= 0) return JD_ERR_INVALID_ARG;
+    FILE* f = fopen(path, "wb");
+    if (!f) return JD_ERR_IO;
+    fprintf(f, "%d %d\n", height, width);  // parser.cpp:203
+    const size_t npx = size_t(width) * height;
+    std::string line;
+    line.reserve(npx * 4);
+    for (int c = 0; c < 3; c++) {  // parser.cpp:204-208: R, G, B planes
+        line.clear();
+        char buf[8];
+        for (size_t i = 0; i < npx; i++) {
+            int n = snprintf(buf, sizeof(buf), "%d ", rgb[i * 3 + c]);
+            line.append(buf, size_t(n));
+        }
+        if (c < 2) line.push_back('\n');
+        fwrite(line.data(), 1, line.size(), f);
+    }
+    fclose(f);
+    return JD_OK;
+}
+
+jd_status jd_device_alloc(jd_ctx* ctx, size_t bytes, void** dptr) {
+    if (!ctx || !dptr) return JD_ERR_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipMalloc(dptr, std::max<size_t>(bytes, 1)));
+    return JD_OK;
+}
+
+jd_status jd_device_free(jd_ctx* ctx, void* dptr) {
+    if (!ctx) return JD_ERR_INVALID_ARG;
+    if (dptr) HIPCHK(ctx, hipFree(dptr));
+    return JD_OK;
+}
+
+jd_status jd_memcpy_h2d(jd_ctx* ctx, void* dst, const void* src, size_t n) {
+    if (!ctx || (n && (!dst || !src))) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return JD_OK;
+}
+
+jd_status jd_memcpy_d2h(jd_ctx* ctx, void* dst, const void* src, size_t n) {
+    if (!ctx || (n && (!dst || !src))) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return JD_OK;
+}
+
+jd_status jd_synchronize(jd_ctx* ctx) {
+    if (!ctx) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return JD_OK;
+}
+
+jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out) {
+    if (!ctx || !out) return JD_ERR_INVALID_ARG;
+    *out = ctx->stats;
+    return JD_OK;
+}
+
+jd_status jd_reset_stats(jd_ctx* ctx) {
+    if (!ctx) return JD_ERR_INVALID_ARG;
+    ctx->stats = jd_stats{};
+    return JD_OK;
+}
+
+jd_status jd_test_idct(jd_ctx* ctx, const int32_t* in_dev, int32_t* out_dev, int nblocks) {
+    if (!ctx || !in_dev || !out_dev || nblocks < 0) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, launch_test_idct(in_dev, out_dev, nblocks, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return JD_OK;
+}
+
+jd_status jd_test_color(jd_ctx* ctx, const int32_t* ycc_dev, uint8_t* rgb_dev, int n) {
+    if (!ctx || !ycc_dev || !rgb_dev || n < 0) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, launch_test_color(ycc_dev, rgb_dev, n, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return JD_OK;
+}
+
+}  // extern "C"

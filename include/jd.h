@@ -1,0 +1,142 @@
+/*
+ * jd.h — C ABI of the MI355X-native batched JPEG decoder (libjdamd.so).
+ *
+ * This is the drop-in boundary for the reference's decode(file/bitstream) -> RGB path.  The
+ * reference exposes that path as C++ free functions plus two CUDA kernels
+ * (/root/reference/cuda-decoder/src/parser.h:49-55) and, on the CPU side, the class
+ * JPEGParser{ctor(path), extract(), decode(), write()} (/root/reference/cpp-decoder/src/parser.h:42-69).
+ * Each entry point below names the reference interface it replaces.  Everything is plain C:
+ * pointers, sizes, status codes; no exceptions cross this boundary and no torch types appear.
+ *
+ * Output format: interleaved uint8 RGB, H*W*3 bytes, row-major (the reference writes the same
+ * values as three int planes in a text `.array` file — jd_write_array reproduces that file).
+ *
+ * Threading: a jd_ctx belongs to one host thread and one HIP device; calls on one context are
+ * ordered on its stream.  jd_parse and jd_write_array are reentrant and context-free.
+ */
+#ifndef JD_H
+#define JD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JD_ABI_VERSION 1
+
+typedef enum jd_status {
+    JD_OK = 0,
+    JD_ERR_INVALID_ARG = 1, /* NULL pointer, bad size, bad device                             */
+    JD_ERR_CORRUPT = 2,     /* malformed stream (bad Huffman code, missing RSTn, overrun ...)   */
+    JD_ERR_UNSUPPORTED = 3, /* progressive / arithmetic / 12-bit / CMYK / multi-scan input      */
+    JD_ERR_TRUNCATED = 4,   /* file ends inside the headers                                     */
+    JD_ERR_HIP = 5,         /* a HIP runtime call failed (reference: checkCudaError throws,
+                               cuda-decoder/src/parser.cu:317-321)                              */
+    JD_ERR_NOMEM = 6,       /* device or host allocation failed                                 */
+    JD_ERR_CAPACITY = 7,    /* batch exceeds the context's limits                               */
+    JD_ERR_IO = 8           /* file could not be read / written                                 */
+} jd_status;
+
+typedef struct jd_ctx jd_ctx;
+
+/* jd_opts.flags */
+#define JD_FLAG_TIMING 1u /* record hipEvents around every kernel launch (jd_get_stats) */
+
+typedef struct jd_opts {
+    unsigned flags;
+    int parse_threads; /* host parse workers for jd_decode_batch; 0 = auto (hardware threads) */
+} jd_opts;
+
+/* Subsampling classes reported by jd_parse. */
+#define JD_SS_GRAY 0
+#define JD_SS_444 1
+#define JD_SS_422 2
+#define JD_SS_420 3
+#define JD_SS_440 4
+#define JD_SS_OTHER 5
+
+typedef struct jd_header {
+    int width, height, ncomp;
+    int h[4], v[4], tq[4];
+    int hmax, vmax, mcux, mcuy, blocks_per_mcu;
+    int restart_interval; /* MCUs per restart interval, 0 = none (DRI absent) */
+    int subsampling;      /* JD_SS_* */
+    uint64_t ecs_offset;  /* first byte of the entropy-coded segment */
+} jd_header;
+
+/* One batch item.  `jpeg` (host) is always required: headers are parsed on the host.
+ * `jpeg_dev` may point at a device copy of the same bytes (already resident in HBM); when NULL the
+ * library uploads the file itself.  `rgb` receives H*W*3 bytes; it is a device pointer when the
+ * batch call's rgb_on_device is non-zero, otherwise a host pointer. */
+typedef struct jd_item {
+    const uint8_t* jpeg;
+    const uint8_t* jpeg_dev;
+    size_t len;
+    uint8_t* rgb;
+} jd_item;
+
+typedef struct jd_result {
+    int status; /* jd_status of this image; a bad image never poisons the rest of the batch */
+    int width, height;
+} jd_result;
+
+/* Context: owns the device pools, stream, events and table caches.
+ * Replaces the reference's allocate() (cuda-decoder/src/parser.cu:324-358). */
+jd_status jd_ctx_create(jd_ctx** ctx, int hip_device, const jd_opts* opts);
+/* Replaces clean() (cuda-decoder/src/parser.cu:684-700). */
+jd_status jd_ctx_destroy(jd_ctx* ctx);
+
+/* Header parse only, host, reentrant.  Replaces the marker walk of extract()
+ * (cuda-decoder/src/parser.cu:360-471, cpp-decoder/src/parser.cpp:24-103). */
+jd_status jd_parse(const uint8_t* jpeg, size_t len, jd_header* hdr);
+
+/* decode(bitstream) -> RGB for one image.  Replaces extract()+decodeKernel<<<1,T>>>+write's D2H
+ * (cuda-decoder/main.cu:7-40, parser.cu:577-611) and JPEGParser::extract()+decode()
+ * (cpp-decoder/src/parser.cpp:24-195).  rgb must hold H*W*3 bytes. */
+jd_status jd_decode(jd_ctx* ctx, const uint8_t* jpeg, size_t len, uint8_t* rgb, int rgb_on_device,
+                    int* width, int* height);
+
+/* Same, reading the file.  Mirrors the CLI `decoder <jpeg>` (cpp-decoder/main.cpp:5-16). */
+jd_status jd_decode_file(jd_ctx* ctx, const char* path, uint8_t* rgb, size_t rgb_capacity,
+                         int rgb_on_device, int* width, int* height);
+
+/* Batched decode of independent images.  Replaces batchDecodeKernel<<<N,T>>>(DeviceData*)
+ * (cuda-decoder/src/parser.cu:663-682, driven by benchmark_thoughput/benchmark.cu:43-93).
+ * hip_stream: hipStream_t to order the work on, or NULL for the context's own stream.  The call
+ * returns after the batch completes; per-image status in results[i]. */
+jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
+                          int rgb_on_device, void* hip_stream);
+
+/* `.array` text writer: "H W\n", then R, G, B planes as space-terminated decimal ints, one plane
+ * per line, no trailing newline.  Replaces JPEGParser::write() (cpp-decoder/src/parser.cpp:197-209)
+ * and the CUDA write() (cuda-decoder/src/parser.cu:702-744). */
+jd_status jd_write_array(const char* path, const uint8_t* rgb, int width, int height);
+
+const char* jd_status_str(jd_status st);
+int jd_abi_version(void);
+
+/* Device-memory helpers for FFI callers that bring no allocator of their own (ctypes tests). */
+jd_status jd_device_alloc(jd_ctx* ctx, size_t bytes, void** dptr);
+jd_status jd_device_free(jd_ctx* ctx, void* dptr);
+jd_status jd_memcpy_h2d(jd_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
+jd_status jd_memcpy_d2h(jd_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
+jd_status jd_synchronize(jd_ctx* ctx);
+
+/* Per-kernel timing (JD_FLAG_TIMING).  Kernels: 0 rst_scan, 1 rst_index, 2 huffman, 3 idct_color. */
+#define JD_NUM_KERNELS 4
+typedef struct jd_stats {
+    int launches[JD_NUM_KERNELS];
+    double total_ms[JD_NUM_KERNELS]; /* hipEvent time, summed over launches                     */
+    double bytes[JD_NUM_KERNELS];    /* algorithmic bytes moved, summed          */
+    double batches, images, pixels, ecs_bytes, blocks, segments;
+} jd_stats;
+jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out);
+jd_status jd_reset_stats(jd_ctx* ctx);
+const char* jd_kernel_name(int k);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JD_H */

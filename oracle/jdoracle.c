@@ -1,0 +1,574 @@
+/*
+ * jdoracle.c — CPU restatement of the reference decoder (TEST INFRASTRUCTURE ONLY).
+ *
+ * This is the checker for the GPU decode path, never part of it: the product library
+ * (gpu-jpeg-decoder_amd/) does not link or call anything here.  Only tests/, the smoke() checker in
+ * __graft_entry__.py and bench.py's cpu_baseline leg load liboracle.so.
+ *
+ * It restates, function by function, the reference's CPU decoder (/root/reference/cpp-decoder):
+ *   bit reader / EXTEND        utils/stream.cpp:8-52
+ *   marker walk                src/parser.cpp:24-103
+ *   Huffman code assignment    src/huffmanTree.cpp:4-110 (tree walk == canonical decode, F.2.2.3)
+ *   block decode + dequant     src/parser.cpp:105-142
+ *   zig-zag + integer IDCT     src/idct.cpp:7-133, src/idct.h:3-9
+ *   MCU raster + crop          src/parser.cpp:144-195
+ *   YCbCr -> RGB               utils/color.cpp:4-19
+ * and extends it (semantics in DESIGN.md §3, not pinned by the reference) to: any Hi/Vi sampling
+ * with replicate chroma upsampling, DRI/RSTn restart intervals (byte-align, predictor reset,
+ * marker skip), SOS/SOF table selectors, multi-table DQT/DHT segments and 1-component frames.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "jdoracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* tables                                                                                      */
+/* ------------------------------------------------------------------------------------------ */
+
+/* natural (row-major) position -> zig-zag index; src/idct.cpp:8-16 */
+static const int kZigzagOfNatural[64] = {
+    0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42, 3,  8,  12, 17, 25, 30,
+    41, 43, 9,  11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38,
+    46, 51, 55, 60, 21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+typedef struct {
+    int present;
+    uint8_t counts[17]; /* counts[l]: number of codes of length l, l = 1..16 */
+    uint8_t vals[256];
+    int nvals;
+    int32_t mincode[17], maxcode[18], valptr[17];
+} huff_t;
+
+typedef struct {
+    jdo_info info;
+    int cid[4];
+    int td[4], ta[4];
+    int32_t q[4][64]; /* zig-zag order as stored in DQT */
+    int qpresent[4];
+    huff_t dc[4], ac[4];
+} img_t;
+
+static uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+/* Canonical code assignment.  The reference inserts leaves leftmost-first in order of increasing
+ * length (huffmanTree.cpp:20-68), which is exactly the canonical assignment of JPEG Annex C. */
+static int huff_build(huff_t* h) {
+    int code = 0, k = 0;
+    for (int l = 1; l <= 16; l++) {
+        h->valptr[l] = k;
+        h->mincode[l] = code;
+        code += h->counts[l];
+        k += h->counts[l];
+        h->maxcode[l] = h->counts[l] ? code - 1 : -1;
+        if (code > (1 << l)) return JDO_ERR_CORRUPT; /* over-subscribed */
+        code <<= 1;
+    }
+    h->maxcode[17] = 0x7fffffff;
+    h->present = 1;
+    return JDO_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* marker walk (restates parser.cpp:24-103, generalised)                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+static int parse(const uint8_t* d, size_t n, img_t* im) {
+    memset(im, 0, sizeof(*im));
+    if (!d || n < 4) return JDO_ERR_INVALID_ARG;
+    if (d[0] != 0xFF || d[1] != 0xD8) return JDO_ERR_CORRUPT;
+    size_t p = 2;
+    int have_sof = 0;
+    for (;;) {
+        if (p + 2 > n) return JDO_ERR_TRUNCATED;
+        if (d[p] != 0xFF) return JDO_ERR_CORRUPT;
+        while (p + 1 < n && d[p + 1] == 0xFF) p++; /* fill bytes */
+        if (p + 2 > n) return JDO_ERR_TRUNCATED;
+        uint8_t m = d[p + 1];
+        p += 2;
+        if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+        if (m == 0xD9) return JDO_ERR_CORRUPT; /* EOI before SOS */
+        if (p + 2 > n) return JDO_ERR_TRUNCATED;
+        size_t L = be16(d + p);
+        if (L < 2 || p + L > n) return JDO_ERR_TRUNCATED;
+        const uint8_t* s = d + p + 2;
+        size_t sl = L - 2;
+        if (m == 0xC0 || m == 0xC1) { /* SOF0 / SOF1: Huffman sequential */
+            if (sl < 6) return JDO_ERR_CORRUPT;
+            if (s[0] != 8) return JDO_ERR_UNSUPPORTED;
+            im->info.height = be16(s + 1);
+            im->info.width = be16(s + 3);
+            int nc = s[5];
+            if (nc != 1 && nc != 3) return JDO_ERR_UNSUPPORTED;
+            if (sl < 6 + 3 * (size_t)nc) return JDO_ERR_CORRUPT;
+            if (im->info.width == 0 || im->info.height == 0) return JDO_ERR_UNSUPPORTED;
+            im->info.ncomp = nc;
+            for (int c = 0; c < nc; c++) {
+                im->cid[c] = s[6 + 3 * c];
+                im->info.h[c] = s[7 + 3 * c] >> 4;
+                im->info.v[c] = s[7 + 3 * c] & 15;
+                im->info.tq[c] = s[8 + 3 * c];
+                if (im->info.h[c] < 1 || im->info.h[c] > 4 || im->info.v[c] < 1 ||
+                    im->info.v[c] > 4 || im->info.tq[c] > 3)
+                    return JDO_ERR_CORRUPT;
+            }
+            have_sof = 1;
+        } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+            return JDO_ERR_UNSUPPORTED; /* progressive, lossless, arithmetic */
+        } else if (m == 0xC4) { /* DHT, possibly several tables */
+            size_t q = 0;
+            while (q < sl) {
+                if (q + 17 > sl) return JDO_ERR_CORRUPT;
+                int tc = s[q] >> 4, th = s[q] & 15;
+                if (tc > 1 || th > 3) return JDO_ERR_CORRUPT;
+                huff_t* h = tc ? &im->ac[th] : &im->dc[th];
+                memset(h, 0, sizeof(*h));
+                int tot = 0;
+                for (int l = 1; l <= 16; l++) {
+                    h->counts[l] = s[q + l];
+                    tot += s[q + l];
+                }
+                if (tot > 256 || q + 17 + tot > sl) return JDO_ERR_CORRUPT;
+                memcpy(h->vals, s + q + 17, tot);
+                h->nvals = tot;
+                if (huff_build(h)) return JDO_ERR_CORRUPT;
+                q += 17 + tot;
+            }
+        } else if (m == 0xDB) { /* DQT, possibly several tables */
+            size_t q = 0;
+            while (q < sl) {
+                int pq = s[q] >> 4, tq = s[q] & 15;
+                if (pq > 1 || tq > 3) return JDO_ERR_CORRUPT;
+                if (q + 1 + 64 * (pq + 1) > sl) return JDO_ERR_CORRUPT;
+                for (int k = 0; k < 64; k++)
+                    im->q[tq][k] = pq ? be16(s + q + 1 + 2 * k) : s[q + 1 + k];
+                im->qpresent[tq] = 1;
+                q += 1 + 64 * (pq + 1);
+            }
+        } else if (m == 0xDD) { /* DRI */
+            if (sl < 2) return JDO_ERR_CORRUPT;
+            im->info.restart_interval = be16(s);
+        } else if (m == 0xDA) { /* SOS */
+            if (!have_sof) return JDO_ERR_CORRUPT;
+            if (sl < 1) return JDO_ERR_CORRUPT;
+            int ns = s[0];
+            if (sl < 4 + 2 * (size_t)ns) return JDO_ERR_CORRUPT;
+            if (ns != im->info.ncomp) return JDO_ERR_UNSUPPORTED; /* multi-scan sequential */
+            for (int i = 0; i < ns; i++) {
+                int cs = s[1 + 2 * i];
+                if (cs != im->cid[i]) return JDO_ERR_UNSUPPORTED; /* scan order != frame order */
+                im->td[i] = s[2 + 2 * i] >> 4;
+                im->ta[i] = s[2 + 2 * i] & 15;
+                if (im->td[i] > 3 || im->ta[i] > 3) return JDO_ERR_CORRUPT;
+                if (!im->dc[im->td[i]].present || !im->ac[im->ta[i]].present)
+                    return JDO_ERR_CORRUPT;
+                if (!im->qpresent[im->info.tq[i]]) return JDO_ERR_CORRUPT;
+            }
+            int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahal = s[3 + 2 * ns];
+            if (ss != 0 || se != 63 || ahal != 0) return JDO_ERR_UNSUPPORTED;
+            im->info.ecs_offset = p + L;
+            break;
+        }
+        /* APPn, COM, DNL, anything else: skipped by length */
+        p += L;
+    }
+    jdo_info* f = &im->info;
+    if (f->ncomp == 1) {
+        f->h[0] = f->v[0] = 1; /* non-interleaved: MCU = one block */
+        f->hmax = f->vmax = 1;
+    } else {
+        f->hmax = f->vmax = 1;
+        for (int c = 0; c < f->ncomp; c++) {
+            if (f->h[c] > f->hmax) f->hmax = f->h[c];
+            if (f->v[c] > f->vmax) f->vmax = f->v[c];
+        }
+        for (int c = 0; c < f->ncomp; c++)
+            if (f->hmax % f->h[c] || f->vmax % f->v[c]) return JDO_ERR_UNSUPPORTED;
+    }
+    f->mcux = (f->width + 8 * f->hmax - 1) / (8 * f->hmax);
+    f->mcuy = (f->height + 8 * f->vmax - 1) / (8 * f->vmax);
+    f->blocks_per_mcu = 0;
+    for (int c = 0; c < f->ncomp; c++) f->blocks_per_mcu += f->h[c] * f->v[c];
+    if (f->blocks_per_mcu > 10) return JDO_ERR_UNSUPPORTED;
+    return JDO_OK;
+}
+
+int jdo_parse(const uint8_t* jpeg, size_t len, jdo_info* info) {
+    img_t im;
+    int st = parse(jpeg, len, &im);
+    if (info) *info = im.info;
+    return st;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* bit reader (restates stream.cpp:8-52 plus byte un-stuffing from parser.cpp:84-98)           */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+    const uint8_t* d;
+    size_t n, pos;
+    int acc, nacc, acc_fill;
+    int at_marker; /* reader stopped in front of a marker (FF xx, xx != 00) */
+    int overrun;   /* consumed a bit that lies beyond the segment's data */
+} br_t;
+
+/* next un-stuffed data byte, or a 0xFF fill byte once a marker / the end is reached */
+static int br_fetch(br_t* b, int* is_fill) {
+    if (!b->at_marker && b->pos < b->n) {
+        uint8_t c = b->d[b->pos];
+        if (c != 0xFF) {
+            b->pos++;
+            *is_fill = 0;
+            return c;
+        }
+        if (b->pos + 1 < b->n && b->d[b->pos + 1] == 0x00) {
+            b->pos += 2;
+            *is_fill = 0;
+            return 0xFF;
+        }
+        b->at_marker = 1; /* leave the marker in place */
+    }
+    *is_fill = 1;
+    return 0xFF;
+}
+
+static inline int br_bit(br_t* b) {
+    if (b->nacc == 0) {
+        b->acc = br_fetch(b, &b->acc_fill);
+        b->nacc = 8;
+    }
+    if (b->acc_fill) b->overrun = 1;
+    b->nacc--;
+    return (b->acc >> b->nacc) & 1;
+}
+
+static inline int br_bits(br_t* b, int n) { /* stream.cpp:15-22 */
+    int v = 0;
+    for (int i = 0; i < n; i++) v = (v << 1) | br_bit(b);
+    return v;
+}
+
+/* EXTEND; stream.cpp:44-52 (s == 0 -> 0, the value the reference computes for ZRL/size-0) */
+static inline int extend(int v, int s) {
+    if (s == 0) return 0;
+    int l = 1 << (s - 1);
+    return v >= l ? v : v - ((l << 1) - 1);
+}
+
+/* huffmanTree.cpp:85-110 bit-by-bit walk, as the canonical DECODE procedure (F.2.2.3) */
+static inline int huff_decode(br_t* b, const huff_t* h, int* bad) {
+    int code = 0;
+    for (int l = 1; l <= 16; l++) {
+        code = (code << 1) | br_bit(b);
+        if (code <= h->maxcode[l]) return h->vals[h->valptr[l] + code - h->mincode[l]];
+    }
+    *bad = 1;
+    return 0;
+}
+
+/* restart: byte-align, expect RST(k mod 8), skip it; resync on the next RSTn when missing */
+static int br_restart(br_t* b, int k) {
+    b->nacc = 0;
+    b->acc_fill = 0;
+    b->at_marker = 0;
+    size_t p = b->pos;
+    while (p + 1 < b->n && b->d[p] == 0xFF && b->d[p + 1] == 0xFF) p++;
+    if (p + 1 < b->n && b->d[p] == 0xFF && b->d[p + 1] == (0xD0 | (k & 7))) {
+        b->pos = p + 2;
+        return 1;
+    }
+    for (; p + 1 < b->n; p++) {
+        if (b->d[p] == 0xFF && b->d[p + 1] >= 0xD0 && b->d[p + 1] <= 0xD7) {
+            b->pos = p + 2;
+            return 0;
+        }
+    }
+    b->pos = b->n;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* integer IDCT (restates idct.cpp:20-133, shortcuts included) and colour (color.cpp:4-19)     */
+/* ------------------------------------------------------------------------------------------ */
+
+enum { C1 = 2841, C2 = 2676, C3 = 2408, C5 = 1609, C6 = 1108, C7 = 565 };
+
+static inline int clip256(int v) { return v < -256 ? -256 : (v > 255 ? 255 : v); }
+
+static void idct_row(int* blk) {
+    int x0, x1, x2, x3, x4, x5, x6, x7, x8;
+    if (!((x1 = blk[4] << 11) | (x2 = blk[6]) | (x3 = blk[2]) | (x4 = blk[1]) | (x5 = blk[7]) |
+          (x6 = blk[5]) | (x7 = blk[3]))) {
+        int v = blk[0] << 3;
+        for (int i = 0; i < 8; i++) blk[i] = v;
+        return;
+    }
+    x0 = (blk[0] << 11) + 128;
+    x8 = C7 * (x4 + x5);
+    x4 = x8 + (C1 - C7) * x4;
+    x5 = x8 - (C1 + C7) * x5;
+    x8 = C3 * (x6 + x7);
+    x6 = x8 - (C3 - C5) * x6;
+    x7 = x8 - (C3 + C5) * x7;
+    x8 = x0 + x1;
+    x0 -= x1;
+    x1 = C6 * (x3 + x2);
+    x2 = x1 - (C2 + C6) * x2;
+    x3 = x1 + (C2 - C6) * x3;
+    x1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = x0 + x2;
+    x0 -= x2;
+    x2 = (181 * (x4 + x5) + 128) >> 8;
+    x4 = (181 * (x4 - x5) + 128) >> 8;
+    blk[0] = (x7 + x1) >> 8;
+    blk[1] = (x3 + x2) >> 8;
+    blk[2] = (x0 + x4) >> 8;
+    blk[3] = (x8 + x6) >> 8;
+    blk[4] = (x8 - x6) >> 8;
+    blk[5] = (x0 - x4) >> 8;
+    blk[6] = (x3 - x2) >> 8;
+    blk[7] = (x7 - x1) >> 8;
+}
+
+static void idct_col(int* blk) {
+    int x0, x1, x2, x3, x4, x5, x6, x7, x8;
+    if (!((x1 = (blk[8 * 4] << 8)) | (x2 = blk[8 * 6]) | (x3 = blk[8 * 2]) | (x4 = blk[8 * 1]) |
+          (x5 = blk[8 * 7]) | (x6 = blk[8 * 5]) | (x7 = blk[8 * 3]))) {
+        int v = clip256((blk[0] + 32) >> 6);
+        for (int i = 0; i < 8; i++) blk[8 * i] = v;
+        return;
+    }
+    x0 = (blk[8 * 0] << 8) + 8192;
+    x8 = C7 * (x4 + x5) + 4;
+    x4 = (x8 + (C1 - C7) * x4) >> 3;
+    x5 = (x8 - (C1 + C7) * x5) >> 3;
+    x8 = C3 * (x6 + x7) + 4;
+    x6 = (x8 - (C3 - C5) * x6) >> 3;
+    x7 = (x8 - (C3 + C5) * x7) >> 3;
+    x8 = x0 + x1;
+    x0 -= x1;
+    x1 = C6 * (x3 + x2) + 4;
+    x2 = (x1 - (C2 + C6) * x2) >> 3;
+    x3 = (x1 + (C2 - C6) * x3) >> 3;
+    x1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = x0 + x2;
+    x0 -= x2;
+    x2 = (181 * (x4 + x5) + 128) >> 8;
+    x4 = (181 * (x4 - x5) + 128) >> 8;
+    blk[8 * 0] = clip256((x7 + x1) >> 14);
+    blk[8 * 1] = clip256((x3 + x2) >> 14);
+    blk[8 * 2] = clip256((x0 + x4) >> 14);
+    blk[8 * 3] = clip256((x8 + x6) >> 14);
+    blk[8 * 4] = clip256((x8 - x6) >> 14);
+    blk[8 * 5] = clip256((x0 - x4) >> 14);
+    blk[8 * 6] = clip256((x3 - x2) >> 14);
+    blk[8 * 7] = clip256((x7 - x1) >> 14);
+}
+
+void jdo_idct_ref(const int32_t in_zz[64], int32_t out[64]) {
+    int blk[64];
+    for (int i = 0; i < 64; i++) blk[i] = in_zz[kZigzagOfNatural[i]]; /* idct.cpp:24-32 */
+    for (int r = 0; r < 8; r++) idct_row(blk + 8 * r);
+    for (int c = 0; c < 8; c++) idct_col(blk + c);
+    for (int i = 0; i < 64; i++) out[i] = blk[i];
+}
+
+static inline int clamp255(int v) { return v > 255 ? 255 : (v < 0 ? 0 : v); }
+
+void jdo_color_ref(int y, int cb, int cr, uint8_t rgb[3]) {
+    /* color.cpp:11-17: products and sums in double, stored to float, +128 in float, truncation */
+    float r = cr * (2 - 2 * 0.299) + y;
+    float b = cb * (2 - 2 * 0.114) + y;
+    float g = (y - 0.114 * b - 0.299 * r) / 0.587;
+    rgb[0] = (uint8_t)clamp255((int)(r + 128));
+    rgb[1] = (uint8_t)clamp255((int)(g + 128));
+    rgb[2] = (uint8_t)clamp255((int)(b + 128));
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* scan decode                                                                                 */
+/* ------------------------------------------------------------------------------------------ */
+
+/* One block: parser.cpp:105-142.  zz[] receives quantised values (zig-zag order, DC absolute). */
+static void decode_block(br_t* b, const huff_t* dc, const huff_t* ac, int* pred, int32_t zz[64],
+                         int* bad) {
+    memset(zz, 0, 64 * sizeof(int32_t));
+    int s = huff_decode(b, dc, bad);
+    if (s > 16) {
+        *bad = 1;
+        s = 16;
+    }
+    int diff = extend(br_bits(b, s), s);
+    *pred += diff;
+    zz[0] = *pred;
+    int k = 1;
+    while (k < 64) {
+        int rs = huff_decode(b, ac, bad);
+        if (rs == 0) break; /* EOB */
+        k += rs >> 4;       /* run (ZRL: 15 zeros + the explicit zero below) */
+        int sz = rs & 15;
+        int bits = br_bits(b, sz);
+        if (k < 64) {
+            zz[k] = extend(bits, sz);
+            k++;
+        }
+    }
+}
+
+typedef struct {
+    int32_t* plane[4];
+    int stride[4]; /* samples per plane row */
+} planes_t;
+
+/* Decodes the whole scan.  Either stores IDCT output into planes (pl != NULL) or quantised
+ * coefficients into coef (coef != NULL). */
+static int decode_scan(const img_t* im, const uint8_t* d, size_t n, planes_t* pl, int32_t* coef) {
+    const jdo_info* f = &im->info;
+    br_t b;
+    memset(&b, 0, sizeof(b));
+    b.d = d + f->ecs_offset;
+    b.n = n - f->ecs_offset;
+    int pred[4] = {0, 0, 0, 0};
+    int bad = 0, rst = 0;
+    const int nmcu = f->mcux * f->mcuy;
+    const int ri = f->restart_interval;
+    int32_t zz[64], deq[64], out[64];
+    for (int m = 0; m < nmcu; m++) {
+        if (ri && m > 0 && m % ri == 0) {
+            if (b.overrun) bad = 1;
+            if (!br_restart(&b, rst)) bad = 1;
+            rst++;
+            b.overrun = 0;
+            for (int c = 0; c < 4; c++) pred[c] = 0;
+        }
+        const int my = m / f->mcux, mx = m % f->mcux;
+        int blk = 0;
+        for (int c = 0; c < f->ncomp; c++) {
+            const huff_t* dc = &im->dc[im->td[c]];
+            const huff_t* ac = &im->ac[im->ta[c]];
+            const int32_t* q = im->q[f->tq[c]];
+            for (int by = 0; by < f->v[c]; by++)
+                for (int bx = 0; bx < f->h[c]; bx++, blk++) {
+                    decode_block(&b, dc, ac, &pred[c], zz, &bad);
+                    if (coef) {
+                        memcpy(coef + ((size_t)m * f->blocks_per_mcu + blk) * 64, zz, sizeof(zz));
+                        continue;
+                    }
+                    for (int k = 0; k < 64; k++) deq[k] = zz[k] * q[k]; /* parser.cpp:111,130 */
+                    jdo_idct_ref(deq, out);
+                    int32_t* dst = pl->plane[c] + (size_t)((my * f->v[c] + by) * 8) * pl->stride[c] +
+                                   (mx * f->h[c] + bx) * 8;
+                    for (int r = 0; r < 8; r++)
+                        memcpy(dst + (size_t)r * pl->stride[c], out + 8 * r, 8 * sizeof(int32_t));
+                }
+        }
+    }
+    if (b.overrun) bad = 1;
+    return bad ? JDO_ERR_CORRUPT : JDO_OK;
+}
+
+int jdo_decode_coefs(const uint8_t* jpeg, size_t len, int32_t* coef) {
+    img_t* im = (img_t*)malloc(sizeof(img_t));
+    if (!im) return JDO_ERR_INVALID_ARG;
+    int st = parse(jpeg, len, im);
+    if (st == JDO_OK) st = decode_scan(im, jpeg, len, NULL, coef);
+    free(im);
+    return st;
+}
+
+int jdo_decode(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* height) {
+    img_t* im = (img_t*)malloc(sizeof(img_t));
+    if (!im) return JDO_ERR_INVALID_ARG;
+    int st = parse(jpeg, len, im);
+    if (st != JDO_OK) {
+        free(im);
+        return st;
+    }
+    const jdo_info* f = &im->info;
+    if (width) *width = f->width;
+    if (height) *height = f->height;
+    planes_t pl;
+    memset(&pl, 0, sizeof(pl));
+    int ok = 1;
+    for (int c = 0; c < f->ncomp; c++) {
+        pl.stride[c] = f->mcux * f->h[c] * 8;
+        pl.plane[c] = (int32_t*)malloc(sizeof(int32_t) * pl.stride[c] * f->mcuy * f->v[c] * 8);
+        if (!pl.plane[c]) ok = 0;
+    }
+    if (!ok) {
+        for (int c = 0; c < 4; c++) free(pl.plane[c]);
+        free(im);
+        return JDO_ERR_INVALID_ARG;
+    }
+    st = decode_scan(im, jpeg, len, &pl, NULL);
+    if (rgb) {
+        /* crop + colour: parser.cpp:169-193 with replicate upsampling for Hi < Hmax / Vi < Vmax */
+        for (int y = 0; y < f->height; y++)
+            for (int x = 0; x < f->width; x++) {
+                int s[3] = {0, 0, 0};
+                for (int c = 0; c < f->ncomp; c++) {
+                    int sx = x * f->h[c] / f->hmax, sy = y * f->v[c] / f->vmax;
+                    s[c] = pl.plane[c][(size_t)sy * pl.stride[c] + sx];
+                }
+                jdo_color_ref(s[0], s[1], s[2], rgb + ((size_t)y * f->width + x) * 3);
+            }
+    }
+    for (int c = 0; c < 4; c++) free(pl.plane[c]);
+    free(im);
+    return st;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* CPU baseline helper                                                                         */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+    const uint8_t* const* jpegs;
+    const size_t* lens;
+    uint8_t* const* rgbs;
+    int* status;
+    int n;
+    int next;
+} work_t;
+
+static void* worker(void* arg) {
+    work_t* w = (work_t*)arg;
+    for (;;) {
+        int i = __sync_fetch_and_add(&w->next, 1);
+        if (i >= w->n) break;
+        int st = jdo_decode(w->jpegs[i], w->lens[i], w->rgbs ? w->rgbs[i] : NULL, NULL, NULL);
+        if (w->status) w->status[i] = st;
+    }
+    return NULL;
+}
+
+double jdo_decode_many(const uint8_t* const* jpegs, const size_t* lens, int n, uint8_t* const* rgbs,
+                       int threads, int* status) {
+    work_t w = {jpegs, lens, rgbs, status, n, 0};
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    if (threads == 1) {
+        worker(&w);
+    } else {
+        for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, worker, &w);
+        for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

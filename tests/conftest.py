@@ -1,0 +1,36 @@
+"""Shared fixtures.  `-m "not gpu"` runs on CPU; `-m gpu` tests need a MI355X (gfx950)."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "gpu-jpeg-decoder_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a MI355X GPU (run with -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        entries = json.load(f)["entries"]
+    for e in entries:
+        with open(os.path.join(GOLDEN, e["file"]), "rb") as f:
+            e["data"] = f.read()
+    return entries
+
+
+@pytest.fixture(scope="session")
+def decoder():
+    import jdamd
+
+    dec = jdamd.Decoder(0, timing=True)
+    yield dec
+    dec.close()

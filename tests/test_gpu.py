@@ -1,0 +1,167 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bar: bit-exact RGB (integer/byte work).  Oracle = oracle/liboracle.so, pinned to the reference by
+tests/test_oracle.py; golden digests from tests/golden/make_golden.py.
+"""
+import hashlib
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import jdamd
+import jdoracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import jd_synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint8).tobytes()).hexdigest()
+
+
+def test_golden_single(decoder, golden):
+    bad = []
+    for e in golden:
+        if e["status"] != 0:
+            with pytest.raises(jdamd.JDError) as ei:
+                decoder.decode(e["data"])
+            assert ei.value.status == e["status"], e["file"]
+            continue
+        out = decoder.decode(e["data"])
+        if sha(out) != e["sha256"]:
+            st, ref = jdoracle.decode(e["data"])
+            diff = np.abs(out.astype(int) - ref.astype(int))
+            bad.append((e["file"], int(diff.max()), int((diff > 0).sum())))
+    assert not bad, bad
+
+
+def test_golden_batch(decoder, golden):
+    """All fixtures in one batch: mixed sizes, sampling factors, table sets, RST / no RST."""
+    outs, status = decoder.decode_batch([e["data"] for e in golden])
+    for e, o, s in zip(golden, outs, status):
+        assert s == e["status"], e["file"]
+        if s == 0:
+            assert sha(o) == e["sha256"], e["file"]
+
+
+def test_device_resident_batch(decoder, golden):
+    """Inputs already in HBM, outputs left in HBM (the bench path)."""
+    ok = [e for e in golden if e["status"] == 0]
+    hosts = [np.frombuffer(e["data"], np.uint8).copy() for e in ok]
+    offs, total = [], 0
+    for h in hosts:
+        offs.append(total)
+        total += (h.nbytes + 255) // 256 * 256
+    din = decoder.alloc(total)
+    for h, o in zip(hosts, offs):
+        din.upload(h, o)
+    sizes = [e["width"] * e["height"] * 3 for e in ok]
+    ooffs, ototal = [], 0
+    for s in sizes:
+        ooffs.append(ototal)
+        ototal += (s + 255) // 256 * 256
+    dout = decoder.alloc(ototal)
+    status = decoder.decode_batch_device(hosts, [din.ptr + o for o in offs], [dout.ptr + o for o in ooffs])
+    assert all(s == 0 for s in status)
+    for e, o, s in zip(ok, ooffs, sizes):
+        img = dout.download(np.empty(s, np.uint8), o)
+        assert sha(img) == e["sha256"], e["file"]
+
+
+@pytest.mark.parametrize("w,h,ss,rows,blocks,q", [
+    (1920, 1080, "4:2:0", 1, 0, 90),   # BASELINE config 2 shape
+    (1920, 1080, "4:2:0", 0, 0, 90),   # no DRI: single segment
+    (1920, 1080, "4:4:4", 0, 0, 90),
+    (1280, 720, "4:2:2", 0, 7, 75),
+    (3840, 2160, "4:2:0", 1, 0, 90),   # BASELINE config 3 shape
+])
+def test_full_size_vs_oracle(decoder, w, h, ss, rows, blocks, q):
+    data = jd_synth.encode(jd_synth.synth_pixels(w, h, 42), q, ss, rows, blocks)
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    out = decoder.decode(data)
+    assert np.array_equal(out, ref)
+
+
+def test_rst_invariance_full_size(decoder):
+    px = jd_synth.synth_pixels(1920, 1080, 7)
+    a = decoder.decode(jd_synth.encode(px, 90, "4:2:0"))
+    b = decoder.decode(jd_synth.encode(px, 90, "4:2:0", restart_rows=1))
+    c = decoder.decode(jd_synth.encode(px, 90, "4:2:0", restart_blocks=5))
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
+def test_idct_kat(decoder):
+    rng = np.random.default_rng(1)
+    blocks = []
+    # DC-only sweep across the whole dequantised DC range
+    dc = np.zeros((4096, 64), np.int32)
+    dc[:, 0] = np.arange(-32768, 32768, 16)[:4096]
+    blocks.append(dc)
+    # sparse realistic blocks and dense random blocks
+    sp = np.zeros((20000, 64), np.int32)
+    for k in range(20000):
+        n = rng.integers(0, 12)
+        idx = rng.integers(0, 64, n)
+        sp[k, idx] = rng.integers(-1024, 1024, n) * rng.integers(1, 40, n)
+    blocks.append(sp)
+    blocks.append(rng.integers(-2048, 2048, (20000, 64), dtype=np.int32))
+    a = np.concatenate(blocks)
+    got = decoder.test_idct(a)
+    want = jdoracle.idct(a)
+    assert np.array_equal(got, want)
+
+
+def test_color_exhaustive(decoder):
+    """All 2^27 (Y, Cb, Cr) in [-256, 255]^3 against utils/color.cpp's double/float formula
+    (restated in numpy, float32/float64 exactly as the reference rounds)."""
+    cb, cr = np.meshgrid(np.arange(-256, 256, dtype=np.int32), np.arange(-256, 256, dtype=np.int32),
+                         indexing="ij")
+    cb = cb.ravel()
+    cr = cr.ravel()
+    bad = 0
+    for y0 in range(-256, 256, 16):
+        ys = np.repeat(np.arange(y0, y0 + 16, dtype=np.int32), cb.size)
+        cbs = np.tile(cb, 16)
+        crs = np.tile(cr, 16)
+        ycc = np.stack([ys, cbs, crs], -1)
+        got = decoder.test_color(ycc)
+        yd = ys.astype(np.float64)
+        r = (crs * (2 - 2 * 0.299) + yd).astype(np.float32)
+        b = (cbs * (2 - 2 * 0.114) + yd).astype(np.float32)
+        g = ((yd - 0.114 * b.astype(np.float64) - 0.299 * r.astype(np.float64)) / 0.587).astype(np.float32)
+        want = np.stack([np.clip((r + np.float32(128)).astype(np.int32), 0, 255),
+                         np.clip((g + np.float32(128)).astype(np.int32), 0, 255),
+                         np.clip((b + np.float32(128)).astype(np.int32), 0, 255)], -1).astype(np.uint8)
+        bad += int((got != want).any(-1).sum())
+    assert bad == 0
+
+
+def test_corrupt_inputs_do_not_poison_batch(decoder, golden):
+    good = next(e for e in golden if e["file"].endswith("2_400x400.jpg"))
+    d = good["data"]
+    trunc = d[: len(d) // 2]                                # ECS cut short -> overrun
+    garbage = d[:700] + bytes(np.random.default_rng(3).integers(0, 256, 4000, dtype=np.uint8)) + b"\xff\xd9"
+    noheader = b"\xff\xd8\xff\xd9"
+    outs, status = decoder.decode_batch([d, trunc, garbage, noheader, d])
+    assert status[0] == 0 and status[4] == 0
+    assert sha(outs[0]) == good["sha256"] and sha(outs[4]) == good["sha256"]
+    assert status[1] != 0 and status[3] != 0
+    for data, s in ((trunc, status[1]), (garbage, status[2])):
+        ost, _ = jdoracle.decode(data)
+        assert (ost == 0) == (s == 0)
+
+
+def test_cli_array_matches_reference_format(tmp_path, golden):
+    exe = os.path.join(ROOT, "gpu-jpeg-decoder_amd", "decoder")
+    img = os.path.join(ROOT, "tests", "golden", "ref", "3_120x120.jpg")
+    subprocess.run([exe, img, str(tmp_path)], check=True)
+    got = open(tmp_path / "3_120x120.array", "rb").read()
+    want = open(os.path.join(ROOT, "tests", "golden", "ref", "3_120x120.array"), "rb").read()
+    assert got == want
