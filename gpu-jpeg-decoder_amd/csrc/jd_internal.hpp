@@ -40,14 +40,16 @@ struct TableSet {
     int32_t lut[kSlotsPerSet];  // index into the LUT array (-1 = unused)
     uint8_t dc_slot[4];
     uint8_t ac_slot[4];
+    int32_t nslots;
 };
 
 // Per image of a batch (device array, one entry per decodable image).
 struct alignas(16) ImgDesc {
-    uint64_t jpeg;         // device address of the file bytes
-    uint64_t rgb;          // device address of the H*W*3 uint8 output
-    uint32_t len;          // file length in bytes
-    uint32_t ecs_off;      // first ECS byte
+    uint64_t jpeg;     // device address of the file bytes
+    uint64_t rgb;      // device address of the H*W*3 uint8 output
+    uint64_t comp;     // device address of this image's un-stuffed entropy-coded data
+    uint32_t len;      // file length in bytes
+    uint32_t ecs_off;  // first ECS byte
     uint32_t width, height;
     uint32_t mcux, mcuy;
     uint32_t ncomp, hmax, vmax, bpm;  // bpm = blocks per MCU
@@ -56,69 +58,79 @@ struct alignas(16) ImgDesc {
     uint32_t seg_base, nseg;          // this image's segments in the global segment list
     uint64_t block_base;              // first global block index
     uint32_t tableset;
-    uint32_t tile_mcus;               // MCUs per IDCT/colour tile (one MCU row slice)
-    uint32_t tiles_x;                 // tiles per MCU row
-    uint32_t chunk_base, nchunks;     // RST-scan chunks of this image
-    uint32_t status_slot;             // index into the per-image status array
+    uint32_t chunk_base, nchunks;     // 16 KiB scan chunks of this image's ECS
+    uint32_t tile_mcus;               // MCU columns per IDCT/colour tile (tile = 128 px wide)
+    uint32_t tile_mrows;              // MCU rows per tile (2 when an MCU is 8 px tall)
+    uint32_t tiles_x, tiles_y;        // tiles per image row / column
+    uint32_t lg_mw, lg_mh;            // log2 of the MCU width / height in pixels
     uint8_t h[4], v[4];
     uint16_t qslot[4];                // quant table of each component (index into batch Q array)
     uint8_t comp_block0[4];           // first MCU block of each component
-    uint32_t pad[1];
+    uint8_t shx[4], shy[4];           // log2(hmax / h[c]), log2(vmax / v[c])
+    uint32_t pad[3];
 };
 
 // Per-block result of the Huffman kernel (sparse coefficient representation):
-//   x = index of the block's first AC entry in the entry array
-//   y = (number of AC entries << 16) | (uint16)DC   (DC already un-predicted, still quantised)
+//   entry_start = index of the block's first AC entry in the entry array
+//   cnt_dc      = (number of AC entries << 16) | (uint16)DC   (DC un-predicted, still quantised)
 // AC entry = (int16 value << 16) | zig-zag index (1..63).
 struct BlockInfo {
     uint32_t entry_start;
     uint32_t cnt_dc;
 };
 
+// A break in the raw ECS found by the scan: FF followed by RSTn, or a terminating marker.
+//   pos  : byte position in the file
+//   info : (stuffed zero bytes in [chunk start, pos) << 1) | is_terminator
+struct Break {
+    uint32_t pos;
+    uint32_t info;
+};
+
 constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
 
-// RST scan geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
+// Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;
 constexpr int kScanBytesPerThread = 64;
 constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
-constexpr int kScanCap = kScanChunk / 2;  // a marker takes 2 bytes: a chunk cannot hold more
+constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cannot hold more
 
 constexpr int kHuffThreads = 256;
 constexpr int kIdctThreads = 256;
-constexpr int kTileMaxBlocks = 48;  // blocks staged in LDS per IDCT/colour tile
+constexpr int kTileWidth = 128;     // pixels per IDCT/colour tile row
+constexpr int kTileMaxBlocks = 96;  // blocks staged in LDS per IDCT/colour tile
 
 // Per-image status bits written by kernels (atomicOr); host maps them to jd_status.
-constexpr uint32_t kStCorrupt = 1u;      // bad code / overrun / DC range
-constexpr uint32_t kStRstMissing = 2u;   // fewer RST markers than intervals
-constexpr uint32_t kStRstOrder = 4u;     // RSTn numbering wrong
+constexpr uint32_t kStCorrupt = 1u;     // bad code / overrun / DC range
+constexpr uint32_t kStRstMissing = 2u;  // fewer RST markers than intervals
+constexpr uint32_t kStRstOrder = 4u;    // RSTn numbering wrong
 
-// Kernel launch wrappers (jd_kernels.hip).
 struct BatchDev {
     const ImgDesc* imgs;
     uint32_t nimg;
     const HuffLut* luts;
     const TableSet* tablesets;
     const uint16_t* qtabs;        // 64 x uint16 per quant table, zig-zag order
-    // segments
+    // segments (restart intervals)
     const uint32_t* seg_img;      // image of each segment (kInvalidImage = padding)
-    uint32_t* seg_start;          // first byte (relative to the file) of each segment
+    uint32_t* seg_cstart;         // first un-stuffed byte of each segment (image-relative)
+    uint32_t* seg_cend;           // end of each segment's data (image-relative, un-stuffed)
     const uint32_t* seg_entry;    // first AC-entry slot of each segment
     uint32_t nseg;                // including padding, multiple of kHuffThreads
     const uint32_t* wg_tableset;  // table set of each Huffman workgroup
-    // rst scan
-    const uint32_t* rst_imgs;     // images with restart intervals
-    uint32_t nrst;
+    uint32_t max_slots;           // LUT slots staged per Huffman workgroup
+    // scan / compaction
     uint32_t max_chunks;
-    uint32_t* chunk_cnt;
-    uint32_t* chunk_pos;          // kScanCap per chunk
-    uint32_t* ecs_end;            // per image: first terminating marker position
+    uint32_t* chunk_nbrk;         // breaks per chunk
+    uint32_t* chunk_drops;        // stuffed zero bytes per chunk
+    uint32_t* chunk_coff;         // un-stuffed offset of each chunk's first byte
+    Break* chunk_brk;             // kScanCap per chunk
     // outputs
     BlockInfo* blocks;
     uint32_t* entries;
     uint32_t* status;             // per image
-    unsigned long long* counters; // [0] AC entries written, [1] blocks written
-    uint32_t max_tiles_x;
-    uint32_t max_tile_rows;
+    unsigned long long* counters; // [0] AC entries written
+    uint32_t max_tiles;
 };
 
 }  // namespace jd

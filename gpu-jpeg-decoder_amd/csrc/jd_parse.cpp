@@ -130,7 +130,7 @@ done:
             if (h.v[c] > h.vmax) h.vmax = h.v[c];
         }
         for (int c = 0; c < h.ncomp; c++)
-            if (h.hmax % h.h[c] || h.vmax % h.v[c]) return JD_ERR_UNSUPPORTED;
+            if (h.h[c] == 3 || h.v[c] == 3 || h.hmax % h.h[c] || h.vmax % h.v[c]) return JD_ERR_UNSUPPORTED;
     }
     h.mcux = (h.width + 8 * h.hmax - 1) / (8 * h.hmax);
     h.mcuy = (h.height + 8 * h.vmax - 1) / (8 * h.vmax);

@@ -61,7 +61,7 @@ struct jd_ctx {
     size_t lut_dev_count = 0;
 
     // pools
-    DevBuf plan, chunk_pos, blocks, entries, input, output;
+    DevBuf plan, chunk_brk, blocks, entries, input, output, comp;
     PinBuf plan_host, input_host;
 
     hipEvent_t ev[JD_NUM_KERNELS][2] = {};
@@ -159,10 +159,10 @@ struct Plan {
     std::vector<int> item_of_img;
     std::vector<TableSet> tablesets;
     std::vector<uint16_t> qtabs;
-    std::vector<uint32_t> seg_img, seg_start, seg_entry, wg_tableset, rst_imgs, ecs_end;
-    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0;
-    uint64_t total_blocks = 0, total_entry_cap = 0;
-    double pixels = 0, ecs_bytes = 0, rst_bytes = 0;
+    std::vector<uint32_t> seg_img, seg_entry, wg_tableset;
+    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, max_slots = 1;
+    uint64_t total_blocks = 0, total_entry_cap = 0, comp_bytes = 0;
+    double pixels = 0, ecs_bytes = 0;
 };
 
 // Largest item prefix [lo, hi) whose sparse-coefficient capacity fits 32-bit entry indices.
@@ -173,8 +173,8 @@ int batch_split(jd_ctx* ctx, int lo, int n) {
         if (ctx->pst[hi] != JD_OK) continue;
         const jd_header& h = ctx->parsed[hi].hdr;
         const uint64_t blocks = uint64_t(h.mcux) * h.mcuy * h.blocks_per_mcu;
-        if (hi > lo && cap + blocks * 63 > 0xF0000000ull) break;
-        cap += blocks * 63;
+        if (hi > lo && cap + blocks * 64 > 0xF0000000ull) break;
+        cap += blocks * 64;
     }
     return hi;
 }
@@ -218,6 +218,8 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
                 t.dc_slot[c] = uint8_t(slot_of(key[1 + c]));
                 t.ac_slot[c] = uint8_t(slot_of(key[4 + c]));
             }
+            t.nslots = nslot;
+            P.max_slots = std::max(P.max_slots, uint32_t(nslot));
             ts = int(P.tablesets.size());
             P.tablesets.push_back(t);
             ts_index.emplace(key, ts);
@@ -264,25 +266,39 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         d.block_base = P.total_blocks;
         P.total_blocks += nmcu * uint64_t(h.blocks_per_mcu);
         d.tableset = uint32_t(ts);
-        d.tile_mcus = std::max(1u, std::min(uint32_t(kTileMaxBlocks) / d.bpm, d.mcux));
-        d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
-        P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.mcuy);
-        d.status_slot = uint32_t(P.imgs.size());
-        if (h.restart_interval && d.nseg > 1) {
+        {  // IDCT/colour tiles: 128 px wide, 16 px (or one MCU row if taller) high
+            uint32_t lw = 0, lh = 0;
+            while ((8u << lw) < 8u * d.hmax) lw++;
+            while ((8u << lh) < 8u * d.vmax) lh++;
+            d.lg_mw = 3 + lw;
+            d.lg_mh = 3 + lh;
+            d.tile_mcus = uint32_t(kTileWidth) >> d.lg_mw;
+            d.tile_mrows = d.vmax == 1 ? 2u : 1u;
+            d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
+            d.tiles_y = (d.mcuy + d.tile_mrows - 1) / d.tile_mrows;
+            for (int c = 0; c < h.ncomp; c++) {
+                uint32_t sx = 0, sy = 0;
+                while ((uint32_t(h.h[c]) << sx) < d.hmax) sx++;
+                while ((uint32_t(h.v[c]) << sy) < d.vmax) sy++;
+                d.shx[c] = uint8_t(sx);
+                d.shy[c] = uint8_t(sy);
+            }
+            P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.tiles_y);
+        }
+        {  // scan chunks over [align16(file + ecs_off), file + len) and the un-stuffed stream
             const uint64_t a0 = (d.jpeg + d.ecs_off) & ~uint64_t(15);
             const uint64_t span = d.jpeg + d.len - a0;
             d.nchunks = uint32_t((span + kScanChunk - 1) / kScanChunk);
             d.chunk_base = P.total_chunks;
             P.total_chunks += d.nchunks;
             P.max_chunks = std::max(P.max_chunks, d.nchunks);
-            P.rst_imgs.push_back(uint32_t(P.imgs.size()));
-            P.rst_bytes += double(d.len - d.ecs_off);
+            d.comp = P.comp_bytes;  // offset for now; rebased onto the pool in run_batch
+            P.comp_bytes += align_up(size_t(d.len - d.ecs_off) + 64, 256);
         }
         P.pixels += double(h.width) * h.height;
         P.ecs_bytes += double(d.len - d.ecs_off);
         P.imgs.push_back(d);
         P.item_of_img.push_back(it);
-        P.ecs_end.push_back(d.len);
         ts_of_img.push_back(ts);
     }
     // segments grouped by table set; each Huffman workgroup sees exactly one table set
@@ -301,14 +317,12 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
                 const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
                 const uint32_t m1 = d.restart_interval ? std::min(m0 + d.restart_interval, nmcu) : nmcu;
                 P.seg_img.push_back(order[oi]);
-                P.seg_start.push_back(k == 0 ? d.ecs_off : 0u);
                 P.seg_entry.push_back(uint32_t(entry_cursor));
                 entry_cursor += uint64_t(m1 - m0) * d.bpm * 63;
             }
         }
         while (P.seg_img.size() % kHuffThreads) {
             P.seg_img.push_back(kInvalidImage);
-            P.seg_start.push_back(0);
             P.seg_entry.push_back(0);
         }
         while (P.wg_tableset.size() < P.seg_img.size() / kHuffThreads) P.wg_tableset.push_back(uint32_t(ts));
@@ -323,6 +337,12 @@ size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
     const size_t off = align_up(blob.size(), 256);
     blob.resize(off + std::max<size_t>(v.size() * sizeof(T), 16));
     if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+size_t reserve(std::vector<uint8_t>& blob, size_t bytes) {
+    const size_t off = align_up(blob.size(), 256);
+    blob.resize(off + std::max<size_t>(bytes, 16));
     return off;
 }
 
@@ -372,58 +392,63 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
     if (st != JD_OK) return st;
     const uint32_t nimg = uint32_t(P.imgs.size());
     if (nimg) {
+        HIPCHK(ctx, ensure_dev(ctx->comp, std::max<size_t>(16, P.comp_bytes)));
+        for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(ctx->comp.p);
         std::vector<uint8_t> blob;
+        const size_t nseg = P.seg_img.size();
         const size_t o_imgs = put(blob, P.imgs);
         const size_t o_ts = put(blob, P.tablesets);
         const size_t o_q = put(blob, P.qtabs);
         const size_t o_segimg = put(blob, P.seg_img);
-        const size_t o_segstart = put(blob, P.seg_start);
         const size_t o_segent = put(blob, P.seg_entry);
         const size_t o_wgts = put(blob, P.wg_tableset);
-        const size_t o_rst = put(blob, P.rst_imgs);
-        const size_t o_cc = put(blob, std::vector<uint32_t>(P.total_chunks, 0));
-        const size_t o_end = put(blob, P.ecs_end);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
         const size_t o_ctr = put(blob, std::vector<unsigned long long>(2, 0));
+        const size_t upload = blob.size();
+        // device-written scratch after the uploaded part (no initialisation needed)
+        const size_t o_cstart = reserve(blob, nseg * 4);
+        const size_t o_cend = reserve(blob, nseg * 4);
+        const size_t o_nbrk = reserve(blob, size_t(P.total_chunks) * 4);
+        const size_t o_drops = reserve(blob, size_t(P.total_chunks) * 4);
+        const size_t o_coff = reserve(blob, size_t(P.total_chunks) * 4);
         HIPCHK(ctx, ensure_dev(ctx->plan, blob.size()));
-        HIPCHK(ctx, ensure_pin(ctx->plan_host, blob.size()));
-        memcpy(ctx->plan_host.p, blob.data(), blob.size());
-        HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, ctx->plan_host.p, blob.size(), hipMemcpyHostToDevice, s));
-        HIPCHK(ctx, ensure_dev(ctx->chunk_pos, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * 4)));
+        HIPCHK(ctx, ensure_pin(ctx->plan_host, upload));
+        memcpy(ctx->plan_host.p, blob.data(), upload);
+        HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, ctx->plan_host.p, upload, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, ensure_dev(ctx->chunk_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
         HIPCHK(ctx, ensure_dev(ctx->blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
         HIPCHK(ctx, ensure_dev(ctx->entries, std::max<size_t>(16, P.total_entry_cap * 4)));
 
         uint8_t* base = static_cast<uint8_t*>(ctx->plan.p);
         BatchDev b;
+        memset(&b, 0, sizeof(b));
         b.imgs = reinterpret_cast<const ImgDesc*>(base + o_imgs);
         b.nimg = nimg;
         b.luts = static_cast<const HuffLut*>(ctx->lut_dev.p);
         b.tablesets = reinterpret_cast<const TableSet*>(base + o_ts);
         b.qtabs = reinterpret_cast<const uint16_t*>(base + o_q);
         b.seg_img = reinterpret_cast<const uint32_t*>(base + o_segimg);
-        b.seg_start = reinterpret_cast<uint32_t*>(base + o_segstart);
+        b.seg_cstart = reinterpret_cast<uint32_t*>(base + o_cstart);
+        b.seg_cend = reinterpret_cast<uint32_t*>(base + o_cend);
         b.seg_entry = reinterpret_cast<const uint32_t*>(base + o_segent);
-        b.nseg = uint32_t(P.seg_img.size());
+        b.nseg = uint32_t(nseg);
         b.wg_tableset = reinterpret_cast<const uint32_t*>(base + o_wgts);
-        b.rst_imgs = reinterpret_cast<const uint32_t*>(base + o_rst);
-        b.nrst = uint32_t(P.rst_imgs.size());
+        b.max_slots = P.max_slots;
         b.max_chunks = P.max_chunks;
-        b.chunk_cnt = reinterpret_cast<uint32_t*>(base + o_cc);
-        b.chunk_pos = static_cast<uint32_t*>(ctx->chunk_pos.p);
-        b.ecs_end = reinterpret_cast<uint32_t*>(base + o_end);
+        b.chunk_nbrk = reinterpret_cast<uint32_t*>(base + o_nbrk);
+        b.chunk_drops = reinterpret_cast<uint32_t*>(base + o_drops);
+        b.chunk_coff = reinterpret_cast<uint32_t*>(base + o_coff);
+        b.chunk_brk = static_cast<Break*>(ctx->chunk_brk.p);
         b.blocks = static_cast<BlockInfo*>(ctx->blocks.p);
         b.entries = static_cast<uint32_t*>(ctx->entries.p);
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
-        b.max_tiles_x = P.max_tiles;
-        b.max_tile_rows = 0;
+        b.max_tiles = P.max_tiles;
 
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
-        hipError_t (*launch[JD_NUM_KERNELS])(const BatchDev&, hipStream_t) = {launch_rst_scan, launch_rst_index,
-                                                                             launch_huffman, launch_idct_color};
-        const bool active[JD_NUM_KERNELS] = {b.nrst > 0, b.nrst > 0, true, true};
+        hipError_t (*launch[JD_NUM_KERNELS])(const BatchDev&, hipStream_t) = {
+            launch_scan, launch_index, launch_compact, launch_huffman, launch_idct_color};
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
-            if (!active[k]) continue;
             if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][0], s));
             HIPCHK(ctx, launch[k](b, s));
             if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][1], s));
@@ -436,14 +461,18 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         for (uint32_t i = 0; i < nimg; i++)
             if (status[i]) ctx->pst[P.item_of_img[i]] = JD_ERR_CORRUPT;
 
+        // algorithmic bytes per kernel
         jd_stats& S = ctx->stats;
         const double entries = double(ctr[0]);
         const double blocks = double(P.total_blocks);
-        const double bytes[JD_NUM_KERNELS] = {P.rst_bytes, double(P.total_chunks) * 4 + double(P.seg_img.size()) * 4,
-                                              P.ecs_bytes + blocks * 8 + entries * 4,
-                                              blocks * 8 + entries * 4 + P.pixels * 3};
+        const double ecs = P.ecs_bytes;
+        const double bytes[JD_NUM_KERNELS] = {
+            ecs,                                               // scan: read the ECS once
+            double(P.total_chunks) * 12 + double(nseg) * 8,    // index: per-chunk counters, boundaries
+            2 * ecs,                                           // compact: read + write the ECS
+            ecs + blocks * 8 + entries * 4,                    // huffman: ECS in, sparse coefficients out
+            blocks * 8 + entries * 4 + P.pixels * 3};          // idct_color: coefficients in, RGB out
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
-            if (!active[k]) continue;
             S.launches[k]++;
             S.bytes[k] += bytes[k];
             if (timing) {
@@ -457,7 +486,7 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         S.pixels += P.pixels;
         S.ecs_bytes += P.ecs_bytes;
         S.blocks += blocks;
-        S.segments += double(P.seg_img.size());
+        S.segments += double(nseg);
     }
 
     // 3. results (and host copies when the caller asked for host output)
@@ -499,7 +528,7 @@ const char* jd_status_str(jd_status st) {
 }
 
 const char* jd_kernel_name(int k) {
-    static const char* names[JD_NUM_KERNELS] = {"k_rst_scan", "k_rst_index", "k_huffman", "k_idct_color"};
+    static const char* names[JD_NUM_KERNELS] = {"k_scan", "k_index", "k_compact", "k_huffman", "k_idct_color"};
     return (k >= 0 && k < JD_NUM_KERNELS) ? names[k] : "?";
 }
 
@@ -532,7 +561,7 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_pos, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output})
+    for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_brk, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output, &ctx->comp})
         if (b->p) (void)hipFree(b->p);
     for (PinBuf* b : {&ctx->plan_host, &ctx->input_host})
         if (b->p) (void)hipHostFree(b->p);

@@ -28,8 +28,8 @@ JD_ERR_NOMEM = 6
 JD_ERR_CAPACITY = 7
 JD_ERR_IO = 8
 JD_FLAG_TIMING = 1
-JD_NUM_KERNELS = 4
-KERNEL_NAMES = ["k_rst_scan", "k_rst_index", "k_huffman", "k_idct_color"]
+JD_NUM_KERNELS = 5
+KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_huffman", "k_idct_color"]
 
 
 class JDError(RuntimeError):

@@ -124,8 +124,9 @@ jd_status jd_memcpy_h2d(jd_ctx* ctx, void* dst_dev, const void* src_host, size_t
 jd_status jd_memcpy_d2h(jd_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
 jd_status jd_synchronize(jd_ctx* ctx);
 
-/* Per-kernel timing (JD_FLAG_TIMING).  Kernels: 0 rst_scan, 1 rst_index, 2 huffman, 3 idct_color. */
-#define JD_NUM_KERNELS 4
+/* Per-kernel timing (JD_FLAG_TIMING).
+ * Kernels: 0 k_scan, 1 k_index, 2 k_compact, 3 k_huffman, 4 k_idct_color. */
+#define JD_NUM_KERNELS 5
 typedef struct jd_stats {
     int launches[JD_NUM_KERNELS];
     double total_ms[JD_NUM_KERNELS]; /* hipEvent time, summed over launches                     */

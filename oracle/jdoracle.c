@@ -185,8 +185,10 @@ static int parse(const uint8_t* d, size_t n, img_t* im) {
             if (f->h[c] > f->hmax) f->hmax = f->h[c];
             if (f->v[c] > f->vmax) f->vmax = f->v[c];
         }
+        /* sampling factors of 3 are rejected (the GPU path indexes samples with shifts) */
         for (int c = 0; c < f->ncomp; c++)
-            if (f->hmax % f->h[c] || f->vmax % f->v[c]) return JDO_ERR_UNSUPPORTED;
+            if (f->h[c] == 3 || f->v[c] == 3 || f->hmax % f->h[c] || f->vmax % f->v[c])
+                return JDO_ERR_UNSUPPORTED;
     }
     f->mcux = (f->width + 8 * f->hmax - 1) / (8 * f->hmax);
     f->mcuy = (f->height + 8 * f->vmax - 1) / (8 * f->vmax);

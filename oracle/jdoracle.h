@@ -6,7 +6,7 @@
  * cpu_baseline leg of bench.py.
  *
  * Parity pinning: the 4:4:4 / no-restart subset is pinned bit-exactly against the reference's own
- * ground truth (/root/reference/testing/ground_truth/*.array, digests in tests/golden/) and against
+ * ground truth (/root/reference/testing/ground_truth/NAME.array, digests in tests/golden/) and against
  * the reference C++ decoder compiled from its sources by oracle/Makefile (oracle/_ref/decoder).
  * The extension to other sampling factors and restart intervals is NOT covered by the reference
  * (it decodes those to garbage); its semantics are defined in DESIGN.md §3 and are
