@@ -34,6 +34,47 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def rank_seed(rank: int, batch: int) -> int:
+    """First synthetic-image seed of a rank: ranks decode disjoint images (weak scaling)."""
+    return rank * batch
+
+
+def gather_counters(local, world: int):
+    """One all-gather of the per-rank [elapsed, pixels, images, ecs bytes, file bytes] counters
+    (RCCL over xGMI on the GPU box, gloo in tests/test_dist.py).  Returns (max elapsed, sums)."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        allc = [torch.zeros_like(local) for _ in range(world)]
+        dist.all_gather(allc, local)
+        allc = torch.stack(allc).cpu().numpy()
+    else:
+        allc = local.cpu().numpy()[None]
+    return float(allc[:, 0].max()), tuple(float(allc[:, k].sum()) for k in range(1, allc.shape[1]))
+
+
+def cpu_baseline(hosts, hdrs, n_req: int, target_s: float = 12.0):
+    """The oracle (CPU restatement of the reference decoder, full decode to RGB) on one core over a
+    bounded sample of the same workload: n_req images, or (n_req < 0) as many as take ~target_s."""
+    import jdoracle
+
+    n = len(hosts)
+    if n_req < 0:
+        probe = min(n, 4)
+        secs, _, _ = jdoracle.decode_many(hosts[:probe], threads=1, want_rgb=True)
+        n_req = int(max(probe, min(n, target_s / max(secs / probe, 1e-6))))
+    n_req = min(n_req, n)
+    secs, st, _ = jdoracle.decode_many(hosts[:n_req], threads=1, want_rgb=True)
+    if any(st):
+        raise SystemExit(f"oracle failed on the CPU sample: {sorted(set(st))}")
+    cpx = float(sum(h.width * h.height for h in hdrs[:n_req]))
+    return {"value": cpx / secs / 1e6, "unit": "MPixels/s", "cores": 1, "kind": "port",
+            "sample": f"first {n_req} of the workload's images decoded to RGB by oracle/liboracle.so "
+                      f"(bit-serial Huffman, reference IDCT + colour), 1 thread, {secs:.2f} s",
+            "images_per_s": n_req / secs}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,6 +85,8 @@ def main():
     ap.add_argument("--quality", type=int, default=90)
     ap.add_argument("--cpu-sample", type=int, default=-1, help="images for the CPU baseline (-1 auto, 0 off)")
     ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact vs the oracle")
+    ap.add_argument("--path", default="auto", choices=["auto", "sync", "lanes"],
+                    help="entropy-decode path (auto: lanes for images with restart intervals)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -66,7 +109,7 @@ def main():
     W, H, ss, rrows, batch, desc = CONFIGS[args.config]
     if args.batch:
         batch = args.batch
-    seed0 = rank * batch  # disjoint images per rank: shard by image
+    seed0 = rank_seed(rank, batch)  # disjoint images per rank: shard by image
     t_gen = time.time()
     datas = jd_synth.make_batch(batch, W, H, args.quality, "4:2:0" if ss == "mixed" else ss, rrows, 0, seed0,
                                 mixed=(ss == "mixed"))
@@ -90,7 +133,7 @@ def main():
     jpeg_dev.copy_(torch.from_numpy(flat))
     torch.cuda.synchronize(dev)
 
-    dec = jdamd.Decoder(local_rank, timing=True)
+    dec = jdamd.Decoder(local_rank, timing=True, path=args.path)
     prepared = dec.make_batch(hosts, [jpeg_dev.data_ptr() + o for o in in_offs],
                               [rgb_dev.data_ptr() + o for o in out_offs])
     pixels = float(sum(h.width * h.height for h in hdrs))
@@ -132,14 +175,7 @@ def main():
     # one all-gather of per-rank counters (RCCL over xGMI when N > 1)
     local = torch.tensor([elapsed, pixels * args.steps, batch * args.steps, ecs * args.steps,
                           jpeg_bytes * args.steps], dtype=torch.float64, device=dev)
-    if world > 1:
-        allc = [torch.zeros_like(local) for _ in range(world)]
-        dist.all_gather(allc, local)
-        allc = torch.stack(allc).cpu().numpy()
-    else:
-        allc = local.cpu().numpy()[None]
-    t_max = float(allc[:, 0].max())
-    tot_px, tot_img, tot_ecs, tot_bytes = (float(allc[:, k].sum()) for k in (1, 2, 3, 4))
+    t_max, (tot_px, tot_img, tot_ecs, tot_bytes) = gather_counters(local, world)
 
     if rank == 0:
         kern = st["kernels"]
@@ -149,17 +185,8 @@ def main():
         per_launch_bytes = kd["bytes"] / max(1, kd["launches"])
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         cpu = None
-        n_cpu = args.cpu_sample if args.cpu_sample >= 0 else max(1, min(batch, 24))
-        if n_cpu:
-            import jdoracle
-
-            sample = hosts[:n_cpu]
-            secs, cst, _ = jdoracle.decode_many(sample, threads=1)
-            cpx = float(sum(h.width * h.height for h in hdrs[:n_cpu]))
-            cpu = {"value": cpx / secs / 1e6, "unit": "MPixels/s", "cores": 1, "kind": "port",
-                   "sample": f"{n_cpu} of the workload's images, oracle/liboracle.so (bit-serial Huffman, "
-                             f"reference IDCT/colour), 1 thread, {secs:.2f} s",
-                   "images_per_s": n_cpu / secs}
+        if args.cpu_sample:
+            cpu = cpu_baseline(hosts, hdrs, args.cpu_sample)
         res = {
             "metric": "MPixels/s decoded (and images/s) at 1/2/4/8 MI355X; % HBM roofline",
             "value": tot_px / t_max / 1e6,
@@ -175,7 +202,8 @@ def main():
             "data": f"synthetic (seeded sinusoid + noise, Pillow baseline encode q{args.quality}, std Huffman)",
             "config": {"workload": desc, "config": args.config, "images_per_rank": batch,
                        "global_batch": batch * world, "width": W, "height": H, "subsampling": ss,
-                       "restart_rows": rrows, "parallelism": f"dp{world} (image sharding)"},
+                       "restart_rows": rrows, "parallelism": f"dp{world} (image sharding)",
+                       "entropy_path": args.path},
             "images_per_s": tot_img / t_max,
             "jpeg_MB_per_s": tot_bytes / t_max / 1e6,
             "ecs_MB_per_s": tot_ecs / t_max / 1e6,

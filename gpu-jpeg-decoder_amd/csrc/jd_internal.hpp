@@ -59,6 +59,7 @@ struct alignas(16) ImgDesc {
     uint64_t block_base;              // first global block index
     uint32_t tableset;
     uint32_t chunk_base, nchunks;     // 16 KiB scan chunks of this image's ECS
+    uint32_t sub_base, sub_cap;       // this image's range in the subsequence list (upper bound)
     uint32_t tile_mcus;               // MCU columns per IDCT/colour tile (tile = 128 px wide)
     uint32_t tile_mrows;              // MCU rows per tile (2 when an MCU is 8 px tall)
     uint32_t tiles_x, tiles_y;        // tiles per image row / column
@@ -67,7 +68,7 @@ struct alignas(16) ImgDesc {
     uint16_t qslot[4];                // quant table of each component (index into batch Q array)
     uint8_t comp_block0[4];           // first MCU block of each component
     uint8_t shx[4], shy[4];           // log2(hmax / h[c]), log2(vmax / v[c])
-    uint32_t pad[3];
+    uint32_t pad[1];
 };
 
 // Per-block result of the Huffman kernel (sparse coefficient representation):
@@ -89,6 +90,31 @@ struct Break {
 
 constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
 
+// Self-synchronising decode: every restart interval (segment) is cut into subsequences of
+// kSubBits bits of un-stuffed data, one lane each (reference:
+// parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208).  A decoder state is
+//   p  : segment-relative bit position of the next symbol
+//   sk : (bi << 16) | (k << 8) | ncur   — block-in-MCU, coefficient index (0 = DC next),
+//        AC entries already emitted for the current block
+constexpr int kSubBits = 512;
+struct SubState {
+    uint32_t p;
+    uint32_t sk;
+};
+struct SubCount {  // decoded from a subsequence's true entry state
+    uint32_t blocks;   // DC symbols (block starts)
+    uint32_t entries;  // non-zero AC entries
+    int32_t dc[3];     // sum of DC differences per component
+    uint32_t pad;
+};
+struct SubEntry {  // verified entry state + prefix sums within the segment
+    uint32_t p, sk;
+    uint32_t blk;      // segment-relative index of the next block to start
+    uint32_t ent;      // global index of the next AC entry
+    int32_t pred[3];   // DC predictors
+    uint32_t pad;
+};
+
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;
 constexpr int kScanBytesPerThread = 64;
@@ -96,6 +122,10 @@ constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
 constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cannot hold more
 
 constexpr int kHuffThreads = 256;
+constexpr int kSegThreads = 64;  // k_seg workgroup: one lane per restart interval
+// An image is decoded interval-per-lane (k_seg) when it has at least this many restart
+// intervals; otherwise (no DRI, or very long intervals) by the self-synchronising passes.
+constexpr uint32_t kMinLaneSegments = 4;
 constexpr int kIdctThreads = 256;
 constexpr int kTileWidth = 128;     // pixels per IDCT/colour tile row
 constexpr int kTileMaxBlocks = 96;  // blocks staged in LDS per IDCT/colour tile
@@ -112,13 +142,26 @@ struct BatchDev {
     const TableSet* tablesets;
     const uint16_t* qtabs;        // 64 x uint16 per quant table, zig-zag order
     // segments (restart intervals)
-    const uint32_t* seg_img;      // image of each segment (kInvalidImage = padding)
+    const uint32_t* seg_img;      // image of each segment
     uint32_t* seg_cstart;         // first un-stuffed byte of each segment (image-relative)
     uint32_t* seg_cend;           // end of each segment's data (image-relative, un-stuffed)
     const uint32_t* seg_entry;    // first AC-entry slot of each segment
-    uint32_t nseg;                // including padding, multiple of kHuffThreads
-    const uint32_t* wg_tableset;  // table set of each Huffman workgroup
-    uint32_t max_slots;           // LUT slots staged per Huffman workgroup
+    uint32_t* seg_sub_base;       // first subsequence of each segment
+    uint32_t* seg_nsub;           // subsequences of each segment
+    uint32_t nseg;
+    // subsequences
+    uint32_t* sub_seg;            // segment of each subsequence (kInvalidImage = unused)
+    uint32_t nsub;                // multiple of kHuffThreads
+    const uint32_t* wg_tableset;  // table set of each decode workgroup (kHuffThreads subsequences)
+    uint32_t max_slots;           // LUT slots staged per decode workgroup
+    SubState* exit_spec;          // pass 0 exits (speculative entries)
+    SubState* exit_cnt;           // pass 1 exits
+    SubCount* sub_cnt;            // pass 1 counts
+    SubEntry* sub_entry;          // chain output
+    // restart-interval lanes (images with DRI, decoded by k_seg)
+    const uint32_t* seg_lane;     // segment of each lane (kInvalidImage = padding)
+    uint32_t nseg_lane;           // multiple of kSegThreads
+    const uint32_t* lane_wg_tableset;  // table set of each k_seg workgroup
     // scan / compaction
     uint32_t max_chunks;
     uint32_t* chunk_nbrk;         // breaks per chunk
@@ -128,6 +171,7 @@ struct BatchDev {
     // outputs
     BlockInfo* blocks;
     uint32_t* entries;
+    uint64_t entries_cap;         // entry slots allocated
     uint32_t* status;             // per image
     unsigned long long* counters; // [0] AC entries written
     uint32_t max_tiles;

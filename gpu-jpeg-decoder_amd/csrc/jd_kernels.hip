@@ -4,13 +4,16 @@
 //   k_index       one wave per image: chunk offsets in the un-stuffed stream, restart-interval
 //                 (segment) boundaries, RSTn order / count checks
 //   k_compact     16 KiB per workgroup: drops the stuffed 00 after every FF (byte compaction)
-//   k_huffman     one lane per restart interval: Huffman + DPCM/RLE -> sparse coefficients
+//   k_subplan / k_decode<0,1,2> / k_chain
+//                 self-synchronising Huffman + DPCM/RLE decode, one lane per 512-bit
+//                 subsequence of a restart interval -> sparse coefficients (Stage 3 below)
 //   k_idct_color  one workgroup per 128-px tile: dequant + integer IDCT (LDS tile) + replicate
 //                 chroma upsample + YCbCr->RGB -> uint8 HWC
 //
 // Arithmetic follows the reference CPU decoder bit for bit (cpp-decoder/src/idct.cpp,
 // utils/color.cpp); the restatement used as checker lives in oracle/ (tests only).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "jd_kernels.hpp"
 
@@ -277,27 +280,33 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Stage 3: Huffman decode.  One lane owns one restart interval (segment) and walks it symbol by
-// symbol in a single flattened loop (DC and AC steps share one body, so lanes of a wave never
-// wait for each other's blocks).
-//
-// Memory discipline: the decode steps contain NO global loads.  gfx950 counts stores and loads
-// on one vmcnt, so any wait for a bitstream load inside the divergent step would also wait for
-// every coefficient store in flight — and with 64 lanes some lane needs new bytes almost every
-// step.  Each lane's (already un-stuffed) bitstream lives in a 128-byte LDS ring (layout
-// [word][lane]: a lane always hits bank lane%32, conflict-free), refilled in a wave-uniform
-// service phase every kRound steps: a service commits the 64 bytes loaded by the previous service
-// and issues the next load, so every load has a full round to land.  Ring words are stored
-// byte-swapped (MSB-first), so a symbol's 32-bit window is two LDS reads and one funnel shift.
+// Stage 3: self-synchronising Huffman decode (the reference's parallelHuffManDecode idea,
+// cuda-decoder/src/parser.cu:132-208, re-planned for wave64): every restart interval (segment)
+// is cut into kSubBits-bit subsequences of un-stuffed data, one lane each.
+//   k_subplan   per image: subsequences of every segment
+//   k_decode<0> speculative pass: each lane decodes its subsequence from (its first bit, DC of
+//               block 0) — Huffman codes self-synchronise, so its exit state (first symbol
+//               starting in the next subsequence) is almost always the true one
+//   k_decode<1> count pass: from the predecessor's speculative exit; exit state + counts
+//               (blocks, AC entries, DC-difference sums)
+//   k_chain     per segment (one wave): a lane whose count-pass entry differs from its
+//               predecessor's count-pass exit is re-decoded (rare), then prefix sums give every
+//               subsequence its block index, entry offset and DC predictors
+//   k_decode<2> write pass: from the verified entry, BlockInfo + AC entries out
+// A lane's subsequence (plus the overlap for a symbol that crosses its end) is loaded once into
+// its own LDS row — the decode steps do no global loads, so no s_waitcnt on stores ever stalls
+// a step (gfx950 counts loads and stores on one vmcnt).  Rows are byte-swapped (MSB-first) so a
+// symbol's 32-bit window is two LDS reads and one funnel shift; rows are [lane][word] with an odd
+// pitch (25 words), so 32 lanes reading the same word index hit 32 different banks.
 // ------------------------------------------------------------------------------------------
-constexpr int kRingWords = 32;  // per-lane ring: 128 bytes (+1 mirror word for wrap reads)
-constexpr int kRingBytes = kRingWords * 4;
-constexpr int kFillBytes = 64;  // bytes fetched per lane per service
-constexpr int kRound = 8;       // decode steps between services (<= 32 bytes consumed)
+constexpr int kSubBytes = kSubBits / 8;
+constexpr int kSubBufWords = 24;  // 96 bytes: subsequence + 16-byte misalignment + crossing symbol
+constexpr int kSubStride = 25;
+constexpr int kSubMaxBit = (kSubBufWords - 2) * 32;  // last bit position a peek may start at
 
 __device__ __forceinline__ u32x4 load16(uintptr_t a, uintptr_t last) {
-    // Unconditional (no phi with a fill value, so hipcc does not wait at issue); clamped to the
-    // image's last mapped 16-byte chunk.  Bytes past a segment's end are never consumed as data.
+    // clamped to the image's last mapped 16-byte chunk; bytes past a segment's end are never
+    // consumed as data, so what a clamped load returns there is irrelevant
     return *reinterpret_cast<gu32x4*>(a < last ? a : last);
 }
 
@@ -305,47 +314,6 @@ __device__ __forceinline__ int extend(uint32_t v, int s) {  // utils/stream.cpp:
     if (s == 0) return 0;
     const int l = 1 << (s - 1);
     return int(v) >= l ? int(v) : int(v) - ((l << 1) - 1);
-}
-
-struct Lane {
-    int bitpos;    // next bit (relative to the lane's 16-byte aligned base)
-    int wr;        // ring holds bytes [.., wr)
-    int req;       // loads issued up to base + req
-    bool pending;  // q0..q3 hold bytes [wr, wr + 64) in flight
-};
-
-__device__ __forceinline__ void service(Lane& L, uint32_t* ring, u32x4& q0, u32x4& q1, u32x4& q2, u32x4& q3,
-                                        uintptr_t base, uintptr_t last, bool active) {
-    if (L.pending) {
-        const int w = (L.wr >> 2) & (kRingWords - 1);  // wr is a multiple of 64: no wrap inside
-        uint32_t* r = ring + w * kHuffThreads;
-        r[0 * kHuffThreads] = __builtin_bswap32(q0.x);
-        r[1 * kHuffThreads] = __builtin_bswap32(q0.y);
-        r[2 * kHuffThreads] = __builtin_bswap32(q0.z);
-        r[3 * kHuffThreads] = __builtin_bswap32(q0.w);
-        r[4 * kHuffThreads] = __builtin_bswap32(q1.x);
-        r[5 * kHuffThreads] = __builtin_bswap32(q1.y);
-        r[6 * kHuffThreads] = __builtin_bswap32(q1.z);
-        r[7 * kHuffThreads] = __builtin_bswap32(q1.w);
-        r[8 * kHuffThreads] = __builtin_bswap32(q2.x);
-        r[9 * kHuffThreads] = __builtin_bswap32(q2.y);
-        r[10 * kHuffThreads] = __builtin_bswap32(q2.z);
-        r[11 * kHuffThreads] = __builtin_bswap32(q2.w);
-        r[12 * kHuffThreads] = __builtin_bswap32(q3.x);
-        r[13 * kHuffThreads] = __builtin_bswap32(q3.y);
-        r[14 * kHuffThreads] = __builtin_bswap32(q3.z);
-        r[15 * kHuffThreads] = __builtin_bswap32(q3.w);
-        if (w == 0) ring[kRingWords * kHuffThreads] = __builtin_bswap32(q0.x);  // mirror word
-        L.wr += kFillBytes;
-    }
-    // the bytes requested now land at the next service over ring bytes [req-128, req-64)
-    L.pending = active && (L.req - ((L.bitpos >> 5) << 2) <= kRingBytes - kFillBytes);
-    const uintptr_t a = base + uintptr_t(L.req);
-    q0 = load16(a, last);
-    q1 = load16(a + 16, last);
-    q2 = load16(a + 32, last);
-    q3 = load16(a + 48, last);
-    if (L.pending) L.req += kFillBytes;
 }
 
 // One Huffman symbol (+ magnitude bits) from the 32-bit window `peek`: symbol, EXTENDed value,
@@ -384,112 +352,610 @@ __device__ __forceinline__ int decode_sym(uint32_t peek, const HuffLut* t, bool 
     return len + s;
 }
 
-__global__ __launch_bounds__(kHuffThreads) void k_huffman(BatchDev b) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
-    uint32_t* s_ring = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
+struct SegInfo {
+    uint64_t blk0;     // first global block of the segment
+    uint32_t nblk;     // blocks in the segment
+    uint32_t bits;     // un-stuffed data bits of the segment
+    uintptr_t data;    // address of the segment's first un-stuffed byte
+    uintptr_t last;    // last mapped 16-byte chunk of the image's un-stuffed region
+    uint32_t ent0;     // first AC-entry slot of the segment
+    uint32_t pattern, bpm;
+};
+
+__device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo& S) {
+    const ImgDesc& im = b.imgs[b.seg_img[s]];
+    const uint32_t k_seg = s - im.seg_base;
+    const uint32_t nmcu = im.mcux * im.mcuy;
+    const uint32_t ri = im.restart_interval;
+    const uint32_t mcu0 = ri ? k_seg * ri : 0u;
+    const uint32_t mcu1 = ri ? min(mcu0 + ri, nmcu) : nmcu;
+    const uint32_t cstart = b.seg_cstart[s];
+    const uint32_t cend = max(cstart, b.seg_cend[s]);
+    S.blk0 = im.block_base + uint64_t(mcu0) * im.bpm;
+    S.nblk = (mcu1 - mcu0) * im.bpm;
+    S.bits = (cend - cstart) * 8;
+    S.data = uintptr_t(im.comp) + cstart;
+    S.last = (uintptr_t(im.comp) + (im.len - im.ecs_off) + 63) & ~uintptr_t(15);
+    S.ent0 = b.seg_entry[s];
+    S.pattern = im.block_pattern;
+    S.bpm = im.bpm;
+}
+
+// Loads subsequence j of a segment into an LDS row (byte-swapped words).  Returns the row bit
+// offset of the subsequence's first bit.
+__device__ __forceinline__ int load_row(uint32_t* row, int stride, uintptr_t data, uint32_t j, uintptr_t last) {
+    const uintptr_t a = data + uintptr_t(j) * kSubBytes;
+    const uintptr_t a16 = a & ~uintptr_t(15);
+#pragma unroll
+    for (int q = 0; q < kSubBufWords / 4; q++) {
+        const u32x4 v = load16(a16 + 16 * q, last);
+        row[(4 * q + 0) * stride] = __builtin_bswap32(v.x);
+        row[(4 * q + 1) * stride] = __builtin_bswap32(v.y);
+        row[(4 * q + 2) * stride] = __builtin_bswap32(v.z);
+        row[(4 * q + 3) * stride] = __builtin_bswap32(v.w);
+    }
+    return int(a & 15) * 8;
+}
+
+__device__ __forceinline__ uint32_t pack_sk(int bi, int k, int ncur) {
+    return (uint32_t(bi) << 16) | (uint32_t(k) << 8) | uint32_t(ncur);
+}
+
+// The decode loop shared by all passes.  MODE 0: exit only; 1: exit + counts; 2: write.
+struct DecIn {
+    int bpos, bend;          // row bit positions: start, first position not decoded from
+    int bi, k, ncur;         // entry state
+    uint32_t blk, ent;       // MODE 2: next block index (segment-relative), next entry slot
+    int pred0, pred1, pred2; // MODE 2: DC predictors
+};
+struct DecOut {
+    int bpos, bi, k, ncur;
+    uint32_t nblocks, nent;
+    int dc0, dc1, dc2;
+    uint32_t blk;
+    bool bad;
+};
+
+template <int MODE>
+__device__ __forceinline__ void decode_run(const DecIn& in, const uint32_t* row, int stride, const HuffLut* luts,
+                                           const int (&dsl)[3], const int (&asl)[3], const SegInfo& S,
+                                           const BatchDev& b, DecOut& o) {
+    // Entry states are well-formed by construction; the clamps below only make garbage (corrupt
+    // streams) unable to index outside the row, the block range or the entry range.
+    int bpos = max(in.bpos, 0);
+    const int bend = min(in.bend, kSubMaxBit);
+    int bi = in.bi < int(S.bpm) ? in.bi : 0, k = min(in.k, 63), ncur = min(in.ncur, 63);
+    const uint32_t ent_end = S.ent0 + 63u * S.nblk;
+    int comp = int((S.pattern >> (2 * bi)) & 3u);
+    uint32_t nblocks = 0, nent = 0;
+    int dc0 = 0, dc1 = 0, dc2 = 0;
+    uint32_t blk = in.blk, ent = in.ent;
+    int p0 = in.pred0, p1 = in.pred1, p2 = in.pred2;
+    // MODE 2: a block entered mid-way was started by the predecessor
+    uint32_t blk_cur = blk - 1, ent_blk = ent - uint32_t(ncur);
+    int dc = comp == 0 ? p0 : (comp == 1 ? p1 : p2);
+    bool bad = false;
+    while (bpos < bend) {
+        if (MODE == 2 && k == 0 && blk >= S.nblk) break;  // segment complete
+        const int w = bpos >> 5;
+        const uint32_t w0 = row[w * stride];
+        const uint32_t w1 = row[(w + 1) * stride];
+        const uint32_t sh = uint32_t(bpos) & 31u;
+        const uint32_t al = __builtin_amdgcn_alignbit(w0, w1, 32u - sh);
+        const uint32_t peek = sh ? al : w0;
+        const bool is_dc = (k == 0);
+        const int slot = is_dc ? (comp == 0 ? dsl[0] : (comp == 1 ? dsl[1] : dsl[2]))
+                               : (comp == 0 ? asl[0] : (comp == 1 ? asl[1] : asl[2]));
+        int sym, val;
+        bpos += decode_sym(peek, &luts[slot], is_dc, sym, val, bad);
+        if (is_dc) {  // parser.cpp:106-111: DPCM
+            if (MODE == 1) {
+                nblocks++;
+                if (comp == 0) dc0 += val;
+                else if (comp == 1) dc1 += val;
+                else dc2 += val;
+            }
+            if (MODE == 2) {
+                const int pr = (comp == 0 ? p0 : (comp == 1 ? p1 : p2)) + val;
+                if (comp == 0) p0 = pr;
+                else if (comp == 1) p1 = pr;
+                else p2 = pr;
+                if (pr < -32768 || pr > 32767) bad = true;
+                dc = pr;
+                blk_cur = blk++;
+                ent_blk = ent;
+            }
+            k = 1;
+            ncur = 0;
+        } else if (sym == 0) {  // EOB: parser.cpp:117-119
+            k = 64;
+        } else {  // run/size: parser.cpp:122-133
+            k += sym >> 4;
+            if (k < 64) {
+                if (sym & 15) {
+                    ncur++;
+                    if (MODE == 1) nent++;
+                    if (MODE == 2) {
+                        if (ent < ent_end) b.entries[ent] = (uint32_t(val) << 16) | uint32_t(k);
+                        else bad = true;
+                        ent++;
+                    }
+                }
+                k++;
+            }
+        }
+        if (k >= 64) {
+            if (MODE == 2) {
+                if (blk_cur < S.nblk && ent <= ent_end)
+                    b.blocks[S.blk0 + blk_cur] =
+                        BlockInfo{ent_blk, (min(ent - ent_blk, 63u) << 16) | (uint32_t(dc) & 0xFFFFu)};
+                else
+                    bad = true;
+            }
+            bi = (bi + 1 == int(S.bpm)) ? 0 : bi + 1;
+            comp = int((S.pattern >> (2 * bi)) & 3u);
+            k = 0;
+        }
+    }
+    o.bpos = bpos;
+    o.bi = bi;
+    o.k = k;
+    o.ncur = ncur;
+    o.nblocks = nblocks;
+    o.nent = nent;
+    o.dc0 = dc0;
+    o.dc1 = dc1;
+    o.dc2 = dc2;
+    o.blk = blk;
+    o.bad = bad;
+}
+
+__device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads) {
     for (int slot = 0; slot < ts.nslots; slot++) {
         const uint4* src = reinterpret_cast<const uint4*>(b.luts + ts.lut[slot]);
         uint4* dst = reinterpret_cast<uint4*>(s_lut + slot);
-        for (int i = threadIdx.x; i < int(sizeof(HuffLut) / 16); i += kHuffThreads) dst[i] = src[i];
+        for (int i = threadIdx.x; i < int(sizeof(HuffLut) / 16); i += nthreads) dst[i] = src[i];
     }
-    __syncthreads();
+}
 
-    const uint32_t g = blockIdx.x * kHuffThreads + threadIdx.x;
-    const uint32_t ii = (g < b.nseg) ? b.seg_img[g] : kInvalidImage;
-    if (__all(ii == kInvalidImage)) return;  // whole wave is padding
-    const bool valid = ii != kInvalidImage;
-    const ImgDesc& im = b.imgs[valid ? ii : 0u];
-    uint32_t* ring = s_ring + threadIdx.x;
-
-    uint64_t gblk = 0, gend = 0;
-    uint32_t cstart = 0, cend = 0;
-    if (valid) {
-        const uint32_t k_seg = g - im.seg_base;
-        const uint32_t nmcu = im.mcux * im.mcuy;
-        const uint32_t ri = im.restart_interval;
-        const uint32_t mcu0 = ri ? k_seg * ri : 0u;
-        const uint32_t mcu1 = ri ? min(mcu0 + ri, nmcu) : nmcu;
-        cstart = b.seg_cstart[g];
-        cend = max(cstart, b.seg_cend[g]);
-        gblk = im.block_base + uint64_t(mcu0) * im.bpm;
-        gend = im.block_base + uint64_t(mcu1) * im.bpm;
-    }
-    const uintptr_t comp = valid ? uintptr_t(im.comp) : uintptr_t(b.imgs);
-    const uintptr_t last = valid ? ((comp + (im.len - im.ecs_off) + 63) & ~uintptr_t(15)) : (comp & ~uintptr_t(15));
-    const uintptr_t base = (comp + cstart) & ~uintptr_t(15);
-    const int bit0 = int((comp + cstart) & 15) * 8;
-    const int bit_end = bit0 + int(cend - cstart) * 8;
-
-    Lane L;
-    L.bitpos = bit0;
-    L.wr = 0;
-    L.req = 0;
-    L.pending = false;
-    u32x4 q0, q1, q2, q3;
-    service(L, ring, q0, q1, q2, q3, base, last, valid);
-    service(L, ring, q0, q1, q2, q3, base, last, valid);
-
-    const int d0 = ts.dc_slot[0], d1 = ts.dc_slot[1], d2 = ts.dc_slot[2];
-    const int a0 = ts.ac_slot[0], a1 = ts.ac_slot[1], a2 = ts.ac_slot[2];
-    const uint32_t pattern = im.block_pattern, bpm = im.bpm;
-    uint32_t bi = 0;
-    int comp_id = int(pattern & 3u);
-    int k = 0, p0 = 0, p1 = 0, p2 = 0, dc = 0;
-    const uint32_t ent_first = valid ? b.seg_entry[g] : 0u;
-    uint32_t ent = ent_first, ent0 = ent_first;
-    bool bad = false;
-
-    for (;;) {
-        const bool active = gblk < gend;
-        if (!__any(active)) break;
-        service(L, ring, q0, q1, q2, q3, base, last, active);
-        for (int it = 0; it < kRound; it++) {
-            if (gblk < gend && ((L.bitpos >> 5) << 2) + 8 <= L.wr) {
-                const int w = (L.bitpos >> 5) & (kRingWords - 1);
-                const uint32_t w0 = ring[w * kHuffThreads];
-                const uint32_t w1 = ring[(w + 1) * kHuffThreads];
-                const uint32_t sh = uint32_t(L.bitpos) & 31u;
-                const uint32_t al = __builtin_amdgcn_alignbit(w0, w1, 32u - sh);
-                const uint32_t peek = sh ? al : w0;
-                const bool is_dc = (k == 0);
-                const int slot = is_dc ? (comp_id == 0 ? d0 : (comp_id == 1 ? d1 : d2))
-                                       : (comp_id == 0 ? a0 : (comp_id == 1 ? a1 : a2));
-                int sym, val;
-                L.bitpos += decode_sym(peek, &s_lut[slot], is_dc, sym, val, bad);
-                if (is_dc) {  // parser.cpp:106-111: DPCM
-                    const int pr = (comp_id == 0 ? p0 : (comp_id == 1 ? p1 : p2)) + val;
-                    if (comp_id == 0) p0 = pr;
-                    else if (comp_id == 1) p1 = pr;
-                    else p2 = pr;
-                    if (pr < -32768 || pr > 32767) bad = true;
-                    dc = pr;
-                    ent0 = ent;
-                    k = 1;
-                } else if (sym == 0) {  // EOB: parser.cpp:117-119
-                    k = 64;
-                } else {  // run/size: parser.cpp:122-133
-                    k += sym >> 4;
-                    if (k < 64) {
-                        if (sym & 15) b.entries[ent++] = (uint32_t(val) << 16) | uint32_t(k);
-                        k++;
-                    }
-                }
-                if (k >= 64) {
-                    b.blocks[gblk] = BlockInfo{ent0, ((ent - ent0) << 16) | (uint32_t(dc) & 0xFFFFu)};
-                    gblk++;
-                    bi = (bi + 1 == bpm) ? 0u : bi + 1;
-                    comp_id = int((pattern >> (2 * bi)) & 3u);
-                    k = 0;
-                }
-            }
+// Per image (one wave): number of subsequences of every segment, segment -> subsequence map.
+__global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
+    const ImgDesc& im = b.imgs[blockIdx.x];
+    const int lane = threadIdx.x;
+    if (im.sub_cap == 0) {  // restart-interval image: decoded by k_seg
+        for (uint32_t k = lane; k < im.nseg; k += 64) {
+            b.seg_sub_base[im.seg_base + k] = 0;
+            b.seg_nsub[im.seg_base + k] = 0;
         }
+        return;
     }
+    uint32_t run = 0;
+    for (uint32_t k0 = 0; k0 < im.nseg; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        uint32_t n = 0;
+        if (k < im.nseg) {
+            const uint32_t s = im.seg_base + k;
+            const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
+            n = max(1u, ((ce - cs) * 8 + kSubBits - 1) / kSubBits);
+        }
+        const uint32_t incl = wave_incl_scan(n);
+        if (k < im.nseg) {
+            const uint32_t s = im.seg_base + k;
+            b.seg_sub_base[s] = im.sub_base + run + incl - n;
+            b.seg_nsub[s] = n;
+        }
+        run += __shfl(int(incl), 63, 64);
+    }
+    // n <= cap by construction (host bound: ceil(ECS bits / kSubBits) + nseg)
+    const uint32_t used = min(run, im.sub_cap);
+    for (uint32_t k = 0; k < im.nseg; k++) {
+        const uint32_t s = im.seg_base + k;
+        const uint32_t base = b.seg_sub_base[s] - im.sub_base, n = b.seg_nsub[s];
+        for (uint32_t u = lane; u < n; u += 64)
+            if (base + u < im.sub_cap) b.sub_seg[im.sub_base + base + u] = s;
+    }
+    for (uint32_t u = used + lane; u < im.sub_cap; u += 64) b.sub_seg[im.sub_base + u] = kInvalidImage;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kHuffThreads) void k_decode(BatchDev b) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
+    stage_luts(b, ts, s_lut, kHuffThreads);
+
+    const uint32_t u = blockIdx.x * kHuffThreads + threadIdx.x;
+    const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
+    const bool valid = s != kInvalidImage;
+    SegInfo S;
+    uint32_t j = 0, nsub = 1;
+    if (valid) {
+        seg_info(b, s, S);
+        j = u - b.seg_sub_base[s];
+        nsub = b.seg_nsub[s];
+    } else {
+        S.data = S.last = uintptr_t(b.imgs) & ~uintptr_t(15);
+        S.bits = 0;
+        S.nblk = 0;
+        S.blk0 = 0;
+        S.ent0 = 0;
+        S.pattern = 0;
+        S.bpm = 1;
+    }
+    uint32_t* row = s_rows + threadIdx.x * kSubStride;  // [lane][word], odd pitch: conflict-free
+    const int off0 = load_row(row, 1, S.data, j, S.last);
+    __syncthreads();
     if (!valid) return;
-    if (L.bitpos > bit_end) bad = true;  // consumed bits beyond the interval's data
-    if (bad) atomicOr(&b.status[ii], kStCorrupt);
-    atomicAdd(&b.counters[0], (unsigned long long)(ent - ent_first));
+
+    const bool last_sub = (j + 1 == nsub);
+    const int sub0 = int(j) * kSubBits;  // segment bit of the subsequence start
+    DecIn in;
+    in.blk = 0;
+    in.ent = 0;
+    in.pred0 = in.pred1 = in.pred2 = 0;
+    int p = 0, bi = 0, k = 0, ncur = 0;
+    if (MODE == 0) {
+        p = sub0;
+    } else if (MODE == 1) {
+        if (j > 0) {
+            const SubState e = b.exit_spec[u - 1];
+            p = int(e.p);
+            bi = int(e.sk >> 16);
+            k = int((e.sk >> 8) & 0xFFu);
+            ncur = int(e.sk & 0xFFu);
+        }
+    } else {
+        const SubEntry e = b.sub_entry[u];
+        p = int(e.p);
+        bi = int(e.sk >> 16);
+        k = int((e.sk >> 8) & 0xFFu);
+        ncur = int(e.sk & 0xFFu);
+        in.blk = e.blk;
+        in.ent = e.ent;
+        in.pred0 = e.pred[0];
+        in.pred1 = e.pred[1];
+        in.pred2 = e.pred[2];
+    }
+    // decode the symbols that start inside this subsequence (the last one: up to the data end;
+    // the write pass stops on the block count instead)
+    int end_bit = last_sub ? (MODE == 2 ? int(S.bits) + 64 : int(S.bits)) : sub0 + kSubBits;
+    in.bpos = p - sub0 + off0;
+    in.bend = end_bit - sub0 + off0;
+    in.bi = bi;
+    in.k = k;
+    in.ncur = ncur;
+    const int dsl[3] = {ts.dc_slot[0], ts.dc_slot[1], ts.dc_slot[2]};
+    const int asl[3] = {ts.ac_slot[0], ts.ac_slot[1], ts.ac_slot[2]};
+    DecOut o;
+    decode_run<MODE>(in, row, 1, s_lut, dsl, asl, S, b, o);
+    const uint32_t pexit = uint32_t(o.bpos - off0 + sub0);
+    if (MODE == 0) {
+        b.exit_spec[u] = SubState{pexit, pack_sk(o.bi, o.k, o.ncur)};
+    } else if (MODE == 1) {
+        b.exit_cnt[u] = SubState{pexit, pack_sk(o.bi, o.k, o.ncur)};
+        b.sub_cnt[u] = SubCount{o.nblocks, o.nent, {o.dc0, o.dc1, o.dc2}, 0u};
+    } else {
+        bool bad = o.bad;
+        if (last_sub && (o.blk != S.nblk || o.k != 0)) bad = true;  // data ran out before the last block
+        const bool finished_here = o.k == 0 && o.blk >= S.nblk && o.bpos > in.bpos;
+        if (finished_here) {
+            if (pexit > S.bits) bad = true;  // consumed bits past the interval's data
+            // after the last block only padding (< 1 byte) may precede the next RSTn: the
+            // oracle's restart looks for the marker right there (oracle/jdoracle.c br_restart)
+            const ImgDesc& im = b.imgs[b.seg_img[s]];
+            if (s + 1 < im.seg_base + im.nseg && (S.bits >> 3) > ((pexit + 7) >> 3)) bad = true;
+        }
+        if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 3a: restart-interval lanes (images with DRI).  One lane decodes one whole interval and
+// writes its blocks directly: within an interval the decoder state is known, so no
+// synchronisation passes are needed, and 4:2:0 MCU-phase ambiguity (which defeats cheap
+// self-synchronisation) never arises.
+//
+// The lane's bitstream streams through its own LDS row in windows of kWinAdv bytes.  A round
+// issues the loads of the NEXT window into registers, decodes every symbol that starts in the
+// current window, then commits the registers to the row.  The only vmcnt wait per round is that
+// commit, ~150 symbols after the loads were issued (gfx950 counts the coefficient stores on the
+// same counter, so waiting inside the symbol loop would stall on them).
+//
+// Row layout: word 0 = the word before the window (so a 32-bit peek at any bit is one funnel
+// shift of two adjacent words with no sh==0 special case), words 1.. = window bytes, MSB-first.
+// [lane][word] with an odd pitch: lanes reading the same word index hit distinct banks.
+//
+// Per symbol: 3 LDS reads (2 row words, 1 LUT entry), no global loads, branch-free value
+// extraction; table slots for DC/AC of every MCU block are packed 3 bits per block, so the
+// current table is two bit-field extracts away.
+// ------------------------------------------------------------------------------------------
+constexpr int kWinAdv = 128;                      // bytes a round advances
+constexpr int kWinLoads = kWinAdv / 16 + 1;       // 16-byte loads per window (advance + overlap)
+constexpr int kRowWords = 1 + 4 * kWinLoads;      // 37: odd pitch (word 36 unused)
+constexpr int kLutWords = int(sizeof(HuffLut) / 4);
+static_assert(kRowWords % 2 == 1, "row pitch must be odd");
+
+size_t seg_lds_bytes(uint32_t max_slots) {
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(kSegThreads) * kRowWords * 4;
+}
+
+// Canonical slow path (codes longer than kLutBits): the code length is kLutBits+1 plus the
+// number of left-justified limits <= v16 (F.2.2.3 restated), then the symbol from vals[].
+__device__ __forceinline__ uint32_t slow_code(const uint32_t* lut, uint32_t peek, uint32_t& sym, bool& bad) {
+    const HuffLut* t = reinterpret_cast<const HuffLut*>(lut);
+    const uint32_t v16 = peek >> 16;
+    uint32_t l = kLutBits + 1;
+#pragma unroll
+    for (int j = kLutBits + 1; j <= 16; j++) l += (v16 >= t->lim[j]) ? 1u : 0u;
+    if (l > 16) {
+        bad = true;
+        l = 16;
+    }
+    sym = t->vals[uint32_t(t->base[l] + int(v16 >> (16 - l))) & 255u];
+    return l;
+}
+
+template <int VARIANT>
+__global__ __launch_bounds__(kSegThreads) void k_seg(BatchDev b) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
+    const uint32_t* s_lutw = reinterpret_cast<const uint32_t*>(s_dyn);
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    const TableSet& ts = b.tablesets[b.lane_wg_tableset[blockIdx.x]];
+    stage_luts(b, ts, s_lut, kSegThreads);
+
+    const uint32_t s = b.seg_lane[blockIdx.x * kSegThreads + threadIdx.x];
+    const bool valid = s != kInvalidImage;
+    SegInfo S;
+    if (valid) {
+        seg_info(b, s, S);
+    } else {
+        S.data = S.last = uintptr_t(b.imgs) & ~uintptr_t(15);
+        S.bits = 0;
+        S.nblk = 0;
+        S.blk0 = 0;
+        S.ent0 = 0;
+        S.pattern = 0;
+        S.bpm = 1;
+    }
+    uint32_t dcp = 0, acp = 0;  // 3-bit table slot per MCU block
+    for (uint32_t q = 0; q < S.bpm && q < 10; q++) {
+        const uint32_t c = (S.pattern >> (2 * q)) & 3u;
+        dcp |= uint32_t(ts.dc_slot[c] & 7u) << (3 * q);
+        acp |= uint32_t(ts.ac_slot[c] & 7u) << (3 * q);
+    }
+    uint32_t* row = s_rows + threadIdx.x * kRowWords;  // window words 0 .. 4*kWinLoads-1
+    uintptr_t wa = S.data & ~uintptr_t(15);
+#pragma unroll
+    for (int q = 0; q < kWinLoads; q++) {
+        const u32x4 v = load16(wa + 16 * q, S.last);
+        row[4 * q + 0] = __builtin_bswap32(v.x);
+        row[4 * q + 1] = __builtin_bswap32(v.y);
+        row[4 * q + 2] = __builtin_bswap32(v.z);
+        row[4 * q + 3] = __builtin_bswap32(v.w);
+    }
+    // 64-bit bit buffer: the next symbol is always in its top 32 bits (nb >= 32 between steps).
+    // The word for the next refill is read one step ahead (nextw), so the only LDS latency on a
+    // symbol's critical path is its table lookup.
+    const uint32_t off = uint32_t(S.data & 15) * 8;
+    int rp = int(off >> 5);
+    uint64_t bb = ((uint64_t(row[rp]) << 32) | row[rp + 1]) << (off & 31);
+    int nb = 64 - int(off & 31);
+    rp += 2;
+    uint32_t nextw = row[rp];
+    int consumed = 0;
+    const int sbits = int(S.bits);
+    const uint32_t ent_end = S.ent0 + 63u * S.nblk;
+    BlockInfo* const bout = b.blocks + (S.blk0 - 1);  // bout[blk] after blk++ = this block
+    uint32_t* const eout = b.entries;
+    // decode state (critical path)
+    int k = 0, bi = 0;
+    uint32_t nblk_seen = 0;
+    // bookkeeping state (off the critical path) and the pending step it has not consumed yet
+    uint32_t ent = S.ent0, ent_blk = S.ent0, blk = 0;
+    int p0 = 0, p1 = 0, p2 = 0, dc = 0;
+    bool q_valid = false, q_dc = false, q_emit = false, q_fin = false;
+    int q_val = 0, q_k = 0;
+    uint32_t q_comp = 0;
+    bool bad = false;
+    bool active = valid && S.nblk > 0;
+    const int bpm = int(S.bpm);
+    // bookkeeping of one decoded symbol: DPCM (parser.cpp:106-111), AC entry, block record
+#define JD_SEG_BOOK()                                                                                          \
+    do {                                                                                                       \
+        const int pc0 = p0, pc1 = p1, pc2 = p2;                                                                \
+        const int pr = (q_comp == 0u ? pc0 : (q_comp == 1u ? pc1 : pc2)) + q_val;                              \
+        p0 = (q_dc && q_comp == 0u) ? pr : pc0;                                                                \
+        p1 = (q_dc && q_comp == 1u) ? pr : pc1;                                                                \
+        p2 = (q_dc && q_comp == 2u) ? pr : pc2;                                                                \
+        bad |= q_dc && (pr < -32768 || pr > 32767);                                                            \
+        dc = q_dc ? pr : dc;                                                                                   \
+        ent_blk = q_dc ? ent : ent_blk;                                                                        \
+        blk += q_dc ? 1u : 0u;                                                                                 \
+        const bool st_ = q_emit && ent < ent_end;                                                              \
+        if (VARIANT != 1 && st_) eout[ent] = (uint32_t(q_val) << 16) | uint32_t(q_k);                          \
+        bad |= q_emit && !st_;                                                                                 \
+        ent += st_ ? 1u : 0u;                                                                                  \
+        if (VARIANT != 1 && q_fin)                                                                             \
+            bout[blk] = BlockInfo{ent_blk, (min(ent - ent_blk, 63u) << 16) | (uint32_t(dc) & 0xFFFFu)};       \
+    } while (0)
+    while (true) {
+        const uintptr_t na = wa + kWinAdv;
+        u32x4 nx[kWinLoads];
+#pragma unroll
+        for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
+        while (active && rp <= kWinAdv / 4) {
+            // (1) table lookup for this symbol
+            const uint32_t peek = uint32_t(bb >> 32);
+            const bool is_dc = (k == 0);
+            const uint32_t slot = __builtin_amdgcn_ubfe(is_dc ? dcp : acp, uint32_t(3 * bi), 3u);
+            const uint32_t* lut = s_lutw + slot * kLutWords;
+            uint32_t e = lut[peek >> (32 - kLutBits)];
+            // (2) while it is in flight: bookkeeping of the previous symbol
+            if (q_valid) JD_SEG_BOOK();
+            // (3) decode
+            if ((e & 31u) == 0) {  // code longer than kLutBits (0.3 % of symbols)
+                uint32_t sy;
+                const uint32_t l = slow_code(lut, peek, sy, bad);
+                e = l | (sy << 8);
+            }
+            const uint32_t clen = e & 31u;
+            const uint32_t sym = __builtin_amdgcn_ubfe(e, 8u, 8u);
+            const uint32_t sz0 = is_dc ? sym : (sym & 15u);
+            bad |= sz0 > 16u;  // DC size beyond 16 bits: corrupt table/stream
+            const uint32_t sz = min(sz0, 16u);
+            const bool complete = (e & kLutFlagComplete) != 0;
+            const uint32_t L = complete ? clen : clen + sz;
+            const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - clen - sz, sz);  // width 0 -> 0
+            const uint32_t half = (1u << sz) >> 1;
+            const int v = int(mag) - (mag < half ? int(2 * half - 1) : 0);  // EXTEND, stream.cpp:44-52
+            // consume L bits, refill one word if fewer than 32 remain
+            bb <<= L;
+            nb -= int(L);
+            const bool need = nb < 32;
+            bb |= need ? (uint64_t(nextw) << (32 - nb)) : 0ull;
+            nb += need ? 32 : 0;
+            rp += need ? 1 : 0;
+            nextw = row[rp];
+            consumed += int(L);
+            // next decoder state (EOB / ZRL / run-size, parser.cpp:114-134)
+            const int knew = k + int(sym >> 4);
+            const int kn = is_dc ? 1 : (sym == 0 ? 64 : (knew < 64 ? knew + 1 : knew));
+            const bool fin = kn >= 64;
+            q_valid = true;
+            q_dc = is_dc;
+            q_comp = __builtin_amdgcn_ubfe(S.pattern, uint32_t(2 * bi), 2u);
+            q_val = complete ? (int32_t(e) >> 16) : v;
+            q_emit = !is_dc && (sym & 15u) != 0 && knew < 64;
+            q_k = knew;
+            q_fin = fin;
+            nblk_seen += is_dc ? 1u : 0u;
+            bi = fin ? (bi + 1 == bpm ? 0 : bi + 1) : bi;
+            k = fin ? 0 : kn;
+            bad |= consumed > sbits;  // consumed bits past the interval's data
+            active = !bad && !(fin && nblk_seen >= S.nblk);
+        }
+        if (__ballot(active) == 0) break;  // wave-uniform
+#pragma unroll
+        for (int q = 0; q < kWinLoads; q++) {
+            row[4 * q + 0] = __builtin_bswap32(nx[q].x);
+            row[4 * q + 1] = __builtin_bswap32(nx[q].y);
+            row[4 * q + 2] = __builtin_bswap32(nx[q].z);
+            row[4 * q + 3] = __builtin_bswap32(nx[q].w);
+        }
+        rp -= kWinAdv / 4;
+        wa = na;
+    }
+    if (q_valid) JD_SEG_BOOK();
+#undef JD_SEG_BOOK
+    if (!valid) return;
+    const uint32_t pexit = uint32_t(consumed);
+    if (S.nblk > 0 && !bad) {
+        if (blk != S.nblk || k != 0) bad = true;
+        // after the last block only padding (< 1 byte) may precede the next RSTn: the oracle's
+        // restart looks for the marker right there (oracle/jdoracle.c br_restart)
+        const ImgDesc& im = b.imgs[b.seg_img[s]];
+        if (s + 1 < im.seg_base + im.nseg && (S.bits >> 3) > ((pexit + 7) >> 3)) bad = true;
+    }
+    if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+    atomicAdd(&b.counters[0], (unsigned long long)(ent - S.ent0));
+}
+
+// Per segment (one wave): verify the subsequence chain, re-decode broken links, prefix sums.
+__global__ __launch_bounds__(64) void k_chain(BatchDev b) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
+    uint32_t* s_row = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    const uint32_t s = blockIdx.x;
+    const int lane = threadIdx.x;
+    SegInfo S;
+    seg_info(b, s, S);
+    const ImgDesc& im = b.imgs[b.seg_img[s]];
+    const TableSet& ts = b.tablesets[im.tableset];
+    const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
+    if (n == 0) return;  // interval decoded by k_seg
+    bool luts = false;
+    SubState carry{0u, 0u};  // true exit of the previous chunk's last subsequence
+    uint32_t blk_run = 0, ent_run = S.ent0;
+    int pr0 = 0, pr1 = 0, pr2 = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        const uint32_t j = c0 + lane;
+        const bool in = j < n;
+        const uint32_t u = base + j;
+        SubState ex = in ? b.exit_cnt[u] : SubState{0u, 0u};
+        SubCount ct = in ? b.sub_cnt[u] : SubCount{0u, 0u, {0, 0, 0}, 0u};
+        const SubState used = (in && j > 0) ? b.exit_spec[u - 1] : SubState{0u, 0u};
+        SubState te;  // true entry = true exit of the predecessor
+        te.p = uint32_t(__shfl_up(int(ex.p), 1, 64));
+        te.sk = uint32_t(__shfl_up(int(ex.sk), 1, 64));
+        if (lane == 0) te = (j == 0) ? SubState{0u, 0u} : carry;
+        bool mm = in && (te.p != used.p || te.sk != used.sk);
+        uint64_t mask = __ballot(mm);
+        while (mask) {
+            const int v = __builtin_ctzll(mask);
+            if (!luts) {  // wave-uniform
+                stage_luts(b, ts, s_lut, 64);
+                luts = true;
+            }
+            const uint32_t jv = c0 + uint32_t(v);
+            const uint32_t tp = uint32_t(__shfl(int(te.p), v, 64)), tsk = uint32_t(__shfl(int(te.sk), v, 64));
+            __syncthreads();
+            int off0 = 0;
+            if (lane == 0) off0 = load_row(s_row, 1, S.data, jv, S.last);
+            off0 = __shfl(off0, 0, 64);
+            __syncthreads();
+            const int sub0 = int(jv) * kSubBits;
+            const bool lastv = (jv + 1 == n);
+            DecIn din;
+            din.bpos = int(tp) - sub0 + off0;
+            din.bend = (lastv ? int(S.bits) : sub0 + kSubBits) - sub0 + off0;
+            din.bi = int(tsk >> 16);
+            din.k = int((tsk >> 8) & 0xFFu);
+            din.ncur = int(tsk & 0xFFu);
+            din.blk = din.ent = 0;
+            din.pred0 = din.pred1 = din.pred2 = 0;
+            const int dsl[3] = {ts.dc_slot[0], ts.dc_slot[1], ts.dc_slot[2]};
+            const int asl[3] = {ts.ac_slot[0], ts.ac_slot[1], ts.ac_slot[2]};
+            DecOut o;
+            decode_run<1>(din, s_row, 1, s_lut, dsl, asl, S, b, o);  // every lane: same result
+            const SubState nex{uint32_t(o.bpos - off0 + sub0), pack_sk(o.bi, o.k, o.ncur)};
+            if (lane == v) {
+                ex = nex;
+                ct = SubCount{o.nblocks, o.nent, {o.dc0, o.dc1, o.dc2}, 0u};
+                mm = false;
+            }
+            if (lane == v + 1) {
+                te = nex;
+                mm = in && (te.p != used.p || te.sk != used.sk);
+            }
+            if (v == 63) carry = nex;  // next chunk's lane 0 compares against it
+            mask = __ballot(mm);
+        }
+        // prefix sums over the chunk
+        const uint32_t ib = wave_incl_scan(ct.blocks), ie = wave_incl_scan(ct.entries);
+        const uint32_t i0 = wave_incl_scan(uint32_t(ct.dc[0])), i1 = wave_incl_scan(uint32_t(ct.dc[1])),
+                       i2 = wave_incl_scan(uint32_t(ct.dc[2]));
+        if (in) {
+            SubEntry e;
+            e.p = te.p;
+            e.sk = te.sk;
+            e.blk = blk_run + ib - ct.blocks;
+            e.ent = ent_run + ie - ct.entries;
+            e.pred[0] = pr0 + int(i0 - uint32_t(ct.dc[0]));
+            e.pred[1] = pr1 + int(i1 - uint32_t(ct.dc[1]));
+            e.pred[2] = pr2 + int(i2 - uint32_t(ct.dc[2]));
+            e.pad = 0;
+            b.sub_entry[u] = e;
+        }
+        blk_run += uint32_t(__shfl(int(ib), 63, 64));
+        ent_run += uint32_t(__shfl(int(ie), 63, 64));
+        pr0 += __shfl(int(i0), 63, 64);
+        pr1 += __shfl(int(i1), 63, 64);
+        pr2 += __shfl(int(i2), 63, 64);
+        const uint32_t cp = uint32_t(__shfl(int(ex.p), 63, 64)), csk = uint32_t(__shfl(int(ex.sk), 63, 64));
+        carry = SubState{cp, csk};
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -648,7 +1114,9 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
         const uint32_t comp = (im.block_pattern >> (2 * bb)) & 3u;
         const uint64_t gb = im.block_base + uint64_t((r0 + mr) * im.mcux + m0 + mi) * bpm + bb;
         const BlockInfo bi = b.blocks[gb];
-        const int cnt = int(bi.cnt_dc >> 16);
+        // a block of a corrupt stream may never have been written: never index past the entries
+        int cnt = min(int(bi.cnt_dc >> 16), 63);
+        if (uint64_t(bi.entry_start) + uint64_t(cnt) > b.entries_cap) cnt = 0;
         int* blk = s_coef + j * 64;
         if (sub == 0) blk[0] = int(int16_t(bi.cnt_dc & 0xFFFFu)) * s_q[comp][0];
         for (int i = int(sub); i < cnt; i += 4) {
@@ -772,12 +1240,29 @@ hipError_t launch_compact(const BatchDev& b, hipStream_t s) {
 }
 
 size_t huffman_lds_bytes(uint32_t max_slots) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(kRingWords + 1) * kHuffThreads * 4;
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(kSubStride) * kHuffThreads * 4;
 }
 
 hipError_t launch_huffman(const BatchDev& b, hipStream_t s) {
-    if (!b.nseg) return hipSuccess;
-    hipLaunchKernelGGL(k_huffman, dim3(b.nseg / kHuffThreads), dim3(kHuffThreads), huffman_lds_bytes(b.max_slots), s, b);
+    if (!b.nimg) return hipSuccess;
+    if (b.nseg_lane) {
+        static const int variant = getenv("JD_SEG_VARIANT") ? atoi(getenv("JD_SEG_VARIANT")) : 0;  // A/B experiments
+        if (variant == 1)
+            hipLaunchKernelGGL(k_seg<1>, dim3(b.nseg_lane / kSegThreads), dim3(kSegThreads), seg_lds_bytes(b.max_slots), s, b);
+        else
+            hipLaunchKernelGGL(k_seg<0>, dim3(b.nseg_lane / kSegThreads), dim3(kSegThreads), seg_lds_bytes(b.max_slots), s, b);
+    }
+    if (!b.nsub) return hipGetLastError();
+    const size_t lds = huffman_lds_bytes(b.max_slots);
+    const size_t lds_chain = size_t(b.max_slots) * sizeof(HuffLut) + size_t(kSubStride + 1) * 4;
+    // every slot not claimed by a segment (per-image slack, workgroup padding) must read invalid
+    hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_subplan, dim3(b.nimg), dim3(64), 0, s, b);
+    hipLaunchKernelGGL(k_decode<0>, dim3(b.nsub / kHuffThreads), dim3(kHuffThreads), lds, s, b);
+    hipLaunchKernelGGL(k_decode<1>, dim3(b.nsub / kHuffThreads), dim3(kHuffThreads), lds, s, b);
+    hipLaunchKernelGGL(k_chain, dim3(b.nseg), dim3(64), lds_chain, s, b);
+    hipLaunchKernelGGL(k_decode<2>, dim3(b.nsub / kHuffThreads), dim3(kHuffThreads), lds, s, b);
     return hipGetLastError();
 }
 

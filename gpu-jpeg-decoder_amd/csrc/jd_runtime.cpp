@@ -69,6 +69,10 @@ struct jd_ctx {
 
     std::vector<ParsedJpeg> parsed;
     std::vector<jd_status> pst;
+
+    // last batch (jd_debug_fetch)
+    BatchDev last{};
+    uint64_t last_blocks = 0, last_entries = 0;
 };
 
 namespace {
@@ -160,7 +164,8 @@ struct Plan {
     std::vector<TableSet> tablesets;
     std::vector<uint16_t> qtabs;
     std::vector<uint32_t> seg_img, seg_entry, wg_tableset;
-    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, max_slots = 1;
+    std::vector<uint32_t> seg_lane, lane_wg_tableset;  // k_seg lanes, grouped by table set
+    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, max_slots = 1, nsub = 0;
     uint64_t total_blocks = 0, total_entry_cap = 0, comp_bytes = 0;
     double pixels = 0, ecs_bytes = 0;
 };
@@ -301,32 +306,55 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         P.item_of_img.push_back(it);
         ts_of_img.push_back(ts);
     }
-    // segments grouped by table set; each Huffman workgroup sees exactly one table set
+    // segments in image order; subsequence ranges grouped by table set, so each decode workgroup
+    // (kHuffThreads subsequences) sees exactly one table set
+    uint64_t entry_cursor = 0;
+    for (size_t i = 0; i < P.imgs.size(); i++) {
+        ImgDesc& d = P.imgs[i];
+        d.seg_base = uint32_t(P.seg_img.size());
+        const uint32_t nmcu = d.mcux * d.mcuy;
+        for (uint32_t k = 0; k < d.nseg; k++) {
+            const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
+            const uint32_t m1 = d.restart_interval ? std::min(m0 + d.restart_interval, nmcu) : nmcu;
+            P.seg_img.push_back(uint32_t(i));
+            P.seg_entry.push_back(uint32_t(entry_cursor));
+            entry_cursor += uint64_t(m1 - m0) * d.bpm * 63;
+        }
+    }
     std::vector<uint32_t> order(P.imgs.size());
     for (size_t i = 0; i < order.size(); i++) order[i] = uint32_t(i);
     std::stable_sort(order.begin(), order.end(),
                      [&](uint32_t a, uint32_t b) { return ts_of_img[a] < ts_of_img[b]; });
-    uint64_t entry_cursor = 0;
+    // images with enough restart intervals: one k_seg lane per interval; the others are cut
+    // into subsequences for the self-synchronising passes
+    auto lane_mode = [&](const ImgDesc& d) {
+        if (ctx->flags & JD_FLAG_FORCE_SYNC) return false;
+        if (ctx->flags & JD_FLAG_FORCE_LANES) return true;
+        return d.restart_interval != 0 && d.nseg >= kMinLaneSegments;
+    };
+    uint64_t sub = 0;
     for (size_t oi = 0; oi < order.size();) {
         const int ts = ts_of_img[order[oi]];
-        for (; oi < order.size() && ts_of_img[order[oi]] == ts; oi++) {
-            ImgDesc& d = P.imgs[order[oi]];
-            d.seg_base = uint32_t(P.seg_img.size());
-            const uint32_t nmcu = d.mcux * d.mcuy;
-            for (uint32_t k = 0; k < d.nseg; k++) {
-                const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
-                const uint32_t m1 = d.restart_interval ? std::min(m0 + d.restart_interval, nmcu) : nmcu;
-                P.seg_img.push_back(order[oi]);
-                P.seg_entry.push_back(uint32_t(entry_cursor));
-                entry_cursor += uint64_t(m1 - m0) * d.bpm * 63;
+        size_t oj = oi;
+        for (; oj < order.size() && ts_of_img[order[oj]] == ts; oj++) {
+            ImgDesc& d = P.imgs[order[oj]];
+            d.sub_base = uint32_t(sub);
+            if (lane_mode(d)) {
+                d.sub_cap = 0;
+                for (uint32_t k = 0; k < d.nseg; k++) P.seg_lane.push_back(d.seg_base + k);
+            } else {
+                d.sub_cap = uint32_t((uint64_t(d.len - d.ecs_off) * 8 + kSubBits - 1) / kSubBits + d.nseg);
+                sub += d.sub_cap;
             }
         }
-        while (P.seg_img.size() % kHuffThreads) {
-            P.seg_img.push_back(kInvalidImage);
-            P.seg_entry.push_back(0);
-        }
-        while (P.wg_tableset.size() < P.seg_img.size() / kHuffThreads) P.wg_tableset.push_back(uint32_t(ts));
+        oi = oj;
+        sub = align_up(sub, kHuffThreads);
+        while (P.wg_tableset.size() < sub / kHuffThreads) P.wg_tableset.push_back(uint32_t(ts));
+        while (P.seg_lane.size() % kSegThreads) P.seg_lane.push_back(kInvalidImage);
+        while (P.lane_wg_tableset.size() < P.seg_lane.size() / kSegThreads) P.lane_wg_tableset.push_back(uint32_t(ts));
     }
+    if (sub > 0x7FFFFFFFull) return JD_ERR_CAPACITY;
+    P.nsub = uint32_t(sub);
     if (entry_cursor > 0xFFFFFFFFull) return JD_ERR_CAPACITY;
     P.total_entry_cap = entry_cursor;
     return JD_OK;
@@ -340,9 +368,10 @@ size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
     return off;
 }
 
-size_t reserve(std::vector<uint8_t>& blob, size_t bytes) {
-    const size_t off = align_up(blob.size(), 256);
-    blob.resize(off + std::max<size_t>(bytes, 16));
+// Device-only scratch laid out after the uploaded part: only the offset advances (no host bytes).
+size_t reserve(size_t& end, size_t bytes) {
+    const size_t off = align_up(end, 256);
+    end = off + std::max<size_t>(bytes, 16);
     return off;
 }
 
@@ -396,22 +425,33 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(ctx->comp.p);
         std::vector<uint8_t> blob;
         const size_t nseg = P.seg_img.size();
+        const size_t nsub = P.nsub;
         const size_t o_imgs = put(blob, P.imgs);
         const size_t o_ts = put(blob, P.tablesets);
         const size_t o_q = put(blob, P.qtabs);
         const size_t o_segimg = put(blob, P.seg_img);
         const size_t o_segent = put(blob, P.seg_entry);
         const size_t o_wgts = put(blob, P.wg_tableset);
+        const size_t o_lane = put(blob, P.seg_lane);
+        const size_t o_lanets = put(blob, P.lane_wg_tableset);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
         const size_t o_ctr = put(blob, std::vector<unsigned long long>(2, 0));
         const size_t upload = blob.size();
         // device-written scratch after the uploaded part (no initialisation needed)
-        const size_t o_cstart = reserve(blob, nseg * 4);
-        const size_t o_cend = reserve(blob, nseg * 4);
-        const size_t o_nbrk = reserve(blob, size_t(P.total_chunks) * 4);
-        const size_t o_drops = reserve(blob, size_t(P.total_chunks) * 4);
-        const size_t o_coff = reserve(blob, size_t(P.total_chunks) * 4);
-        HIPCHK(ctx, ensure_dev(ctx->plan, blob.size()));
+        size_t end = upload;
+        const size_t o_cstart = reserve(end, nseg * 4);
+        const size_t o_cend = reserve(end, nseg * 4);
+        const size_t o_nbrk = reserve(end, size_t(P.total_chunks) * 4);
+        const size_t o_drops = reserve(end, size_t(P.total_chunks) * 4);
+        const size_t o_coff = reserve(end, size_t(P.total_chunks) * 4);
+        const size_t o_ssb = reserve(end, nseg * 4);
+        const size_t o_sns = reserve(end, nseg * 4);
+        const size_t o_subseg = reserve(end, nsub * 4);
+        const size_t o_exs = reserve(end, nsub * sizeof(SubState));
+        const size_t o_exc = reserve(end, nsub * sizeof(SubState));
+        const size_t o_cnt = reserve(end, nsub * sizeof(SubCount));
+        const size_t o_sent = reserve(end, nsub * sizeof(SubEntry));
+        HIPCHK(ctx, ensure_dev(ctx->plan, end));
         HIPCHK(ctx, ensure_pin(ctx->plan_host, upload));
         memcpy(ctx->plan_host.p, blob.data(), upload);
         HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, ctx->plan_host.p, upload, hipMemcpyHostToDevice, s));
@@ -432,7 +472,18 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         b.seg_cend = reinterpret_cast<uint32_t*>(base + o_cend);
         b.seg_entry = reinterpret_cast<const uint32_t*>(base + o_segent);
         b.nseg = uint32_t(nseg);
+        b.seg_sub_base = reinterpret_cast<uint32_t*>(base + o_ssb);
+        b.seg_nsub = reinterpret_cast<uint32_t*>(base + o_sns);
+        b.sub_seg = reinterpret_cast<uint32_t*>(base + o_subseg);
+        b.nsub = uint32_t(nsub);
+        b.exit_spec = reinterpret_cast<SubState*>(base + o_exs);
+        b.exit_cnt = reinterpret_cast<SubState*>(base + o_exc);
+        b.sub_cnt = reinterpret_cast<SubCount*>(base + o_cnt);
+        b.sub_entry = reinterpret_cast<SubEntry*>(base + o_sent);
         b.wg_tableset = reinterpret_cast<const uint32_t*>(base + o_wgts);
+        b.seg_lane = reinterpret_cast<const uint32_t*>(base + o_lane);
+        b.nseg_lane = uint32_t(P.seg_lane.size());
+        b.lane_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_lanets);
         b.max_slots = P.max_slots;
         b.max_chunks = P.max_chunks;
         b.chunk_nbrk = reinterpret_cast<uint32_t*>(base + o_nbrk);
@@ -441,10 +492,14 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         b.chunk_brk = static_cast<Break*>(ctx->chunk_brk.p);
         b.blocks = static_cast<BlockInfo*>(ctx->blocks.p);
         b.entries = static_cast<uint32_t*>(ctx->entries.p);
+        b.entries_cap = ctx->entries.cap / 4;
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
         b.max_tiles = P.max_tiles;
 
+        ctx->last = b;
+        ctx->last_blocks = P.total_blocks;
+        ctx->last_entries = P.total_entry_cap;
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
         hipError_t (*launch[JD_NUM_KERNELS])(const BatchDev&, hipStream_t) = {
             launch_scan, launch_index, launch_compact, launch_huffman, launch_idct_color};
@@ -487,6 +542,7 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         S.ecs_bytes += P.ecs_bytes;
         S.blocks += blocks;
         S.segments += double(nseg);
+        S.subsequences += double(nsub);
     }
 
     // 3. results (and host copies when the caller asked for host output)
@@ -526,6 +582,8 @@ const char* jd_status_str(jd_status st) {
     }
     return "unknown status";
 }
+
+const char* jd_ctx_last_error(jd_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
 
 const char* jd_kernel_name(int k) {
     static const char* names[JD_NUM_KERNELS] = {"k_scan", "k_index", "k_compact", "k_huffman", "k_idct_color"};
@@ -695,6 +753,34 @@ jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out) {
 jd_status jd_reset_stats(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
     ctx->stats = jd_stats{};
+    return JD_OK;
+}
+
+jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* nbytes) {
+    if (!ctx || !nbytes) return JD_ERR_INVALID_ARG;
+    const BatchDev& b = ctx->last;
+    const void* src = nullptr;
+    size_t n = 0;
+    switch (what) {
+        case 0: src = b.blocks; n = ctx->last_blocks * sizeof(BlockInfo); break;
+        case 1: src = b.seg_cstart; n = size_t(b.nseg) * 4; break;
+        case 2: src = b.seg_cend; n = size_t(b.nseg) * 4; break;
+        case 3: src = b.seg_sub_base; n = size_t(b.nseg) * 4; break;
+        case 4: src = b.seg_nsub; n = size_t(b.nseg) * 4; break;
+        case 5: src = b.exit_spec; n = size_t(b.nsub) * sizeof(SubState); break;
+        case 6: src = b.exit_cnt; n = size_t(b.nsub) * sizeof(SubState); break;
+        case 7: src = b.sub_cnt; n = size_t(b.nsub) * sizeof(SubCount); break;
+        case 8: src = b.sub_entry; n = size_t(b.nsub) * sizeof(SubEntry); break;
+        case 9: src = b.sub_seg; n = size_t(b.nsub) * 4; break;
+        case 10: src = b.status; n = size_t(b.nimg) * 4; break;
+        case 11: src = b.entries; n = ctx->last_entries * 4; break;
+        default: return JD_ERR_INVALID_ARG;
+    }
+    *nbytes = n;
+    if (dst && src && n) {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, hipMemcpy(dst, src, std::min(n, cap), hipMemcpyDeviceToHost));
+    }
     return JD_OK;
 }
 

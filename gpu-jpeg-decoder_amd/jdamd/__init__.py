@@ -28,6 +28,9 @@ JD_ERR_NOMEM = 6
 JD_ERR_CAPACITY = 7
 JD_ERR_IO = 8
 JD_FLAG_TIMING = 1
+JD_FLAG_FORCE_SYNC = 2
+JD_FLAG_FORCE_LANES = 4
+PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES}
 JD_NUM_KERNELS = 5
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_huffman", "k_idct_color"]
 
@@ -65,7 +68,7 @@ class _Stats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_int * JD_NUM_KERNELS), ("total_ms", ctypes.c_double * JD_NUM_KERNELS),
                 ("bytes", ctypes.c_double * JD_NUM_KERNELS), ("batches", ctypes.c_double),
                 ("images", ctypes.c_double), ("pixels", ctypes.c_double), ("ecs_bytes", ctypes.c_double),
-                ("blocks", ctypes.c_double), ("segments", ctypes.c_double)]
+                ("blocks", ctypes.c_double), ("segments", ctypes.c_double), ("subsequences", ctypes.c_double)]
 
 
 # Every symbol include/jd.h and include/jd_test.h declare (checked by tests/test_abi.py).
@@ -73,7 +76,7 @@ EXPORTED_SYMBOLS = [
     "jd_ctx_create", "jd_ctx_destroy", "jd_parse", "jd_decode", "jd_decode_file", "jd_decode_batch",
     "jd_write_array", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
     "jd_memcpy_h2d", "jd_memcpy_d2h", "jd_synchronize", "jd_get_stats", "jd_reset_stats",
-    "jd_kernel_name", "jd_test_idct", "jd_test_color",
+    "jd_kernel_name", "jd_test_idct", "jd_test_color", "jd_debug_fetch", "jd_ctx_last_error",
 ]
 
 _lib = None
@@ -112,6 +115,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         "jd_kernel_name": (ctypes.c_char_p, [c_int]),
         "jd_test_idct": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
         "jd_test_color": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+        "jd_debug_fetch": (c_int, [c_void_p, c_int, c_void_p, c_size_t, ctypes.POINTER(c_size_t)]),
+        "jd_ctx_last_error": (ctypes.c_char_p, [c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -209,10 +214,10 @@ class Decoder:
     """One jd_ctx on one HIP device.  Mirrors the reference's allocate()/decode/clean() lifecycle
     (cuda-decoder/src/parser.cu:324-358, 577-700) as a context object."""
 
-    def __init__(self, device: int = 0, timing: bool = False, parse_threads: int = 0):
+    def __init__(self, device: int = 0, timing: bool = False, parse_threads: int = 0, path: str = "auto"):
         self.lib = load_library()
         self.ctx = ctypes.c_void_p()
-        opts = _Opts(JD_FLAG_TIMING if timing else 0, parse_threads)
+        opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path], parse_threads)
         st = self.lib.jd_ctx_create(ctypes.byref(self.ctx), device, ctypes.byref(opts))
         if st != JD_OK:
             raise JDError(st, "jd_ctx_create")
@@ -242,7 +247,7 @@ class Decoder:
         w, h = ctypes.c_int(), ctypes.c_int()
         st = self.lib.jd_decode(self.ctx, data, len(data), out.ctypes.data, 0, ctypes.byref(w), ctypes.byref(h))
         if st != JD_OK:
-            raise JDError(st, "jd_decode")
+            raise JDError(st, "jd_decode " + (self.last_error() if st == JD_ERR_HIP else ""))
         return out
 
     def decode_file(self, path: str) -> np.ndarray:
@@ -325,11 +330,32 @@ class Decoder:
             "kernels": {KERNEL_NAMES[k]: {"launches": s.launches[k], "total_ms": s.total_ms[k], "bytes": s.bytes[k]}
                         for k in range(JD_NUM_KERNELS)},
             "batches": s.batches, "images": s.images, "pixels": s.pixels, "ecs_bytes": s.ecs_bytes,
-            "blocks": s.blocks, "segments": s.segments,
+            "blocks": s.blocks, "segments": s.segments, "subsequences": s.subsequences,
         }
+
+    def last_error(self) -> str:
+        return (self.lib.jd_ctx_last_error(self.ctx) or b"").decode()
 
     def reset_stats(self) -> None:
         self.lib.jd_reset_stats(self.ctx)
+
+    DEBUG_ARRAYS = {"blocks": (0, np.uint32, 2), "seg_cstart": (1, np.uint32, 1), "seg_cend": (2, np.uint32, 1),
+                    "seg_sub_base": (3, np.uint32, 1), "seg_nsub": (4, np.uint32, 1), "exit_spec": (5, np.uint32, 2),
+                    "exit_cnt": (6, np.uint32, 2), "sub_cnt": (7, np.int32, 6), "sub_entry": (8, np.int32, 8),
+                    "sub_seg": (9, np.uint32, 1), "status": (10, np.uint32, 1), "entries": (11, np.uint32, 1)}
+
+    def debug_fetch(self, name: str) -> np.ndarray:
+        """Internal array of the most recent batch (white-box tests and debugging)."""
+        what, dt, width = self.DEBUG_ARRAYS[name]
+        n = ctypes.c_size_t()
+        st = self.lib.jd_debug_fetch(self.ctx, what, None, 0, ctypes.byref(n))
+        if st != JD_OK:
+            raise JDError(st, "jd_debug_fetch " + self.last_error())
+        out = np.empty(n.value // np.dtype(dt).itemsize, dt)
+        st = self.lib.jd_debug_fetch(self.ctx, what, out.ctypes.data, out.nbytes, ctypes.byref(n))
+        if st != JD_OK:
+            raise JDError(st, "jd_debug_fetch " + self.last_error())
+        return out.reshape(-1, width) if width > 1 else out
 
     def test_idct(self, zz_dequant: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(zz_dequant, dtype=np.int32).reshape(-1, 64)

@@ -43,6 +43,11 @@ typedef struct jd_ctx jd_ctx;
 
 /* jd_opts.flags */
 #define JD_FLAG_TIMING 1u /* record hipEvents around every kernel launch (jd_get_stats) */
+/* Entropy-decode path selection (default: images with >= 4 restart intervals are decoded one
+ * interval per lane, the others by the self-synchronising subsequence passes).  Results are
+ * identical either way; the flags exist so tests can drive each path over every input. */
+#define JD_FLAG_FORCE_SYNC 2u  /* every image through the self-synchronising passes */
+#define JD_FLAG_FORCE_LANES 4u /* every image one lane per interval (whole image if no DRI) */
 
 typedef struct jd_opts {
     unsigned flags;
@@ -116,6 +121,8 @@ jd_status jd_write_array(const char* path, const uint8_t* rgb, int width, int he
 
 const char* jd_status_str(jd_status st);
 int jd_abi_version(void);
+/* Text of the most recent HIP failure on this context ("" if none). */
+const char* jd_ctx_last_error(jd_ctx* ctx);
 
 /* Device-memory helpers for FFI callers that bring no allocator of their own (ctypes tests). */
 jd_status jd_device_alloc(jd_ctx* ctx, size_t bytes, void** dptr);
@@ -131,7 +138,7 @@ typedef struct jd_stats {
     int launches[JD_NUM_KERNELS];
     double total_ms[JD_NUM_KERNELS]; /* hipEvent time, summed over launches                     */
     double bytes[JD_NUM_KERNELS];    /* algorithmic bytes moved, summed          */
-    double batches, images, pixels, ecs_bytes, blocks, segments;
+    double batches, images, pixels, ecs_bytes, blocks, segments, subsequences;
 } jd_stats;
 jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out);
 jd_status jd_reset_stats(jd_ctx* ctx);

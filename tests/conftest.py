@@ -27,10 +27,21 @@ def golden():
     return entries
 
 
-@pytest.fixture(scope="session")
-def decoder():
+@pytest.fixture(scope="session", params=["auto", "sync", "lanes"])
+def decoder(request):
+    """A decoder per entropy-decode path: default selection, every image through the
+    self-synchronising passes, every image one lane per restart interval."""
     import jdamd
 
-    dec = jdamd.Decoder(0, timing=True)
+    dec = jdamd.Decoder(0, timing=True, path=request.param)
+    yield dec
+    dec.close()
+
+
+@pytest.fixture(scope="session")
+def sync_decoder():
+    import jdamd
+
+    dec = jdamd.Decoder(0, timing=True, path="sync")
     yield dec
     dec.close()

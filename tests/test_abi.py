@@ -1,0 +1,118 @@
+"""CPU tests of the C-ABI boundary (libjdamd.so): it loads, exports every symbol include/*.h
+declares, and its host-only entry points (jd_parse, jd_write_array, jd_status_str) behave like the
+reference's extract()/write().  No compute calls: there is no GPU here."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import jdamd
+import jdoracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def declared_functions():
+    names = set()
+    for h in ("jd.h", "jd_test.h"):
+        txt = open(os.path.join(INCLUDE, h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(jd_[a-z0-9_]+)\s*\(", txt))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = jdamd.load_library()
+    decl = declared_functions()
+    assert decl == set(jdamd.EXPORTED_SYMBOLS)
+    for name in decl:
+        assert hasattr(lib, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", jdamd.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (jd_[a-z0-9_]+)$", nm, flags=re.M))
+    assert decl <= exported
+    # nothing but the C ABI leaks out under the jd_ prefix, and no C++ mangled jd:: entry points
+    assert exported == decl
+
+
+def test_headers_compile_as_c():
+    with tempfile.TemporaryDirectory() as td:
+        src = os.path.join(td, "t.c")
+        with open(src, "w") as f:
+            f.write('#include "jd.h"\n#include "jd_test.h"\nint main(void){return jd_abi_version()==JD_ABI_VERSION?0:1;}\n')
+        lib_dir = os.path.dirname(jdamd.LIB_PATH)
+        exe = os.path.join(td, "t")
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", INCLUDE, src, "-L", lib_dir, "-ljdamd",
+                        "-Wl,-rpath," + lib_dir, "-o", exe], check=True)
+        assert subprocess.run([exe]).returncode == 0
+
+
+def test_status_strings():
+    lib = jdamd.load_library()
+    seen = set()
+    for st in range(9):
+        s = lib.jd_status_str(st).decode()
+        assert s and s not in seen
+        seen.add(s)
+    assert lib.jd_status_str(99)
+
+
+def test_parse_matches_golden_dimensions(golden):
+    for e in golden:
+        if e["status"] == 0:
+            h = jdamd.parse(e["data"])
+            assert (h.width, h.height) == (e["width"], e["height"]), e["file"]
+            assert h.ecs_offset < len(e["data"])
+            assert h.blocks_per_mcu == sum(h.h[c] * h.v[c] for c in range(h.ncomp)) or h.ncomp == 1
+        elif e["status"] in (3, 4):
+            with pytest.raises(jdamd.JDError) as ei:
+                jdamd.parse(e["data"])
+            assert ei.value.status == e["status"], e["file"]
+
+
+def test_parse_rejects_bad_input():
+    lib = jdamd.load_library()
+    h = jdamd._Header()
+    assert lib.jd_parse(None, 10, ctypes.byref(h)) == jdamd.JD_ERR_INVALID_ARG
+    assert lib.jd_parse(b"\xff\xd8", 2, None) == jdamd.JD_ERR_INVALID_ARG
+    assert lib.jd_parse(b"\x00\x00\x00\x00", 4, ctypes.byref(h)) != 0
+    d = open(os.path.join(ROOT, "tests", "golden", "ref", "1_320x240.jpg"), "rb").read()
+    assert lib.jd_parse(d[:60], 60, ctypes.byref(h)) == jdamd.JD_ERR_TRUNCATED
+
+
+def test_write_array_is_byte_identical_to_reference_ground_truth():
+    """jd_write_array(oracle RGB) reproduces the reference's own ground-truth .array file."""
+    ref_path = os.path.join(ROOT, "tests", "golden", "ref", "3_120x120.array")
+    st, rgb = jdoracle.decode(open(os.path.join(ROOT, "tests", "golden", "ref", "3_120x120.jpg"), "rb").read())
+    assert st == 0
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "o.array")
+        jdamd.write_array(out, rgb)
+        assert open(out, "rb").read() == open(ref_path, "rb").read()
+
+
+def test_context_creation_fails_cleanly_without_gpu():
+    """No GPU in this container: jd_ctx_create must return an error, never crash or fall back."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = jdamd.load_library()
+    ctx = ctypes.c_void_p()
+    st = lib.jd_ctx_create(ctypes.byref(ctx), 0, None)
+    assert st != jdamd.JD_OK and not ctx.value
+    with pytest.raises(jdamd.JDError):
+        jdamd.Decoder(0)
+
+
+def test_null_context_calls_are_rejected():
+    lib = jdamd.load_library()
+    assert lib.jd_ctx_destroy(None) in (jdamd.JD_OK, jdamd.JD_ERR_INVALID_ARG)
+    w, h = ctypes.c_int(), ctypes.c_int()
+    assert lib.jd_decode(None, b"\xff\xd8", 2, None, 0, ctypes.byref(w), ctypes.byref(h)) == jdamd.JD_ERR_INVALID_ARG
+    assert lib.jd_decode_batch(None, None, 1, None, 0, None) == jdamd.JD_ERR_INVALID_ARG
+    assert lib.jd_kernel_name(0).decode() == jdamd.KERNEL_NAMES[0]

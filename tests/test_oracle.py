@@ -1,0 +1,216 @@
+"""CPU tests: the oracle (oracle/liboracle.so) is pinned before anything is checked against it.
+
+  - reference ground truth (the reference's own testing/ground_truth .array files, as digests)
+  - the reference C++ decoder compiled from its sources (oracle/_ref/decoder), when present
+  - reference arithmetic: IDCT with the DC shortcuts vs the branch-free form the GPU uses,
+    colour conversion vs the GPU's exact fp32/integer restatement (exhaustive)
+  - restart-interval invariance and decoder-state invariants for the extension
+"""
+import hashlib
+import io
+import os
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+import jdoracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import jd_trace  # noqa: E402
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint8).tobytes()).hexdigest()
+
+
+def test_golden_digests(golden):
+    for e in golden:
+        st, rgb = jdoracle.decode(e["data"])
+        assert st == e["status"], e["file"]
+        if st == 0:
+            assert sha(rgb) == e["sha256"], e["file"]
+
+
+def test_reference_ground_truth_array_format():
+    """The committed .array fixture (reference ground truth) equals the oracle's RGB."""
+    arr = jdoracle.read_array(os.path.join(ROOT, "tests", "golden", "ref", "3_120x120.array"))
+    with open(os.path.join(ROOT, "tests", "golden", "ref", "3_120x120.jpg"), "rb") as f:
+        st, rgb = jdoracle.decode(f.read())
+    assert st == 0 and np.array_equal(arr, rgb)
+
+
+@pytest.mark.skipif(not jdoracle.ref_available(), reason="oracle/_ref/decoder not built")
+def test_oracle_vs_reference_decoder_random_444():
+    """Fresh 4:4:4 no-RST images (the reference's supported subset) through both decoders."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import jd_synth
+
+    rng = np.random.default_rng(123)
+    with tempfile.TemporaryDirectory() as td:
+        for i in range(6):
+            w, h = int(rng.integers(8, 300)), int(rng.integers(8, 300))
+            q = int(rng.choice([30, 60, 85, 95, 100]))
+            data = jd_synth.encode(jd_synth.synth_pixels(w, h, 1000 + i), q, "4:4:4", 0, 0, optimize=bool(i % 2))
+            p = os.path.join(td, f"r{i}.jpg")
+            with open(p, "wb") as f:
+                f.write(data)
+            ref = jdoracle.ref_decode(p, td)
+            st, got = jdoracle.decode(data)
+            assert st == 0 and np.array_equal(ref, got), (w, h, q)
+
+
+def _idct_branch_free(zz):
+    """The GPU's idct_row/idct_col (jd_kernels.hip) restated in numpy: no DC shortcuts, int32
+    wrap-around before every arithmetic shift (as the reference's `int` arithmetic)."""
+    nat = np.zeros_like(zz)
+    zzo = [0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24,
+           31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60, 21, 34, 37, 47, 50, 56,
+           59, 61, 35, 36, 48, 49, 57, 58, 62, 63]
+    nat[:] = zz[:, zzo]
+    b = nat.reshape(-1, 8, 8).astype(np.int64)
+    C1, C2, C3, C5, C6, C7 = 2841, 2676, 2408, 1609, 1108, 565
+
+    def wrap(x):
+        return ((x + 2**31) % 2**32) - 2**31
+
+    def one(v, row):
+        if row:
+            x1 = v[4] << 11
+            x0 = (v[0] << 11) + 128
+            r8 = lambda a: a  # noqa: E731
+            x8 = C7 * (v[1] + v[7])
+            x4 = x8 + (C1 - C7) * v[1]
+            x5 = x8 - (C1 + C7) * v[7]
+            x8 = C3 * (v[5] + v[3])
+            x6 = x8 - (C3 - C5) * v[5]
+            x7 = x8 - (C3 + C5) * v[3]
+            x1c = C6 * (v[2] + v[6])
+            x2 = x1c - (C2 + C6) * v[6]
+            x3 = x1c + (C2 - C6) * v[2]
+        else:
+            x1 = v[4] << 8
+            x0 = (v[0] << 8) + 8192
+            r8 = lambda a: wrap(a) >> 3  # noqa: E731
+            x8 = C7 * (v[1] + v[7]) + 4
+            x4 = r8(x8 + (C1 - C7) * v[1])
+            x5 = r8(x8 - (C1 + C7) * v[7])
+            x8 = C3 * (v[5] + v[3]) + 4
+            x6 = r8(x8 - (C3 - C5) * v[5])
+            x7 = r8(x8 - (C3 + C5) * v[3])
+            x1c = C6 * (v[2] + v[6]) + 4
+            x2 = r8(x1c - (C2 + C6) * v[6])
+            x3 = r8(x1c + (C2 - C6) * v[2])
+        x8 = x0 + x1
+        x0 = x0 - x1
+        x1 = x4 + x6
+        x4 = x4 - x6
+        x6 = x5 + x7
+        x5 = x5 - x7
+        x7 = x8 + x3
+        x8 = x8 - x3
+        x3 = x0 + x2
+        x0 = x0 - x2
+        x2 = wrap(181 * wrap(x4 + x5) + 128) >> 8
+        x4 = wrap(181 * wrap(x4 - x5) + 128) >> 8
+        sh = 8 if row else 14
+        out = [wrap(o) >> sh for o in (x7 + x1, x3 + x2, x0 + x4, x8 + x6, x8 - x6, x0 - x4, x3 - x2, x7 - x1)]
+        if not row:
+            out = [np.clip(o, -256, 255) for o in out]
+        return out
+
+    for r in range(8):
+        v = [b[:, r, c] for c in range(8)]
+        o = one(v, True)
+        for c in range(8):
+            b[:, r, c] = o[c]
+    for c in range(8):
+        v = [b[:, r, c] for r in range(8)]
+        o = one(v, False)
+        for r in range(8):
+            b[:, r, c] = o[r]
+    return b.reshape(-1, 64)
+
+
+def test_idct_shortcuts_equal_branch_free():
+    """Reference idct.cpp (with its DC-only shortcuts) == the branch-free form."""
+    rng = np.random.default_rng(5)
+    a = np.zeros((3000, 64), np.int32)
+    a[:1000, 0] = np.arange(-32000, 32000, 64)[:1000]
+    for k in range(1000, 2000):
+        n = rng.integers(0, 10)
+        a[k, rng.integers(0, 64, n)] = rng.integers(-2000, 2000, n)
+    a[2000:] = rng.integers(-1500, 1500, (1000, 64))
+    want = jdoracle.idct(a)
+    got = _idct_branch_free(a.astype(np.int64))
+    assert np.array_equal(got, want)
+
+
+def test_color_fast_path_exhaustive():
+    """The GPU colour arithmetic (fp32 FMA for R/B, integer G with an exact fallback window),
+    restated in numpy, equals utils/color.cpp over all 2^27 inputs."""
+    cb, cr = np.meshgrid(np.arange(-256, 256), np.arange(-256, 256), indexing="ij")
+    cb = cb.ravel().astype(np.int64)
+    cr = cr.ravel().astype(np.int64)
+    n = 202008 * cb + 419198 * cr
+    q = np.floor_divide(n, 587000)
+    rem = n - q * 587000
+    exact_g = (rem < 64) | (rem > 587000 - 64)
+    f32 = np.float32
+    bad = 0
+    for y in range(-256, 256):
+        yd = np.float64(y)
+        r = (cr * (2 - 2 * 0.299) + yd).astype(f32)
+        b = (cb * (2 - 2 * 0.114) + yd).astype(f32)
+        g = ((yd - 0.114 * b.astype(np.float64) - 0.299 * r.astype(np.float64)) / 0.587).astype(f32)
+        R = np.clip((r + f32(128)).astype(np.int32), 0, 255)
+        G = np.clip((g + f32(128)).astype(np.int32), 0, 255)
+        B = np.clip((b + f32(128)).astype(np.int32), 0, 255)
+        # fast path: R/B by fp32 FMA (numpy: product is exact in fp64, then one rounding to fp32)
+        rf = (cr.astype(np.float64) * np.float64(f32(1.402)) + yd).astype(f32)
+        bf = (cb.astype(np.float64) * np.float64(f32(1.772)) + yd).astype(f32)
+        Rf = np.clip((rf + f32(128)).astype(np.int32), 0, 255)
+        Bf = np.clip((bf + f32(128)).astype(np.int32), 0, 255)
+        Gf = np.where(exact_g, G, np.clip(y + 127 - q, 0, 255))
+        bad += int(((Rf != R) | (Bf != B) | (Gf != G)).sum())
+    assert bad == 0
+
+
+@pytest.mark.parametrize("ss", ["4:4:4", "4:2:2", "4:2:0"])
+def test_restart_interval_invariance(ss):
+    """DRI does not change coefficients, so every restart interval layout decodes identically."""
+    import jd_synth
+
+    px = jd_synth.synth_pixels(203, 117, 9)
+    base = jdoracle.decode(jd_synth.encode(px, 85, ss))[1]
+    for kw in ({"restart_rows": 1}, {"restart_blocks": 1}, {"restart_blocks": 7}):
+        st, rgb = jdoracle.decode(jd_synth.encode(px, 85, ss, kw.get("restart_rows", 0), kw.get("restart_blocks", 0)))
+        assert st == 0 and np.array_equal(rgb, base), kw
+
+
+def test_self_sync_emulation_matches_oracle(golden):
+    """The GPU's four-pass self-synchronising decode (spec -> count -> chain -> write), restated
+    in Python (tools/jd_trace.emulate), reproduces the oracle's coefficients exactly."""
+    for e in golden[:30]:
+        if e["status"] != 0:
+            continue
+        blocks, _ = jd_trace.emulate(e["data"])
+        st, coef = jdoracle.decode_coefs(e["data"])
+        assert len(blocks) == coef.shape[0], e["file"]
+        for i, (dc, ents) in enumerate(blocks):
+            got = np.zeros(64, np.int64)
+            got[0] = dc
+            for z, v in ents:
+                got[z] = v
+            assert np.array_equal(got, coef[i]), (e["file"], i)
+
+
+def test_corrupt_and_unsupported_statuses():
+    with open(os.path.join(ROOT, "tests", "golden", "ref", "5_200x200.jpg"), "rb") as f:
+        d = f.read()
+    assert jdoracle.decode(d[: len(d) // 2])[0] == 2          # truncated ECS -> overrun
+    assert jdoracle.decode(b"\xff\xd8\xff\xd9")[0] == 2       # EOI before SOS
+    assert jdoracle.decode(b"\x00\x01\x02\x03")[0] == 2       # no SOI
+    assert jdoracle.decode(d[:100])[0] == 4                   # ends inside the headers
