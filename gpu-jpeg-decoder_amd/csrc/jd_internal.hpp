@@ -60,8 +60,8 @@ struct alignas(16) ImgDesc {
     uint32_t tableset;
     uint32_t chunk_base, nchunks;     // 16 KiB scan chunks of this image's ECS
     uint32_t sub_base, sub_cap;       // this image's range in the subsequence list (upper bound)
-    uint32_t tile_mcus;               // MCU columns per IDCT/colour tile (tile = 128 px wide)
-    uint32_t tile_mrows;              // MCU rows per tile (2 when an MCU is 8 px tall)
+    uint32_t tile_mcus;               // MCU columns per IDCT/colour tile
+    uint32_t tile_mrows;              // MCU rows per tile (tile_mcus * tile_mrows * bpm <= 64)
     uint32_t tiles_x, tiles_y;        // tiles per image row / column
     uint32_t lg_mw, lg_mh;            // log2 of the MCU width / height in pixels
     uint8_t h[4], v[4];
@@ -126,9 +126,8 @@ constexpr int kSegThreads = 64;  // k_seg workgroup: one lane per restart interv
 // An image is decoded interval-per-lane (k_seg) when it has at least this many restart
 // intervals; otherwise (no DRI, or very long intervals) by the self-synchronising passes.
 constexpr uint32_t kMinLaneSegments = 4;
-constexpr int kIdctThreads = 256;
-constexpr int kTileWidth = 128;     // pixels per IDCT/colour tile row
-constexpr int kTileMaxBlocks = 96;  // blocks staged in LDS per IDCT/colour tile
+constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
+constexpr int kTileMaxBlocks = 64;   // blocks per IDCT/colour tile (one lane each)
 
 // Per-image status bits written by kernels (atomicOr); host maps them to jd_status.
 constexpr uint32_t kStCorrupt = 1u;     // bad code / overrun / DC range

@@ -98,15 +98,40 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     const uint32_t nextb = (t0 + 64 < fend) ? uint32_t(*reinterpret_cast<gu8*>(t0 + 64)) : 0u;
 
     uint32_t ndrop = 0, nbrk = 0;
+    if (t0 >= lo && t0 + 64 < fend) {
+        // interior thread: exact per-byte masks (high bit of each byte lane), 16 words at a time
+        //   ff[k]   : byte == 0xFF            zero[k]: byte == 0x00
+        //   drop    : 00 preceded by FF       brk    : FF followed by neither 00 nor FF
+        uint32_t ff[16], nz[16];
 #pragma unroll
-    for (int i = 0; i < 64; i++) {
-        const uint32_t by = byte_of(w, i);
-        const uint32_t pb = i ? byte_of(w, i - 1) : prevb;
-        const uint32_t nb = i < 63 ? byte_of(w, i + 1) : nextb;
-        const uintptr_t a = t0 + i;
-        const bool inr = a >= lo && a < fend;
-        ndrop += (inr && a > lo && by == 0x00u && pb == 0xFFu) ? 1u : 0u;
-        nbrk += (inr && a + 1 < fend && by == 0xFFu && nb != 0x00u && nb != 0xFFu) ? 1u : 0u;
+        for (int q = 0; q < 16; q++) {
+            const uint32_t x = w[q], t = ~x;
+            ff[q] = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+            const uint32_t zero = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+            nz[q] = ~(zero | ff[q]) & 0x80808080u;  // neither 00 nor FF
+        }
+        const uint32_t ffprev = (prevb == 0xFFu) ? 0x80u : 0u;            // byte before the thread
+        const uint32_t nznext = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;  // byte after it
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const uint32_t x = w[q];
+            const uint32_t zero = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+            const uint32_t pf = (ff[q] << 8) | (q ? (ff[q - 1] >> 24) : ffprev);
+            const uint32_t nn = (nz[q] >> 8) | ((q < 15 ? nz[q + 1] : nznext) << 24);
+            ndrop += __builtin_popcount(zero & pf);
+            nbrk += __builtin_popcount(ff[q] & nn);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 64; i++) {
+            const uint32_t by = byte_of(w, i);
+            const uint32_t pb = i ? byte_of(w, i - 1) : prevb;
+            const uint32_t nb = i < 63 ? byte_of(w, i + 1) : nextb;
+            const uintptr_t a = t0 + i;
+            const bool inr = a >= lo && a < fend;
+            ndrop += (inr && a > lo && by == 0x00u && pb == 0xFFu) ? 1u : 0u;
+            nbrk += (inr && a + 1 < fend && by == 0xFFu && nb != 0x00u && nb != 0xFFu) ? 1u : 0u;
+        }
     }
     uint32_t tot_drop, tot_brk;
     const uint32_t drop_before = block_excl_scan(ndrop, s_wsum[0], &tot_drop);
@@ -1060,106 +1085,256 @@ __device__ __attribute__((noinline)) int color_g_exact(int y, int cb, int cr) {
     return clamp255(int(g + 128.0f));
 }
 
-// Exact restatement of utils/color.cpp:8-19 (verified exhaustively over [-256,255]^3:
-// tests/test_gpu.py::test_color_exhaustive):
-//   R, B: one fp32 FMA; the true value is >= 0.002 away from an integer unless it is one, so the
-//         fp32 result truncates like the reference's double->float result.
-//   G   : g = y - N/587000 with N = 202008*cb + 419198*cr exactly; away from integers (rem not
-//         within 64/587000 of 0) trunc(g + 128) = y + 127 - floor(N/587000); else exact path.
-__device__ __forceinline__ void color_px(int y, int cb, int cr, uint32_t& R, uint32_t& G, uint32_t& B) {
-    const float r = __builtin_fmaf(float(cr), 1.402f, float(y));
-    const float bb = __builtin_fmaf(float(cb), 1.772f, float(y));
-    R = uint32_t(clamp255(int(r + 128.0f)));
-    B = uint32_t(clamp255(int(bb + 128.0f)));
+// Exact integer restatement of utils/color.cpp:8-19, split into per-chroma-sample terms and a
+// per-pixel add + clamp (verified over all of [-256,255]^3: tests/test_oracle.py):
+//   R = clamp(y + 128 + floor(1402 cr / 1000))       (1.402 cr is >= 0.002 from any integer
+//   B = clamp(y + 128 + floor(1772 cb / 1000))        unless it is one: float rounding is harmless)
+//   G = clamp(y + 127 - floor(N / 587000)), N = 202008 cb + 419198 cr; y + 128 when N == 0; the
+//       reference's double/float path when N / 587000 is within 64/587000 of an integer (2e-4)
+struct ChromaTerms {
+    int r, b, g;
+    bool exact;
+};
+__device__ __forceinline__ ChromaTerms chroma_terms(int cb, int cr) {
+    ChromaTerms t;
+    t.r = int(uint32_t(1402 * cr + 1000 * 359) / 1000u) - 359 + 128;
+    t.b = int(uint32_t(1772 * cb + 1000 * 454) / 1000u) - 454 + 128;
     const int n = 202008 * cb + 419198 * cr;
-    const int nq = n + 587000 * 512;  // > 0 for |cb|,|cr| <= 256
-    const int q = int(uint32_t(nq) / 587000u) - 512;
+    const int q = int(uint32_t(n + 587000 * 512) / 587000u) - 512;
     const int rem = n - q * 587000;
-    if (rem < 64 || rem > 587000 - 64) G = uint32_t(color_g_exact(y, cb, cr));
-    else G = uint32_t(clamp255(y + 127 - q));
+    t.exact = n != 0 && (rem < 64 || rem > 587000 - 64);
+    t.g = n == 0 ? 128 : 127 - q;
+    return t;
+}
+__device__ __forceinline__ uint32_t clamp_u8(int v) { return uint32_t(min(max(v, 0), 255)); }  // v_med3_i32
+
+__device__ __forceinline__ void colour_px(int y, int cb, int cr, const ChromaTerms& t, uint32_t& R, uint32_t& G,
+                                          uint32_t& B) {
+    R = clamp_u8(y + t.r);
+    B = clamp_u8(y + t.b);
+    G = t.exact ? uint32_t(color_g_exact(y, cb, cr)) : clamp_u8(y + t.g);
 }
 
-// One workgroup per tile: 128 px wide x (16 px, or one MCU row when MCUs are 32 px tall).
-// Phases: zero LDS tile -> sparse entries to dense dequantised blocks (4 lanes per block) -> row
-// IDCT (one lane per block row) -> column IDCT -> colour, where each lane owns 8 consecutive
-// pixels of one row and stores them as 24 contiguous bytes (3 x 8-byte stores when aligned).
+// The production per-pixel path in one call (known-answer hook, tests/test_gpu.py).
+__device__ __forceinline__ void color_px(int y, int cb, int cr, uint32_t& R, uint32_t& G, uint32_t& B) {
+    colour_px(y, cb, cr, chroma_terms(cb, cr), R, G, B);
+}
+
+// n = 8 >> SH consecutive int16 samples of a plane row (SH = log2 of the horizontal replication)
+template <int SH>
+__device__ __forceinline__ void load_plane(const int16_t* pl, uint32_t off, int (&v)[8]) {
+    if (SH == 0) {
+        const uint4 q = *reinterpret_cast<const uint4*>(pl + off);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            v[2 * i] = int(int16_t(w[i] & 0xFFFFu));
+            v[2 * i + 1] = int32_t(w[i]) >> 16;
+        }
+    } else if (SH == 1) {
+        const uint2 q = *reinterpret_cast<const uint2*>(pl + off);
+        v[0] = int(int16_t(q.x & 0xFFFFu));
+        v[1] = int32_t(q.x) >> 16;
+        v[2] = int(int16_t(q.y & 0xFFFFu));
+        v[3] = int32_t(q.y) >> 16;
+    } else {
+        const uint32_t q = *reinterpret_cast<const uint32_t*>(pl + off);
+        v[0] = int(int16_t(q & 0xFFFFu));
+        v[1] = int32_t(q) >> 16;
+    }
+}
+
+// Colour of 8 pixels whose chroma samples repeat 2^SH times horizontally (both chroma planes);
+// SH == 3: grayscale (cb = cr = 0).
+template <int SH>
+__device__ __forceinline__ void colour8(const int (&Yv)[8], const int16_t* s_pl, uint32_t cboff, uint32_t croff,
+                                        uint32_t (&rgb)[8][3]) {
+    if (SH == 3) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) rgb[j][0] = rgb[j][1] = rgb[j][2] = clamp_u8(Yv[j] + 128);
+        return;
+    }
+    constexpr int NU = 8 >> SH;
+    int cb[8], cr[8];
+    load_plane<SH>(s_pl, cboff, cb);
+    load_plane<SH>(s_pl, croff, cr);
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const ChromaTerms t = chroma_terms(cb[u], cr[u]);
+#pragma unroll
+        for (int r = 0; r < (1 << SH); r++) {
+            const int j = (u << SH) + r;
+            colour_px(Yv[j], cb[u], cr[u], t, rgb[j][0], rgb[j][1], rgb[j][2]);
+        }
+    }
+}
+
+// One wave per tile of tile_mcus x tile_mrows MCUs (host-chosen, <= 64 blocks):
+//  1. lane j owns block j: its LDS row (pitch 65 words) is filled with the block's DC and AC
+//     entries, dequantised in zig-zag order (parser.cpp:111,130) and placed at natural positions
+//  2. integer IDCT entirely in registers: rows, then columns (idct.cpp:34-122)
+//  3. the clipped samples go to int16 component planes of the tile (16-byte LDS stores)
+//  4. lane = 8 consecutive output pixels: replicate chroma upsampling from the planes, colour
+//     (color.cpp:8-19), 24 contiguous output bytes per lane
+// Every LDS access pattern is conflict-free or 16-byte-vectorised; no LDS traffic in the IDCT.
+constexpr int kIdctPitch = 65;
+
+// 8 horizontally consecutive output samples of one plane row, replicate-upsampled by 2^shx:
+// one aligned 16-byte LDS read, then register selects only (no dynamically indexed arrays).
+__device__ __forceinline__ void load8_samples(const int16_t* pl, uint32_t off, uint32_t shx, int (&v)[8]) {
+    const uint4 q = *reinterpret_cast<const uint4*>(pl + (off & ~7u));
+    const uint32_t d2 = (off & 7u) >> 1;  // first dword holding the samples (shx >= 1: off even)
+    const uint32_t a0 = d2 == 0 ? q.x : (d2 == 1 ? q.y : (d2 == 2 ? q.z : q.w));
+    const uint32_t a1 = d2 == 0 ? q.y : (d2 == 1 ? q.z : q.w);
+    const int x0 = int(int16_t(q.x & 0xFFFFu)), x1 = int32_t(q.x) >> 16;
+    const int x2 = int(int16_t(q.y & 0xFFFFu)), x3 = int32_t(q.y) >> 16;
+    const int x4 = int(int16_t(q.z & 0xFFFFu)), x5 = int32_t(q.z) >> 16;
+    const int x6 = int(int16_t(q.w & 0xFFFFu)), x7 = int32_t(q.w) >> 16;
+    const int l0 = int(int16_t(a0 & 0xFFFFu)), h0 = int32_t(a0) >> 16;
+    const int l1 = int(int16_t(a1 & 0xFFFFu)), h1 = int32_t(a1) >> 16;
+    const bool s0 = shx == 0, s1 = shx == 1;
+    v[0] = s0 ? x0 : l0;
+    v[1] = s0 ? x1 : l0;
+    v[2] = s0 ? x2 : (s1 ? h0 : l0);
+    v[3] = s0 ? x3 : (s1 ? h0 : l0);
+    v[4] = s0 ? x4 : (s1 ? l1 : h0);
+    v[5] = s0 ? x5 : (s1 ? l1 : h0);
+    v[6] = s0 ? x6 : (s1 ? h1 : h0);
+    v[7] = s0 ? x7 : (s1 ? h1 : h0);
+}
+
 __global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
-    __shared__ int s_coef[kTileMaxBlocks * 64];
-    __shared__ int s_q[3][64];
+    __shared__ __attribute__((aligned(16))) int s_buf[64 * kIdctPitch + 3];
+    __shared__ uint32_t s_tab[3][64];  // (q << 6) | natural index, per component and zig-zag index
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t tile = blockIdx.x;
     const uint32_t tiles_x = im.tiles_x;
     if (tile >= tiles_x * im.tiles_y) return;
+    const uint32_t lane = threadIdx.x;
     const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
-    const uint32_t T = im.tile_mcus, R = im.tile_mrows;
-    const uint32_t m0 = tx * T, r0 = ty * R;
-    const uint32_t nm = min(T, im.mcux - m0), nr = min(R, im.mcuy - r0);
-    const uint32_t bpm = im.bpm, nblk = T * R * bpm;
-    const int tid = threadIdx.x;
-
-    for (uint32_t i = tid; i < nblk * 16; i += kIdctThreads)
-        reinterpret_cast<int4*>(s_coef)[i] = make_int4(0, 0, 0, 0);
-    if (tid < int(im.ncomp) * 64) {
-        const int c = tid >> 6, z = tid & 63;
-        s_q[c][z] = int(b.qtabs[size_t(im.qslot[c]) * 64 + z]);
+    const uint32_t TM = im.tile_mcus, TR = im.tile_mrows, bpm = im.bpm, nc = im.ncomp;
+    const uint32_t m0 = tx * TM, r0 = ty * TR;
+    const uint32_t nm = min(TM, im.mcux - m0), nr = min(TR, im.mcuy - r0);
+    for (uint32_t i = lane; i < nc * 64; i += kIdctThreads) {
+        const uint32_t c = i >> 6, z = i & 63u;
+        s_tab[c][z] = (uint32_t(b.qtabs[size_t(im.qslot[c]) * 64 + z]) << 6) | kNatOfZz[z];
     }
+    int4* z4 = reinterpret_cast<int4*>(s_buf);
+    for (uint32_t i = lane; i < (64 * kIdctPitch + 3) / 4; i += kIdctThreads) z4[i] = make_int4(0, 0, 0, 0);
     __syncthreads();
 
-    // sparse -> dense, dequantised in zig-zag order (parser.cpp:111,130), natural placement
-    for (uint32_t j = uint32_t(tid) >> 2; j < nblk; j += kIdctThreads / 4) {
-        const uint32_t m = j / bpm, bb = j - m * bpm;
-        const uint32_t mr = m / T, mi = m - mr * T;
-        if (mi >= nm || mr >= nr) continue;
-        const uint32_t sub = uint32_t(tid) & 3;
-        const uint32_t comp = (im.block_pattern >> (2 * bb)) & 3u;
+    // 1. sparse -> dense (my block)
+    const uint32_t m = lane / bpm, bb = lane - m * bpm;
+    const uint32_t mr = m / TM, mi = m - mr * TM;
+    const bool have = mr < nr && mi < nm;
+    const uint32_t comp = (im.block_pattern >> (2 * bb)) & 3u;
+    int* row = s_buf + lane * kIdctPitch;
+    if (have) {
         const uint64_t gb = im.block_base + uint64_t((r0 + mr) * im.mcux + m0 + mi) * bpm + bb;
         const BlockInfo bi = b.blocks[gb];
         // a block of a corrupt stream may never have been written: never index past the entries
         int cnt = min(int(bi.cnt_dc >> 16), 63);
         if (uint64_t(bi.entry_start) + uint64_t(cnt) > b.entries_cap) cnt = 0;
-        int* blk = s_coef + j * 64;
-        if (sub == 0) blk[0] = int(int16_t(bi.cnt_dc & 0xFFFFu)) * s_q[comp][0];
-        for (int i = int(sub); i < cnt; i += 4) {
-            const uint32_t e = b.entries[bi.entry_start + i];
-            const int z = int(e & 63u);
-            blk[kNatOfZz[z]] = (int32_t(e) >> 16) * s_q[comp][z];
+        row[0] = int(int16_t(bi.cnt_dc & 0xFFFFu)) * int(s_tab[comp][0] >> 6);
+        // entries in 16-byte loads, four in flight at a time (the entry buffer is padded by 64 B)
+        const uint32_t lead = bi.entry_start & 3u;
+        const uint32_t* ep = b.entries + (bi.entry_start - lead);
+        const int n4 = int(lead + uint32_t(cnt) + 3u) >> 2;
+        for (int c = 0; c < n4; c += 4) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                v[u] = (c + u < n4) ? *reinterpret_cast<const uint4*>(ep + 4 * (c + u)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int i = 4 * (c + u) + q - int(lead);
+                    if (i >= 0 && i < cnt) {
+                        const uint32_t t = s_tab[comp][w[q] & 63u];
+                        row[t & 63u] = (int32_t(w[q]) >> 16) * int(t >> 6);
+                    }
+                }
+            }
         }
     }
     __syncthreads();
-    for (uint32_t r = tid; r < nblk * 8; r += kIdctThreads) idct_row(s_coef + r * 8);
-    __syncthreads();
-    for (uint32_t c = tid; c < nblk * 8; c += kIdctThreads) idct_col(s_coef + (c >> 3) * 64 + (c & 7));
-    __syncthreads();
 
-    const uint32_t lg_mw = im.lg_mw, lg_mh = im.lg_mh;
-    const uint32_t rows = R << lg_mh;  // tile rows
-    const uint32_t W = im.width, H = im.height, nc = im.ncomp;
-    const uint32_t x_tile = m0 << lg_mw, y_tile = r0 << lg_mh;
-    uint8_t* out = reinterpret_cast<uint8_t*>(im.rgb);
-    for (uint32_t it = tid; it < rows * (kTileWidth / 8); it += kIdctThreads) {
-        const uint32_t py = it >> 4, gx = (it & 15u) << 3;
-        const uint32_t y = y_tile + py, x = x_tile + gx;
-        if (y >= H || x >= W) continue;
-        const uint32_t mr = py >> lg_mh, uy = py & ((1u << lg_mh) - 1);
-        const uint32_t mi = gx >> lg_mw, ux0 = gx & ((1u << lg_mw) - 1);
-        const uint32_t mcu_base = (mr * T + mi) * bpm;
-        int sbase[3], ssh[3];
+    // 2. IDCT in registers
+    int blk[64];
+#pragma unroll
+    for (int p = 0; p < 64; p++) blk[p] = row[p];
+#pragma unroll
+    for (int r = 0; r < 8; r++) idct_row(blk + 8 * r);
+#pragma unroll
+    for (int c = 0; c < 8; c++) idct_col(blk + c);
+    __syncthreads();  // every row read back before the planes overwrite the staging area
+
+    // 3. component planes (int16), pitch = plane width + 8 samples
+    int16_t* s_pl = reinterpret_cast<int16_t*>(s_buf);
+    uint32_t pbase[3] = {0u, 0u, 0u}, ppitch[3] = {8u, 8u, 8u};
+    {
+        uint32_t off = 0;
 #pragma unroll
         for (int c = 0; c < 3; c++) {
-            const uint32_t sy = uy >> im.shy[c];
-            sbase[c] = int((mcu_base + im.comp_block0[c] + (sy >> 3) * im.h[c]) * 64 + (sy & 7) * 8);
-            ssh[c] = im.shx[c];
-        }
-        uint32_t rgb[8][3];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            int s3[3];
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                const uint32_t sx = (ux0 + j) >> ssh[c];
-                s3[c] = (uint32_t(c) < nc) ? s_coef[sbase[c] + int((sx >> 3) * 64 + (sx & 7))] : 0;
+            if (uint32_t(c) < nc) {
+                ppitch[c] = TM * im.h[c] * 8 + 8;
+                pbase[c] = off;
+                off += ppitch[c] * TR * im.v[c] * 8;
             }
-            color_px(s3[0], s3[1], s3[2], rgb[j][0], rgb[j][1], rgb[j][2]);
+        }
+    }
+    if (have) {
+        const uint32_t hc = im.h[comp];
+        const uint32_t t = bb - im.comp_block0[comp];
+        const uint32_t tyb = t / hc, txb = t - tyb * hc;
+        const uint32_t pitch = comp == 0 ? ppitch[0] : (comp == 1 ? ppitch[1] : ppitch[2]);
+        const uint32_t base = comp == 0 ? pbase[0] : (comp == 1 ? pbase[1] : pbase[2]);
+        int16_t* dst = s_pl + base + ((mr * im.v[comp] + tyb) * 8) * pitch + (mi * hc + txb) * 8;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            uint4 q;
+            q.x = (uint32_t(blk[8 * r + 0]) & 0xFFFFu) | (uint32_t(blk[8 * r + 1]) << 16);
+            q.y = (uint32_t(blk[8 * r + 2]) & 0xFFFFu) | (uint32_t(blk[8 * r + 3]) << 16);
+            q.z = (uint32_t(blk[8 * r + 4]) & 0xFFFFu) | (uint32_t(blk[8 * r + 5]) << 16);
+            q.w = (uint32_t(blk[8 * r + 6]) & 0xFFFFu) | (uint32_t(blk[8 * r + 7]) << 16);
+            *reinterpret_cast<uint4*>(dst + r * pitch) = q;
+        }
+    }
+    __syncthreads();
+
+    // 4. upsample + colour, 8 pixels per lane
+    const uint32_t lg_mw = im.lg_mw, lg_mh = im.lg_mh;
+    const uint32_t gpr = (TM << lg_mw) >> 3;  // 8-pixel groups per tile row
+    const uint32_t th = TR << lg_mh;
+    const uint32_t W = im.width, H = im.height;
+    const uint32_t x_tile = m0 << lg_mw, y_tile = r0 << lg_mh;
+    const uint32_t shx1 = im.shx[1], shy1 = im.shy[1], shx2 = im.shx[2], shy2 = im.shy[2];
+    const uint32_t cmode = nc == 1 ? 3u : (shx1 == shx2 ? shx1 : 4u);
+    uint8_t* out = reinterpret_cast<uint8_t*>(im.rgb);
+    for (uint32_t it = lane; it < th * gpr; it += kIdctThreads) {
+        const uint32_t py = it / gpr, gx = (it - py * gpr) << 3;
+        const uint32_t y = y_tile + py, x = x_tile + gx;
+        if (y >= H || x >= W) continue;
+        int Yv[8];
+        load_plane<0>(s_pl, pbase[0] + py * ppitch[0] + gx, Yv);
+        const uint32_t cboff = pbase[1] + (py >> shy1) * ppitch[1] + (gx >> shx1);
+        const uint32_t croff = pbase[2] + (py >> shy2) * ppitch[2] + (gx >> shx2);
+        uint32_t rgb[8][3];
+        switch (cmode) {  // wave-uniform
+            case 0: colour8<0>(Yv, s_pl, cboff, croff, rgb); break;
+            case 1: colour8<1>(Yv, s_pl, cboff, croff, rgb); break;
+            case 2: colour8<2>(Yv, s_pl, cboff, croff, rgb); break;
+            case 3: colour8<3>(Yv, s_pl, cboff, croff, rgb); break;
+            default: {  // chroma planes with different horizontal factors
+                int Cb[8], Cr[8];
+                load8_samples(s_pl, cboff, shx1, Cb);
+                load8_samples(s_pl, croff, shx2, Cr);
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    colour_px(Yv[j], Cb[j], Cr[j], chroma_terms(Cb[j], Cr[j]), rgb[j][0], rgb[j][1], rgb[j][2]);
+            }
         }
         uint8_t* dst = out + (size_t(y) * W + x) * 3;
         const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
@@ -1169,7 +1344,7 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
             for (int q = 0; q < 6; q++) {
                 uint32_t v = 0;
 #pragma unroll
-                for (int bb = 0; bb < 4; bb++) v |= rgb[(4 * q + bb) / 3][(4 * q + bb) % 3] << (8 * bb);
+                for (int k = 0; k < 4; k++) v |= rgb[(4 * q + k) / 3][(4 * q + k) % 3] << (8 * k);
                 w[q] = v;
             }
             if ((ad & 7) == 0) {

@@ -271,14 +271,21 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         d.block_base = P.total_blocks;
         P.total_blocks += nmcu * uint64_t(h.blocks_per_mcu);
         d.tableset = uint32_t(ts);
-        {  // IDCT/colour tiles: 128 px wide, 16 px (or one MCU row if taller) high
+        {  // IDCT/colour tiles: one wave, one lane per block: the most blocks <= 64 over 1 or 2 MCU rows
             uint32_t lw = 0, lh = 0;
             while ((8u << lw) < 8u * d.hmax) lw++;
             while ((8u << lh) < 8u * d.vmax) lh++;
             d.lg_mw = 3 + lw;
             d.lg_mh = 3 + lh;
-            d.tile_mcus = uint32_t(kTileWidth) >> d.lg_mw;
-            d.tile_mrows = d.vmax == 1 ? 2u : 1u;
+            uint32_t best = 0;
+            for (uint32_t tr = 1; tr <= 2; tr++) {
+                const uint32_t tm = std::max(1u, uint32_t(kTileMaxBlocks) / (tr * d.bpm));
+                if (tm * tr * d.bpm > best) {
+                    best = tm * tr * d.bpm;
+                    d.tile_mcus = tm;
+                    d.tile_mrows = tr;
+                }
+            }
             d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
             d.tiles_y = (d.mcuy + d.tile_mrows - 1) / d.tile_mrows;
             for (int c = 0; c < h.ncomp; c++) {
@@ -457,7 +464,7 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, ctx->plan_host.p, upload, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, ensure_dev(ctx->chunk_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
         HIPCHK(ctx, ensure_dev(ctx->blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
-        HIPCHK(ctx, ensure_dev(ctx->entries, std::max<size_t>(16, P.total_entry_cap * 4)));
+        HIPCHK(ctx, ensure_dev(ctx->entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
 
         uint8_t* base = static_cast<uint8_t*>(ctx->plan.p);
         BatchDev b;
@@ -492,7 +499,7 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         b.chunk_brk = static_cast<Break*>(ctx->chunk_brk.p);
         b.blocks = static_cast<BlockInfo*>(ctx->blocks.p);
         b.entries = static_cast<uint32_t*>(ctx->entries.p);
-        b.entries_cap = ctx->entries.cap / 4;
+        b.entries_cap = (ctx->entries.cap - 64) / 4;  // last 64 B: padding for 16-byte over-reads
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
         b.max_tiles = P.max_tiles;
