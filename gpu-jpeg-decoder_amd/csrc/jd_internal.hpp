@@ -14,15 +14,24 @@ namespace jd {
 constexpr int kLutBits = 10;
 constexpr int kLutSize = 1 << kLutBits;
 
+#if defined(__HIPCC__)
+#define JD_HD __host__ __device__
+#else
+#define JD_HD
+#endif
+
 // Device Huffman table (built on the host from a DHT table, uploaded once, cached by content).
-//   fast[i]: entry for the next kLutBits stream bits = i
-//     bits 0..4  : bits to consume (0 = slow path)
-//     bit  5     : value-complete (magnitude bits already included in the count)
-//     bits 8..15 : symbol (DC: size s; AC: run<<4 | size)
-//     bits 16..31: int16 coefficient value when value-complete
+//   fast[i]: entry for the symbol whose code starts the next kLutBits stream bits (= i):
+//     bits 0..4   L    bits the symbol consumes, code + magnitude (0: code longer than kLutBits)
+//     bits 5..8   run  AC zero run (symbol >> 4); 0 for DC
+//     bit  9      eob  AC end-of-block (symbol 0x00)
+//     bit  10     emit AC coefficient stored (size != 0)
+//     bits 11..15 sz   magnitude bits (DC: symbol, AC: symbol & 15)
+//   The coefficient is always EXTEND(the last sz of the L bits), so a decode step is one lookup
+//   plus bit-field extracts.  Codes longer than kLutBits take the canonical slow path:
 //   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not
 //                < lim[l-1]) — the canonical DECODE procedure of JPEG Annex F.2.2.3
-//   base[l]    : valptr[l] - mincode[l]
+//   base[l]    : valptr[l] - mincode[l]; vals[] the symbols in code order
 struct alignas(16) HuffLut {
     uint32_t fast[kLutSize];
     uint32_t lim[20];
@@ -30,7 +39,16 @@ struct alignas(16) HuffLut {
     uint8_t vals[256];
 };
 static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
-constexpr uint32_t kLutFlagComplete = 32u;
+constexpr int kLutWords = int(sizeof(HuffLut) / 4);
+
+// Entry of a code of length l for symbol sym; 0 when it cannot be represented (l + sz > 31 or a
+// DC size beyond 16 bits: corrupt for 8-bit baseline, whose DC sizes are <= 11).
+JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
+    const uint32_t sz = is_dc ? sym : (sym & 15u);
+    if (sz > 16u || l + sz > 31u || l == 0u) return 0u;
+    if (is_dc) return (l + sz) | (sz << 11);
+    return (l + sz) | ((sym >> 4) << 5) | (sym == 0u ? 512u : 0u) | (sz ? 1024u : 0u) | (sz << 11);
+}
 
 // Maximum Huffman tables a table set (one workgroup of the Huffman kernel) stages into LDS.
 constexpr int kSlotsPerSet = 6;
@@ -73,7 +91,9 @@ struct alignas(16) ImgDesc {
 
 // Per-block result of the Huffman kernel (sparse coefficient representation):
 //   entry_start = index of the block's first AC entry in the entry array
-//   cnt_dc      = (number of AC entries << 16) | (uint16)DC   (DC un-predicted, still quantised)
+//   cnt_dc      = (number of AC entries << 26) | (DC & 0x3FFFFFF): DC quantised, as a 26-bit two's
+//                 complement value — the DC difference until k_dpcm (or the self-synchronising write
+//                 pass) turns it into the predicted DC
 // AC entry = (int16 value << 16) | zig-zag index (1..63).
 struct BlockInfo {
     uint32_t entry_start;
@@ -90,30 +110,14 @@ struct Break {
 
 constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
 
-// Self-synchronising decode: every restart interval (segment) is cut into subsequences of
-// kSubBits bits of un-stuffed data, one lane each (reference:
-// parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208).  A decoder state is
-//   p  : segment-relative bit position of the next symbol
-//   sk : (bi << 16) | (k << 8) | ncur   — block-in-MCU, coefficient index (0 = DC next),
-//        AC entries already emitted for the current block
-constexpr int kSubBits = 512;
-struct SubState {
-    uint32_t p;
-    uint32_t sk;
-};
-struct SubCount {  // decoded from a subsequence's true entry state
-    uint32_t blocks;   // DC symbols (block starts)
-    uint32_t entries;  // non-zero AC entries
-    int32_t dc[3];     // sum of DC differences per component
-    uint32_t pad;
-};
-struct SubEntry {  // verified entry state + prefix sums within the segment
-    uint32_t p, sk;
-    uint32_t blk;      // segment-relative index of the next block to start
-    uint32_t ent;      // global index of the next AC entry
-    int32_t pred[3];   // DC predictors
-    uint32_t pad;
-};
+// Huffman decode geometry: every interval is cut into pieces of piece_bits un-stuffed bits, one
+// lane each; a piece's scan synchronises from piece_overlap bits before its start (jd_kernels.hip
+// Stage 3; reference: parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208).  4:2:0 MCU
+// phase needs a few thousand bits to lock: speculative starts failed 45 % / 12 % / 0 % of the
+// time at 1024 / 2048 / 4096 bits on the bench images (tools/jd_trace.py emulate()).
+constexpr uint32_t kPieceBits = 8192;
+constexpr uint32_t kPieceOverlap = 4096;
+constexpr int kPieceThreads = 256;  // one workgroup shares one copy of its table set in LDS
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;
@@ -121,11 +125,6 @@ constexpr int kScanBytesPerThread = 64;
 constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
 constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cannot hold more
 
-constexpr int kHuffThreads = 256;
-constexpr int kSegThreads = 64;  // k_seg workgroup: one lane per restart interval
-// An image is decoded interval-per-lane (k_seg) when it has at least this many restart
-// intervals; otherwise (no DRI, or very long intervals) by the self-synchronising passes.
-constexpr uint32_t kMinLaneSegments = 4;
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
 constexpr int kTileMaxBlocks = 64;   // blocks per IDCT/colour tile (one lane each)
 
@@ -145,22 +144,24 @@ struct BatchDev {
     uint32_t* seg_cstart;         // first un-stuffed byte of each segment (image-relative)
     uint32_t* seg_cend;           // end of each segment's data (image-relative, un-stuffed)
     const uint32_t* seg_entry;    // first AC-entry slot of each segment
-    uint32_t* seg_sub_base;       // first subsequence of each segment
-    uint32_t* seg_nsub;           // subsequences of each segment
+    uint32_t* seg_sub_base;       // first piece slot of each segment
+    uint32_t* seg_nsub;           // pieces of each segment
     uint32_t nseg;
-    // subsequences
-    uint32_t* sub_seg;            // segment of each subsequence (kInvalidImage = unused)
-    uint32_t nsub;                // multiple of kHuffThreads
-    const uint32_t* wg_tableset;  // table set of each decode workgroup (kHuffThreads subsequences)
-    uint32_t max_slots;           // LUT slots staged per decode workgroup
-    SubState* exit_spec;          // pass 0 exits (speculative entries)
-    SubState* exit_cnt;           // pass 1 exits
-    SubCount* sub_cnt;            // pass 1 counts
-    SubEntry* sub_entry;          // chain output
-    // restart-interval lanes (images with DRI, decoded by k_seg)
-    const uint32_t* seg_lane;     // segment of each lane (kInvalidImage = padding)
-    uint32_t nseg_lane;           // multiple of kSegThreads
-    const uint32_t* lane_wg_tableset;  // table set of each k_seg workgroup
+    // pieces (per image a slot capacity of ceil(ECS bits / piece_bits) + nseg, padded)
+    uint32_t* sub_seg;            // segment of each piece slot (kInvalidImage = unused)
+    uint32_t nsub;                // multiple of kPieceThreads
+    const uint32_t* wg_tableset;  // table set of each k_piece workgroup
+    uint32_t max_slots;           // LUT slots staged per workgroup
+    uint32_t piece_bits, piece_overlap;
+    uint32_t* piece_bit;          // first bit of the piece (an MCU boundary)
+    uint32_t* piece_end;          // scan: first MCU boundary at/after the piece's nominal end
+    uint32_t* piece_nmcu;         // scan: MCUs in the piece (chain: final)
+    uint32_t* piece_nent;         // scan: AC entries in the piece
+    uint32_t* piece_mcu0;         // chain: first MCU of the piece within its segment
+    uint32_t* piece_ent0;         // chain: first AC-entry slot of the piece
+    const uint32_t* chain_seg;    // k_chain: segment of each lane, grouped by table set
+    uint32_t nchain;              // multiple of kPieceThreads
+    const uint32_t* chain_wg_tableset;
     // scan / compaction
     uint32_t max_chunks;
     uint32_t* chunk_nbrk;         // breaks per chunk

@@ -13,7 +13,6 @@
 // Arithmetic follows the reference CPU decoder bit for bit (cpp-decoder/src/idct.cpp,
 // utils/color.cpp); the restatement used as checker lives in oracle/ (tests only).
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
 
 #include "jd_kernels.hpp"
 
@@ -305,85 +304,77 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Stage 3: self-synchronising Huffman decode (the reference's parallelHuffManDecode idea,
-// cuda-decoder/src/parser.cu:132-208, re-planned for wave64): every restart interval (segment)
-// is cut into kSubBits-bit subsequences of un-stuffed data, one lane each.
-//   k_subplan   per image: subsequences of every segment
-//   k_decode<0> speculative pass: each lane decodes its subsequence from (its first bit, DC of
-//               block 0) — Huffman codes self-synchronise, so its exit state (first symbol
-//               starting in the next subsequence) is almost always the true one
-//   k_decode<1> count pass: from the predecessor's speculative exit; exit state + counts
-//               (blocks, AC entries, DC-difference sums)
-//   k_chain     per segment (one wave): a lane whose count-pass entry differs from its
-//               predecessor's count-pass exit is re-decoded (rare), then prefix sums give every
-//               subsequence its block index, entry offset and DC predictors
-//   k_decode<2> write pass: from the verified entry, BlockInfo + AC entries out
-// A lane's subsequence (plus the overlap for a symbol that crosses its end) is loaded once into
-// its own LDS row — the decode steps do no global loads, so no s_waitcnt on stores ever stalls
-// a step (gfx950 counts loads and stores on one vmcnt).  Rows are byte-swapped (MSB-first) so a
-// symbol's 32-bit window is two LDS reads and one funnel shift; rows are [lane][word] with an odd
-// pitch (25 words), so 32 lanes reading the same word index hit 32 different banks.
+// Stage 3: Huffman decode.  Every restart interval (the whole scan when there is no DRI) is cut
+// into pieces of piece_bits un-stuffed bits, one lane each — the reference's self-synchronising
+// decode (parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208) re-planned so that pieces
+// start on MCU boundaries and nothing runs serially:
+//   k_subplan      per image: pieces of every interval (interval lengths are only known on the
+//                  GPU, after k_index)
+//   k_piece<Scan>  lane per piece j: starts piece_overlap bits before j*piece_bits with a guessed
+//                  state (Huffman codes self-synchronise; so does the MCU phase given a few
+//                  thousand bits), takes the first MCU boundary at/after j*piece_bits as the
+//                  piece start, and counts MCUs and AC entries up to the first MCU boundary
+//                  at/after (j+1)*piece_bits.  Piece 0 starts at bit 0 in the true state.
+//   k_chain        wave per interval: piece j's end must be piece j+1's start; a mismatch (the
+//                  guess had not synchronised) is re-scanned from the verified boundary.  Prefix
+//                  sums give each piece its first MCU and AC-entry slot.
+//   k_piece<Write> lane per piece, from its verified MCU boundary: BlockInfo + AC entries, DC as
+//                  differences
+//   k_dpcm         wave per interval: DC differences -> DC values (parser.cpp:106-111)
+//
+// A lane's bitstream streams through its own LDS row in windows of kWinAdv bytes: a round issues
+// the loads of the NEXT window into registers, decodes every symbol whose refill word lies in the
+// current window, then commits the registers.  The only vmcnt wait per round is that commit
+// (gfx950 counts stores and loads on one vmcnt, so a wait inside the symbol loop would stall on
+// the coefficient stores).  The symbol loop keeps a 64-bit bit buffer in registers, refilled
+// from a row word read one symbol ahead, so its only LDS latency is the table lookup.
 // ------------------------------------------------------------------------------------------
-constexpr int kSubBytes = kSubBits / 8;
-constexpr int kSubBufWords = 24;  // 96 bytes: subsequence + 16-byte misalignment + crossing symbol
-constexpr int kSubStride = 25;
-constexpr int kSubMaxBit = (kSubBufWords - 2) * 32;  // last bit position a peek may start at
-
 __device__ __forceinline__ u32x4 load16(uintptr_t a, uintptr_t last) {
-    // clamped to the image's last mapped 16-byte chunk; bytes past a segment's end are never
+    // clamped to the image's last mapped 16-byte chunk; bytes past an interval's end are never
     // consumed as data, so what a clamped load returns there is irrelevant
     return *reinterpret_cast<gu32x4*>(a < last ? a : last);
 }
 
-__device__ __forceinline__ int extend(uint32_t v, int s) {  // utils/stream.cpp:44-52
-    if (s == 0) return 0;
-    const int l = 1 << (s - 1);
-    return int(v) >= l ? int(v) : int(v) - ((l << 1) - 1);
+// Codes longer than kLutBits: the canonical limits decide the length (kLutBits+1 plus the number
+// of left-justified limits <= v16: F.2.2.3 restated, independent LDS reads), then the symbol.
+// Returns the entry in the fast-table format.  Codes that match nothing and symbols the format
+// cannot represent (corrupt streams/tables) give kEntryBad: 16 bits consumed (decoding always
+// advances) and bit 16 set.
+constexpr uint32_t kEntryBad = 16u | (1u << 16);
+__device__ __forceinline__ uint32_t huff_slow(const uint32_t* lutw, uint32_t peek, bool is_dc) {
+    const HuffLut* t = reinterpret_cast<const HuffLut*>(lutw);
+    const uint32_t v16 = peek >> 16;
+    uint32_t l = kLutBits + 1;
+#pragma unroll
+    for (int j = kLutBits + 1; j <= 16; j++) l += (v16 >= t->lim[j]) ? 1u : 0u;
+    uint32_t e = 0;
+    if (l <= 16 && v16 >= t->lim[kLutBits]) {
+        const uint32_t sym = t->vals[uint32_t(t->base[l] + int(v16 >> (16 - l))) & 255u];
+        e = lut_entry(l, sym, is_dc);
+    }
+    return e ? e : kEntryBad;
 }
 
-// One Huffman symbol (+ magnitude bits) from the 32-bit window `peek`: symbol, EXTENDed value,
-// bits consumed.
-__device__ __forceinline__ int decode_sym(uint32_t peek, const HuffLut* t, bool is_dc, int& sym, int& val, bool& bad) {
-    const uint32_t e = t->fast[peek >> (32 - kLutBits)];
-    int len;
-    if (e & 31u) {
-        len = int(e & 31u);
-        sym = int((e >> 8) & 255u);
-        val = int32_t(e) >> 16;
-        if (e & kLutFlagComplete) return len;
-    } else {  // code longer than kLutBits (or invalid): canonical limits, F.2.2.3
-        // lim[] is non-decreasing, so the code length is kLutBits+1 plus the number of limits
-        // <= v16: independent LDS reads, no dependent search loop.
-        const uint32_t v16 = peek >> 16;
-        int l = kLutBits + 1;
-#pragma unroll
-        for (int j = kLutBits + 1; j <= 16; j++) l += (v16 >= t->lim[j]) ? 1 : 0;
-        if (l > 16) {
-            bad = true;
-            l = 16;
-            sym = 0;
-        } else {
-            sym = t->vals[(t->base[l] + int(v16 >> (16 - l))) & 255];
-        }
-        len = l;
-    }
-    int s = is_dc ? sym : (sym & 15);
-    if (s > 16) {
-        bad = true;
-        s = 16;
-    }
-    const uint32_t bits = s ? ((peek << len) >> (32 - s)) : 0u;
-    val = extend(bits, s);
-    return len + s;
+// EXTEND (utils/stream.cpp:44-52) of the last sz bits of the L bits at the top of peek.
+__device__ __forceinline__ int huff_value(uint32_t peek, uint32_t e) {
+    const uint32_t L = e & 31u, sz = __builtin_amdgcn_ubfe(e, 11u, 5u);
+    const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - L, sz);  // width 0 -> 0
+    const uint32_t half = (1u << sz) >> 1;
+    return int(mag) - (mag < half ? int(2 * half - 1) : 0);
+}
+
+// BlockInfo.cnt_dc: AC entry count (6 bits) over a 26-bit two's-complement DC (jd_internal.hpp).
+__device__ __forceinline__ uint32_t pack_cnt_dc(uint32_t cnt, int dc) {
+    return (min(cnt, 63u) << 26) | (uint32_t(dc) & 0x3FFFFFFu);
 }
 
 struct SegInfo {
-    uint64_t blk0;     // first global block of the segment
-    uint32_t nblk;     // blocks in the segment
-    uint32_t bits;     // un-stuffed data bits of the segment
-    uintptr_t data;    // address of the segment's first un-stuffed byte
+    uint64_t blk0;     // first global block of the interval
+    uint32_t nblk;     // blocks in the interval
+    uint32_t bits;     // un-stuffed data bits of the interval
+    uintptr_t data;    // address of the interval's first un-stuffed byte
     uintptr_t last;    // last mapped 16-byte chunk of the image's un-stuffed region
-    uint32_t ent0;     // first AC-entry slot of the segment
+    uint32_t ent0;     // first AC-entry slot of the interval
     uint32_t pattern, bpm;
 };
 
@@ -406,133 +397,14 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
     S.bpm = im.bpm;
 }
 
-// Loads subsequence j of a segment into an LDS row (byte-swapped words).  Returns the row bit
-// offset of the subsequence's first bit.
-__device__ __forceinline__ int load_row(uint32_t* row, int stride, uintptr_t data, uint32_t j, uintptr_t last) {
-    const uintptr_t a = data + uintptr_t(j) * kSubBytes;
-    const uintptr_t a16 = a & ~uintptr_t(15);
-#pragma unroll
-    for (int q = 0; q < kSubBufWords / 4; q++) {
-        const u32x4 v = load16(a16 + 16 * q, last);
-        row[(4 * q + 0) * stride] = __builtin_bswap32(v.x);
-        row[(4 * q + 1) * stride] = __builtin_bswap32(v.y);
-        row[(4 * q + 2) * stride] = __builtin_bswap32(v.z);
-        row[(4 * q + 3) * stride] = __builtin_bswap32(v.w);
-    }
-    return int(a & 15) * 8;
-}
-
-__device__ __forceinline__ uint32_t pack_sk(int bi, int k, int ncur) {
-    return (uint32_t(bi) << 16) | (uint32_t(k) << 8) | uint32_t(ncur);
-}
-
-// The decode loop shared by all passes.  MODE 0: exit only; 1: exit + counts; 2: write.
-struct DecIn {
-    int bpos, bend;          // row bit positions: start, first position not decoded from
-    int bi, k, ncur;         // entry state
-    uint32_t blk, ent;       // MODE 2: next block index (segment-relative), next entry slot
-    int pred0, pred1, pred2; // MODE 2: DC predictors
-};
-struct DecOut {
-    int bpos, bi, k, ncur;
-    uint32_t nblocks, nent;
-    int dc0, dc1, dc2;
-    uint32_t blk;
-    bool bad;
-};
-
-template <int MODE>
-__device__ __forceinline__ void decode_run(const DecIn& in, const uint32_t* row, int stride, const HuffLut* luts,
-                                           const int (&dsl)[3], const int (&asl)[3], const SegInfo& S,
-                                           const BatchDev& b, DecOut& o) {
-    // Entry states are well-formed by construction; the clamps below only make garbage (corrupt
-    // streams) unable to index outside the row, the block range or the entry range.
-    int bpos = max(in.bpos, 0);
-    const int bend = min(in.bend, kSubMaxBit);
-    int bi = in.bi < int(S.bpm) ? in.bi : 0, k = min(in.k, 63), ncur = min(in.ncur, 63);
-    const uint32_t ent_end = S.ent0 + 63u * S.nblk;
-    int comp = int((S.pattern >> (2 * bi)) & 3u);
-    uint32_t nblocks = 0, nent = 0;
-    int dc0 = 0, dc1 = 0, dc2 = 0;
-    uint32_t blk = in.blk, ent = in.ent;
-    int p0 = in.pred0, p1 = in.pred1, p2 = in.pred2;
-    // MODE 2: a block entered mid-way was started by the predecessor
-    uint32_t blk_cur = blk - 1, ent_blk = ent - uint32_t(ncur);
-    int dc = comp == 0 ? p0 : (comp == 1 ? p1 : p2);
-    bool bad = false;
-    while (bpos < bend) {
-        if (MODE == 2 && k == 0 && blk >= S.nblk) break;  // segment complete
-        const int w = bpos >> 5;
-        const uint32_t w0 = row[w * stride];
-        const uint32_t w1 = row[(w + 1) * stride];
-        const uint32_t sh = uint32_t(bpos) & 31u;
-        const uint32_t al = __builtin_amdgcn_alignbit(w0, w1, 32u - sh);
-        const uint32_t peek = sh ? al : w0;
-        const bool is_dc = (k == 0);
-        const int slot = is_dc ? (comp == 0 ? dsl[0] : (comp == 1 ? dsl[1] : dsl[2]))
-                               : (comp == 0 ? asl[0] : (comp == 1 ? asl[1] : asl[2]));
-        int sym, val;
-        bpos += decode_sym(peek, &luts[slot], is_dc, sym, val, bad);
-        if (is_dc) {  // parser.cpp:106-111: DPCM
-            if (MODE == 1) {
-                nblocks++;
-                if (comp == 0) dc0 += val;
-                else if (comp == 1) dc1 += val;
-                else dc2 += val;
-            }
-            if (MODE == 2) {
-                const int pr = (comp == 0 ? p0 : (comp == 1 ? p1 : p2)) + val;
-                if (comp == 0) p0 = pr;
-                else if (comp == 1) p1 = pr;
-                else p2 = pr;
-                if (pr < -32768 || pr > 32767) bad = true;
-                dc = pr;
-                blk_cur = blk++;
-                ent_blk = ent;
-            }
-            k = 1;
-            ncur = 0;
-        } else if (sym == 0) {  // EOB: parser.cpp:117-119
-            k = 64;
-        } else {  // run/size: parser.cpp:122-133
-            k += sym >> 4;
-            if (k < 64) {
-                if (sym & 15) {
-                    ncur++;
-                    if (MODE == 1) nent++;
-                    if (MODE == 2) {
-                        if (ent < ent_end) b.entries[ent] = (uint32_t(val) << 16) | uint32_t(k);
-                        else bad = true;
-                        ent++;
-                    }
-                }
-                k++;
-            }
-        }
-        if (k >= 64) {
-            if (MODE == 2) {
-                if (blk_cur < S.nblk && ent <= ent_end)
-                    b.blocks[S.blk0 + blk_cur] =
-                        BlockInfo{ent_blk, (min(ent - ent_blk, 63u) << 16) | (uint32_t(dc) & 0xFFFFu)};
-                else
-                    bad = true;
-            }
-            bi = (bi + 1 == int(S.bpm)) ? 0 : bi + 1;
-            comp = int((S.pattern >> (2 * bi)) & 3u);
-            k = 0;
-        }
-    }
-    o.bpos = bpos;
-    o.bi = bi;
-    o.k = k;
-    o.ncur = ncur;
-    o.nblocks = nblocks;
-    o.nent = nent;
-    o.dc0 = dc0;
-    o.dc1 = dc1;
-    o.dc2 = dc2;
-    o.blk = blk;
-    o.bad = bad;
+__device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
+    S.data = S.last = uintptr_t(b.imgs) & ~uintptr_t(15);
+    S.bits = 0;
+    S.nblk = 0;
+    S.blk0 = 0;
+    S.ent0 = 0;
+    S.pattern = 0;
+    S.bpm = 1;
 }
 
 __device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads) {
@@ -543,17 +415,10 @@ __device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts
     }
 }
 
-// Per image (one wave): number of subsequences of every segment, segment -> subsequence map.
+// Per image (one wave): pieces of every interval, interval -> piece map.
 __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     const ImgDesc& im = b.imgs[blockIdx.x];
     const int lane = threadIdx.x;
-    if (im.sub_cap == 0) {  // restart-interval image: decoded by k_seg
-        for (uint32_t k = lane; k < im.nseg; k += 64) {
-            b.seg_sub_base[im.seg_base + k] = 0;
-            b.seg_nsub[im.seg_base + k] = 0;
-        }
-        return;
-    }
     uint32_t run = 0;
     for (uint32_t k0 = 0; k0 < im.nseg; k0 += 64) {
         const uint32_t k = k0 + lane;
@@ -561,7 +426,7 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
         if (k < im.nseg) {
             const uint32_t s = im.seg_base + k;
             const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
-            n = max(1u, ((ce - cs) * 8 + kSubBits - 1) / kSubBits);
+            n = max(1u, uint32_t((uint64_t(ce - cs) * 8 + b.piece_bits - 1) / b.piece_bits));
         }
         const uint32_t incl = wave_incl_scan(n);
         if (k < im.nseg) {
@@ -571,7 +436,7 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
         }
         run += __shfl(int(incl), 63, 64);
     }
-    // n <= cap by construction (host bound: ceil(ECS bits / kSubBits) + nseg)
+    // run <= cap by construction (host bound: ceil(ECS bits / piece_bits) + nseg)
     const uint32_t used = min(run, im.sub_cap);
     for (uint32_t k = 0; k < im.nseg; k++) {
         const uint32_t s = im.seg_base + k;
@@ -582,176 +447,36 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     for (uint32_t u = used + lane; u < im.sub_cap; u += 64) b.sub_seg[im.sub_base + u] = kInvalidImage;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kHuffThreads) void k_decode(BatchDev b) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
-    stage_luts(b, ts, s_lut, kHuffThreads);
-
-    const uint32_t u = blockIdx.x * kHuffThreads + threadIdx.x;
-    const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
-    const bool valid = s != kInvalidImage;
-    SegInfo S;
-    uint32_t j = 0, nsub = 1;
-    if (valid) {
-        seg_info(b, s, S);
-        j = u - b.seg_sub_base[s];
-        nsub = b.seg_nsub[s];
-    } else {
-        S.data = S.last = uintptr_t(b.imgs) & ~uintptr_t(15);
-        S.bits = 0;
-        S.nblk = 0;
-        S.blk0 = 0;
-        S.ent0 = 0;
-        S.pattern = 0;
-        S.bpm = 1;
-    }
-    uint32_t* row = s_rows + threadIdx.x * kSubStride;  // [lane][word], odd pitch: conflict-free
-    const int off0 = load_row(row, 1, S.data, j, S.last);
-    __syncthreads();
-    if (!valid) return;
-
-    const bool last_sub = (j + 1 == nsub);
-    const int sub0 = int(j) * kSubBits;  // segment bit of the subsequence start
-    DecIn in;
-    in.blk = 0;
-    in.ent = 0;
-    in.pred0 = in.pred1 = in.pred2 = 0;
-    int p = 0, bi = 0, k = 0, ncur = 0;
-    if (MODE == 0) {
-        p = sub0;
-    } else if (MODE == 1) {
-        if (j > 0) {
-            const SubState e = b.exit_spec[u - 1];
-            p = int(e.p);
-            bi = int(e.sk >> 16);
-            k = int((e.sk >> 8) & 0xFFu);
-            ncur = int(e.sk & 0xFFu);
-        }
-    } else {
-        const SubEntry e = b.sub_entry[u];
-        p = int(e.p);
-        bi = int(e.sk >> 16);
-        k = int((e.sk >> 8) & 0xFFu);
-        ncur = int(e.sk & 0xFFu);
-        in.blk = e.blk;
-        in.ent = e.ent;
-        in.pred0 = e.pred[0];
-        in.pred1 = e.pred[1];
-        in.pred2 = e.pred[2];
-    }
-    // decode the symbols that start inside this subsequence (the last one: up to the data end;
-    // the write pass stops on the block count instead)
-    int end_bit = last_sub ? (MODE == 2 ? int(S.bits) + 64 : int(S.bits)) : sub0 + kSubBits;
-    in.bpos = p - sub0 + off0;
-    in.bend = end_bit - sub0 + off0;
-    in.bi = bi;
-    in.k = k;
-    in.ncur = ncur;
-    const int dsl[3] = {ts.dc_slot[0], ts.dc_slot[1], ts.dc_slot[2]};
-    const int asl[3] = {ts.ac_slot[0], ts.ac_slot[1], ts.ac_slot[2]};
-    DecOut o;
-    decode_run<MODE>(in, row, 1, s_lut, dsl, asl, S, b, o);
-    const uint32_t pexit = uint32_t(o.bpos - off0 + sub0);
-    if (MODE == 0) {
-        b.exit_spec[u] = SubState{pexit, pack_sk(o.bi, o.k, o.ncur)};
-    } else if (MODE == 1) {
-        b.exit_cnt[u] = SubState{pexit, pack_sk(o.bi, o.k, o.ncur)};
-        b.sub_cnt[u] = SubCount{o.nblocks, o.nent, {o.dc0, o.dc1, o.dc2}, 0u};
-    } else {
-        bool bad = o.bad;
-        if (last_sub && (o.blk != S.nblk || o.k != 0)) bad = true;  // data ran out before the last block
-        const bool finished_here = o.k == 0 && o.blk >= S.nblk && o.bpos > in.bpos;
-        if (finished_here) {
-            if (pexit > S.bits) bad = true;  // consumed bits past the interval's data
-            // after the last block only padding (< 1 byte) may precede the next RSTn: the
-            // oracle's restart looks for the marker right there (oracle/jdoracle.c br_restart)
-            const ImgDesc& im = b.imgs[b.seg_img[s]];
-            if (s + 1 < im.seg_base + im.nseg && (S.bits >> 3) > ((pexit + 7) >> 3)) bad = true;
-        }
-        if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// Stage 3a: restart-interval lanes (images with DRI).  One lane decodes one whole interval and
-// writes its blocks directly: within an interval the decoder state is known, so no
-// synchronisation passes are needed, and 4:2:0 MCU-phase ambiguity (which defeats cheap
-// self-synchronisation) never arises.
-//
-// The lane's bitstream streams through its own LDS row in windows of kWinAdv bytes.  A round
-// issues the loads of the NEXT window into registers, decodes every symbol that starts in the
-// current window, then commits the registers to the row.  The only vmcnt wait per round is that
-// commit, ~150 symbols after the loads were issued (gfx950 counts the coefficient stores on the
-// same counter, so waiting inside the symbol loop would stall on them).
-//
-// Row layout: word 0 = the word before the window (so a 32-bit peek at any bit is one funnel
-// shift of two adjacent words with no sh==0 special case), words 1.. = window bytes, MSB-first.
-// [lane][word] with an odd pitch: lanes reading the same word index hit distinct banks.
-//
-// Per symbol: 3 LDS reads (2 row words, 1 LUT entry), no global loads, branch-free value
-// extraction; table slots for DC/AC of every MCU block are packed 3 bits per block, so the
-// current table is two bit-field extracts away.
-// ------------------------------------------------------------------------------------------
-constexpr int kWinAdv = 128;                      // bytes a round advances
+constexpr int kWinAdv = 64;                       // bytes a round advances
 constexpr int kWinLoads = kWinAdv / 16 + 1;       // 16-byte loads per window (advance + overlap)
-constexpr int kRowWords = 1 + 4 * kWinLoads;      // 37: odd pitch (word 36 unused)
-constexpr int kLutWords = int(sizeof(HuffLut) / 4);
+constexpr int kRowWords = 1 + 4 * kWinLoads;      // 21: odd pitch (last word unused)
 static_assert(kRowWords % 2 == 1, "row pitch must be odd");
+constexpr int kWalkScan = 0, kWalkWrite = 1;
+constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 
-size_t seg_lds_bytes(uint32_t max_slots) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(kSegThreads) * kRowWords * 4;
+size_t piece_lds_bytes(uint32_t max_slots) {
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * kRowWords * 4;
 }
 
-// Canonical slow path (codes longer than kLutBits): the code length is kLutBits+1 plus the
-// number of left-justified limits <= v16 (F.2.2.3 restated), then the symbol from vals[].
-__device__ __forceinline__ uint32_t slow_code(const uint32_t* lut, uint32_t peek, uint32_t& sym, bool& bad) {
-    const HuffLut* t = reinterpret_cast<const HuffLut*>(lut);
-    const uint32_t v16 = peek >> 16;
-    uint32_t l = kLutBits + 1;
-#pragma unroll
-    for (int j = kLutBits + 1; j <= 16; j++) l += (v16 >= t->lim[j]) ? 1u : 0u;
-    if (l > 16) {
-        bad = true;
-        l = 16;
-    }
-    sym = t->vals[uint32_t(t->base[l] + int(v16 >> (16 - l))) & 255u];
-    return l;
-}
+// One walk over an interval's bits from `start`.
+//   scan : (true MCU-start state at `start` when warm_to == start, else speculative) until the
+//          first MCU boundary at/after warm_to = the piece start; then MCUs and AC entries until
+//          the first MCU boundary at/after stop_at (or past the data end)
+//   write: nmcu MCUs from the MCU boundary `start`: BlockInfo (DC difference) + AC entries
+struct Walk {
+    uint32_t start, warm_to, stop_at;   // scan
+    uint32_t nmcu, ent0;                // write
+    uint64_t blk0;                      // write: global block of the first MCU's first block
+    uint32_t m_start, m_end, mcus, ents;  // scan results (m_start = kNoPiece: none found)
+    uint32_t end;                       // bit after the last symbol decoded
+    bool bad;
+};
 
-template <int VARIANT>
-__global__ __launch_bounds__(kSegThreads) void k_seg(BatchDev b) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
-    const uint32_t* s_lutw = reinterpret_cast<const uint32_t*>(s_dyn);
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    const TableSet& ts = b.tablesets[b.lane_wg_tableset[blockIdx.x]];
-    stage_luts(b, ts, s_lut, kSegThreads);
-
-    const uint32_t s = b.seg_lane[blockIdx.x * kSegThreads + threadIdx.x];
-    const bool valid = s != kInvalidImage;
-    SegInfo S;
-    if (valid) {
-        seg_info(b, s, S);
-    } else {
-        S.data = S.last = uintptr_t(b.imgs) & ~uintptr_t(15);
-        S.bits = 0;
-        S.nblk = 0;
-        S.blk0 = 0;
-        S.ent0 = 0;
-        S.pattern = 0;
-        S.bpm = 1;
-    }
-    uint32_t dcp = 0, acp = 0;  // 3-bit table slot per MCU block
-    for (uint32_t q = 0; q < S.bpm && q < 10; q++) {
-        const uint32_t c = (S.pattern >> (2 * q)) & 3u;
-        dcp |= uint32_t(ts.dc_slot[c] & 7u) << (3 * q);
-        acp |= uint32_t(ts.ac_slot[c] & 7u) << (3 * q);
-    }
-    uint32_t* row = s_rows + threadIdx.x * kRowWords;  // window words 0 .. 4*kWinLoads-1
-    uintptr_t wa = S.data & ~uintptr_t(15);
+template <int MODE>
+__device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp,
+                                     uint32_t acp, uint32_t* row, bool active_in, Walk& W) {
+    const uintptr_t a_start = S.data + (W.start >> 3);
+    uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
     for (int q = 0; q < kWinLoads; q++) {
         const u32x4 v = load16(wa + 16 * q, S.last);
@@ -760,50 +485,72 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(BatchDev b) {
         row[4 * q + 2] = __builtin_bswap32(v.z);
         row[4 * q + 3] = __builtin_bswap32(v.w);
     }
-    // 64-bit bit buffer: the next symbol is always in its top 32 bits (nb >= 32 between steps).
-    // The word for the next refill is read one step ahead (nextw), so the only LDS latency on a
-    // symbol's critical path is its table lookup.
-    const uint32_t off = uint32_t(S.data & 15) * 8;
+    // 64-bit bit buffer: the next symbol is always in its top 32 bits (nb >= 32 between steps)
+    const uint32_t off = uint32_t(a_start & 15) * 8 + (W.start & 7u);
     int rp = int(off >> 5);
     uint64_t bb = ((uint64_t(row[rp]) << 32) | row[rp + 1]) << (off & 31);
     int nb = 64 - int(off & 31);
     rp += 2;
     uint32_t nextw = row[rp];
-    int consumed = 0;
+    int consumed = int(W.start);  // interval bit of the next symbol
     const int sbits = int(S.bits);
     const uint32_t ent_end = S.ent0 + 63u * S.nblk;
-    BlockInfo* const bout = b.blocks + (S.blk0 - 1);  // bout[blk] after blk++ = this block
+    BlockInfo* const bout = b.blocks + (W.blk0 - 1);  // bout[blk] after blk++ = this block
     uint32_t* const eout = b.entries;
-    // decode state (critical path)
-    int k = 0, bi = 0;
-    uint32_t nblk_seen = 0;
-    // bookkeeping state (off the critical path) and the pending step it has not consumed yet
-    uint32_t ent = S.ent0, ent_blk = S.ent0, blk = 0;
-    int p0 = 0, p1 = 0, p2 = 0, dc = 0;
-    bool q_valid = false, q_dc = false, q_emit = false, q_fin = false;
-    int q_val = 0, q_k = 0;
-    uint32_t q_comp = 0;
-    bool bad = false;
-    bool active = valid && S.nblk > 0;
     const int bpm = int(S.bpm);
-    // bookkeeping of one decoded symbol: DPCM (parser.cpp:106-111), AC entry, block record
-#define JD_SEG_BOOK()                                                                                          \
+    const uint32_t nblk = W.nmcu * S.bpm;
+    // decode state: k = next coefficient index (0: DC next), bi = block in MCU, tab = LDS word
+    // offset of the next symbol's table
+    int k = 0, bi = 0;
+    uint32_t actab = (acp & 7u) * uint32_t(kLutWords);
+    uint32_t tab = (dcp & 7u) * uint32_t(kLutWords);
+    uint32_t nblk_seen = 0;
+    // scan: phase 0 = synchronising, 1 = counting
+    uint32_t counting = (W.warm_to == W.start) ? 1u : 0u;
+    uint32_t mcus = 0, ents = 0, m_start = counting ? W.start : kNoPiece, m_end = 0;
+    // write: pending symbol whose bookkeeping runs while the next lookup is in flight.  Flags are
+    // integer bits in VGPRs (boolean lane masks would need SALU merges at divergent loop exits).
+    constexpr uint32_t kQValid = 1u, kQDc = 2u, kQEmit = 4u, kQFin = 8u;
+    uint32_t qf = 0, q_peek = 0, q_e = 0, q_k = 0;
+    uint32_t ent = W.ent0, ent_blk = W.ent0, blk = 0;
+    int dcd = 0;
+    // AC entries are write-combined into the aligned quad [ent & ~3, +4): one 16-byte store per
+    // four entries (a wave's 64 lanes store to 64 unrelated places, so store instructions, not
+    // bytes, are what the write pass is bound by).  The piece's first and last quads may be
+    // shared with neighbouring pieces: their entries are stored one by one.
+    uint32_t wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;
+    uint32_t bad = 0;
+    bool active = active_in && (MODE == kWalkScan || nblk > 0);
+    if (MODE == kWalkScan && counting && W.start + 8 > S.bits) {  // starts at the data end: empty
+        active = false;
+        m_end = W.start;
+    }
+#define JD_WALK_BOOK()                                                                                         \
     do {                                                                                                       \
-        const int pc0 = p0, pc1 = p1, pc2 = p2;                                                                \
-        const int pr = (q_comp == 0u ? pc0 : (q_comp == 1u ? pc1 : pc2)) + q_val;                              \
-        p0 = (q_dc && q_comp == 0u) ? pr : pc0;                                                                \
-        p1 = (q_dc && q_comp == 1u) ? pr : pc1;                                                                \
-        p2 = (q_dc && q_comp == 2u) ? pr : pc2;                                                                \
-        bad |= q_dc && (pr < -32768 || pr > 32767);                                                            \
-        dc = q_dc ? pr : dc;                                                                                   \
+        const bool q_dc = (qf & kQDc) != 0, q_emit = (qf & kQEmit) != 0;                                       \
+        const int val_ = huff_value(q_peek, q_e);                                                              \
+        dcd = q_dc ? val_ : dcd;                                                                               \
         ent_blk = q_dc ? ent : ent_blk;                                                                        \
         blk += q_dc ? 1u : 0u;                                                                                 \
         const bool st_ = q_emit && ent < ent_end;                                                              \
-        if (VARIANT != 1 && st_) eout[ent] = (uint32_t(q_val) << 16) | uint32_t(q_k);                          \
-        bad |= q_emit && !st_;                                                                                 \
+        const uint32_t ev_ = (uint32_t(val_) << 16) | q_k, sl_ = ent & 3u;                                     \
+        wq0 = (st_ && sl_ == 0u) ? ev_ : wq0;                                                                  \
+        wq1 = (st_ && sl_ == 1u) ? ev_ : wq1;                                                                  \
+        wq2 = (st_ && sl_ == 2u) ? ev_ : wq2;                                                                  \
+        wq3 = (st_ && sl_ == 3u) ? ev_ : wq3;                                                                  \
+        if (st_ && sl_ == 3u) {                                                                                \
+            const uint32_t qb_ = ent - 3u;                                                                     \
+            if (qb_ >= W.ent0) {                                                                               \
+                *reinterpret_cast<uint4*>(eout + qb_) = make_uint4(wq0, wq1, wq2, wq3);                        \
+            } else {                                                                                           \
+                if (qb_ + 1u >= W.ent0) eout[qb_ + 1u] = wq1;                                                  \
+                if (qb_ + 2u >= W.ent0) eout[qb_ + 2u] = wq2;                                                  \
+                eout[qb_ + 3u] = wq3;                                                                          \
+            }                                                                                                  \
+        }                                                                                                      \
+        bad |= (q_emit && !st_) ? 1u : 0u;                                                                     \
         ent += st_ ? 1u : 0u;                                                                                  \
-        if (VARIANT != 1 && q_fin)                                                                             \
-            bout[blk] = BlockInfo{ent_blk, (min(ent - ent_blk, 63u) << 16) | (uint32_t(dc) & 0xFFFFu)};       \
+        if (qf & kQFin) bout[blk] = BlockInfo{ent_blk, pack_cnt_dc(ent - ent_blk, dcd)};                       \
     } while (0)
     while (true) {
         const uintptr_t na = wa + kWinAdv;
@@ -811,31 +558,13 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(BatchDev b) {
 #pragma unroll
         for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
         while (active && rp <= kWinAdv / 4) {
-            // (1) table lookup for this symbol
             const uint32_t peek = uint32_t(bb >> 32);
-            const bool is_dc = (k == 0);
-            const uint32_t slot = __builtin_amdgcn_ubfe(is_dc ? dcp : acp, uint32_t(3 * bi), 3u);
-            const uint32_t* lut = s_lutw + slot * kLutWords;
-            uint32_t e = lut[peek >> (32 - kLutBits)];
-            // (2) while it is in flight: bookkeeping of the previous symbol
-            if (q_valid) JD_SEG_BOOK();
-            // (3) decode
-            if ((e & 31u) == 0) {  // code longer than kLutBits (0.3 % of symbols)
-                uint32_t sy;
-                const uint32_t l = slow_code(lut, peek, sy, bad);
-                e = l | (sy << 8);
-            }
-            const uint32_t clen = e & 31u;
-            const uint32_t sym = __builtin_amdgcn_ubfe(e, 8u, 8u);
-            const uint32_t sz0 = is_dc ? sym : (sym & 15u);
-            bad |= sz0 > 16u;  // DC size beyond 16 bits: corrupt table/stream
-            const uint32_t sz = min(sz0, 16u);
-            const bool complete = (e & kLutFlagComplete) != 0;
-            const uint32_t L = complete ? clen : clen + sz;
-            const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - clen - sz, sz);  // width 0 -> 0
-            const uint32_t half = (1u << sz) >> 1;
-            const int v = int(mag) - (mag < half ? int(2 * half - 1) : 0);  // EXTEND, stream.cpp:44-52
-            // consume L bits, refill one word if fewer than 32 remain
+            const bool is_dc = k == 0;
+            uint32_t e = s_lutw[tab + (peek >> (32 - kLutBits))];
+            if (MODE == kWalkWrite && (qf & kQValid)) JD_WALK_BOOK();  // overlaps the lookup
+            if ((e & 31u) == 0) e = huff_slow(s_lutw + tab, peek, is_dc);  // 0.3 % of symbols
+            bad |= (MODE == kWalkWrite || counting) ? ((e >> 16) & 1u) : 0u;
+            const uint32_t L = e & 31u;
             bb <<= L;
             nb -= int(L);
             const bool need = nb < 32;
@@ -844,22 +573,42 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(BatchDev b) {
             rp += need ? 1 : 0;
             nextw = row[rp];
             consumed += int(L);
-            // next decoder state (EOB / ZRL / run-size, parser.cpp:114-134)
-            const int knew = k + int(sym >> 4);
-            const int kn = is_dc ? 1 : (sym == 0 ? 64 : (knew < 64 ? knew + 1 : knew));
-            const bool fin = kn >= 64;
-            q_valid = true;
-            q_dc = is_dc;
-            q_comp = __builtin_amdgcn_ubfe(S.pattern, uint32_t(2 * bi), 2u);
-            q_val = complete ? (int32_t(e) >> 16) : v;
-            q_emit = !is_dc && (sym & 15u) != 0 && knew < 64;
-            q_k = knew;
-            q_fin = fin;
-            nblk_seen += is_dc ? 1u : 0u;
-            bi = fin ? (bi + 1 == bpm ? 0 : bi + 1) : bi;
-            k = fin ? 0 : kn;
-            bad |= consumed > sbits;  // consumed bits past the interval's data
-            active = !bad && !(fin && nblk_seen >= S.nblk);
+            // EOB / ZRL / run-size (parser.cpp:114-134)
+            const int knew = k + int(__builtin_amdgcn_ubfe(e, 5u, 4u));
+            const bool fin = !is_dc && ((e & 512u) != 0 || knew >= 63);
+            const bool emit = !is_dc && (e & 1024u) != 0 && knew < 64;
+            const int nbi = (bi + 1 == bpm) ? 0 : bi + 1;
+            if (MODE == kWalkWrite) {
+                qf = kQValid | (is_dc ? kQDc : 0u) | (emit ? kQEmit : 0u) | (fin ? kQFin : 0u);
+                q_peek = peek;
+                q_e = e;
+                q_k = uint32_t(knew);
+                nblk_seen += is_dc ? 1u : 0u;
+                bad |= consumed > sbits ? 1u : 0u;  // consumed bits past the interval's data
+                active = !bad && !(fin && nblk_seen >= nblk);
+            } else {
+                ents += (counting && emit) ? 1u : 0u;
+                const bool mcu_end = fin && nbi == 0;
+                const bool sync_done = !counting && mcu_end && uint32_t(consumed) >= W.warm_to;
+                // stop at the first MCU boundary at/after stop_at, or within the last byte (the data
+                // ends there: later pieces are empty; an early stop only costs a chain re-scan)
+                const bool at_end = consumed + 8 > sbits;
+                const bool count_done =
+                    (counting && mcu_end && (uint32_t(consumed) >= W.stop_at || at_end)) || (sync_done && at_end);
+                mcus += (counting && mcu_end) ? 1u : 0u;
+                m_start = sync_done ? uint32_t(consumed) : m_start;
+                m_end = count_done ? uint32_t(consumed) : m_end;
+                counting = sync_done ? 1u : counting;
+                const bool over = consumed > sbits;  // past the data: the walk cannot go on
+                bad |= (counting && over && !count_done) ? 1u : 0u;
+                const bool stop = count_done || over || bad;
+                m_end = stop ? uint32_t(consumed) : m_end;
+                active = !stop;
+            }
+            bi = fin ? nbi : bi;
+            actab = fin ? __builtin_amdgcn_ubfe(acp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
+            tab = fin ? __builtin_amdgcn_ubfe(dcp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
+            k = fin ? 0 : (is_dc ? 1 : knew + 1);
         }
         if (__ballot(active) == 0) break;  // wave-uniform
 #pragma unroll
@@ -872,115 +621,265 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(BatchDev b) {
         rp -= kWinAdv / 4;
         wa = na;
     }
-    if (q_valid) JD_SEG_BOOK();
-#undef JD_SEG_BOOK
-    if (!valid) return;
-    const uint32_t pexit = uint32_t(consumed);
-    if (S.nblk > 0 && !bad) {
-        if (blk != S.nblk || k != 0) bad = true;
-        // after the last block only padding (< 1 byte) may precede the next RSTn: the oracle's
-        // restart looks for the marker right there (oracle/jdoracle.c br_restart)
-        const ImgDesc& im = b.imgs[b.seg_img[s]];
-        if (s + 1 < im.seg_base + im.nseg && (S.bits >> 3) > ((pexit + 7) >> 3)) bad = true;
+    if (MODE == kWalkWrite && (qf & kQValid)) JD_WALK_BOOK();
+#undef JD_WALK_BOOK
+    if (MODE == kWalkWrite && (ent & 3u)) {  // the last, partial quad
+        const uint32_t qb = ent & ~3u;
+        if (qb >= W.ent0) eout[qb] = wq0;
+        if (ent > qb + 1u && qb + 1u >= W.ent0) eout[qb + 1u] = wq1;
+        if (ent > qb + 2u && qb + 2u >= W.ent0) eout[qb + 2u] = wq2;
     }
-    if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
-    atomicAdd(&b.counters[0], (unsigned long long)(ent - S.ent0));
+    W.end = uint32_t(consumed);
+    W.bad = bad != 0;
+    if (MODE == kWalkWrite) {
+        W.bad = W.bad || (nblk > 0 && (nblk_seen != nblk || k != 0));
+        W.ents = ent - W.ent0;
+    } else {
+        W.m_start = m_start;
+        W.m_end = m_end;
+        W.mcus = mcus;
+        W.ents = ents;
+    }
 }
 
-// Per segment (one wave): verify the subsequence chain, re-decode broken links, prefix sums.
-__global__ __launch_bounds__(64) void k_chain(BatchDev b) {
+__device__ __forceinline__ void table_slots(const TableSet& ts, const SegInfo& S, uint32_t& dcp, uint32_t& acp) {
+    dcp = acp = 0;  // 3-bit table slot per MCU block
+    for (uint32_t q = 0; q < S.bpm && q < 10; q++) {
+        const uint32_t c = (S.pattern >> (2 * q)) & 3u;
+        dcp |= uint32_t(ts.dc_slot[c] & 7u) << (3 * q);
+        acp |= uint32_t(ts.ac_slot[c] & 7u) << (3 * q);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
-    uint32_t* s_row = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
+    stage_luts(b, ts, s_lut, kPieceThreads);
+    __syncthreads();
+
+    const uint32_t u = blockIdx.x * kPieceThreads + threadIdx.x;
+    const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
+    bool valid = s != kInvalidImage;
+    SegInfo S;
+    uint32_t j = 0, npc = 1, nmcu_seg = 0;
+    if (valid) {
+        seg_info(b, s, S);
+        j = u - b.seg_sub_base[s];
+        npc = b.seg_nsub[s];
+        nmcu_seg = S.nblk / S.bpm;
+    } else {
+        seg_invalid(b, S);
+    }
+    uint32_t dcp, acp;
+    table_slots(ts, S, dcp, acp);
+    Walk W;
+    W.nmcu = 0;
+    W.ent0 = 0;
+    W.blk0 = 0;
+    if (MODE == kWalkScan) {
+        // piece 0 counts from bit 0 in the true state; piece j > 0 synchronises from
+        // piece_overlap bits before its nominal start (from bit 0, exactly, when that is closer)
+        const uint64_t pstart = uint64_t(j) * b.piece_bits;
+        W.warm_to = (j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
+        W.start = (pstart <= b.piece_overlap) ? 0u : min(uint32_t(pstart - b.piece_overlap), W.warm_to);
+        W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(pstart + b.piece_bits, 0xFFFFFFFEu));
+    } else {
+        W.start = valid ? b.piece_bit[u] : 0u;
+        W.warm_to = W.start;
+        W.stop_at = 0;
+        if (valid) {
+            const uint32_t m0 = b.piece_mcu0[u];
+            W.nmcu = b.piece_nmcu[u];
+            W.ent0 = b.piece_ent0[u];
+            // never write outside the interval (the chain flagged inconsistent counts as corrupt)
+            if (W.start == kNoPiece || W.start > S.bits || m0 + W.nmcu > nmcu_seg || W.ent0 > S.ent0 + 63u * S.nblk)
+                valid = false;
+            W.blk0 = S.blk0 + uint64_t(m0) * S.bpm;
+        }
+        if (!valid) {
+            seg_invalid(b, S);
+            W.start = W.warm_to = 0;
+            W.nmcu = 0;
+        }
+    }
+    walk<MODE>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
+    if (!valid) return;
+    if (MODE == kWalkScan) {
+        // piece 0 starts at bit 0 whatever its walk found (it is the true state)
+        b.piece_bit[u] = (j == 0) ? 0u : W.m_start;
+        b.piece_end[u] = W.m_end;
+        b.piece_nmcu[u] = W.mcus | (W.bad ? 0x80000000u : 0u);  // bit 31: error while counting
+        b.piece_nent[u] = W.ents;
+    } else {
+        bool bad = W.bad;
+        if (j + 1 == npc && !bad) {
+            const uint32_t end = W.nmcu > 0 ? W.end : W.start;
+            if (end > S.bits) bad = true;
+            // after the last block only padding (< 1 byte) may precede the next RSTn: the
+            // oracle's restart looks for the marker right there (oracle/jdoracle.c br_restart)
+            const ImgDesc& im = b.imgs[b.seg_img[s]];
+            if (s + 1 < im.seg_base + im.nseg && (S.bits >> 3) > ((end + 7) >> 3)) bad = true;
+        }
+        if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+        atomicAdd(&b.counters[0], (unsigned long long)W.ents);
+    }
+}
+
+// Lane per piece: re-scan, all at once, every piece whose speculative start disagrees with its
+// predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images).
+// Starting from that end is exact when the predecessor is right; if the predecessor is itself
+// re-scanned in this round the start may be stale, which k_chain's serial verification catches.
+__global__ __launch_bounds__(kPieceThreads) void k_rescan(BatchDev b) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    const uint32_t u = blockIdx.x * kPieceThreads + threadIdx.x;
+    const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
+    uint32_t j = 0, npc = 1, expect = 0;
+    bool need = false;
+    if (s != kInvalidImage) {
+        j = u - b.seg_sub_base[s];
+        npc = b.seg_nsub[s];
+        if (j > 0) {
+            expect = b.piece_end[u - 1];
+            need = b.piece_bit[u] != expect;
+        }
+    }
+    if (!__syncthreads_or(need)) return;  // workgroup-uniform
+    const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
+    stage_luts(b, ts, s_lut, kPieceThreads);
+    __syncthreads();
+    SegInfo S;
+    if (need) seg_info(b, s, S);
+    else seg_invalid(b, S);
+    uint32_t dcp, acp;
+    table_slots(ts, S, dcp, acp);
+    Walk W;
+    W.start = W.warm_to = expect;
+    W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
+    W.nmcu = W.ent0 = 0;
+    W.blk0 = 0;
+    walk<kWalkScan>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, need, W);
+    if (!need) return;
+    b.piece_bit[u] = W.start;
+    b.piece_end[u] = W.m_end;
+    b.piece_nmcu[u] = W.mcus | (W.bad ? 0x80000000u : 0u);
+    b.piece_nent[u] = W.ents;
+}
+
+// One lane per interval (workgroups grouped by table set): verify that every piece starts where
+// its predecessor ended; re-scan a piece whose speculative start had not synchronised (the
+// workgroup stages its tables only when some lane needs one); prefix sums give each piece its
+// first MCU and first AC-entry slot.
+__global__ __launch_bounds__(kPieceThreads) void k_chain(BatchDev b) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    const uint32_t li = blockIdx.x * kPieceThreads + threadIdx.x;
+    const uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
+    const TableSet& ts = b.tablesets[b.chain_wg_tableset[blockIdx.x]];
+    const bool valid = s != kInvalidImage;
+    SegInfo S;
+    uint32_t base = 0, n = 0;
+    if (valid) {
+        seg_info(b, s, S);
+        base = b.seg_sub_base[s];
+        n = b.seg_nsub[s];
+    } else {
+        seg_invalid(b, S);
+    }
+    // does any piece need a re-scan?  (the first mismatch is enough to know)
+    bool need = false;
+    {
+        uint32_t expect = 0;
+        for (uint32_t j = 0; j < n && !need; j++) {
+            need = b.piece_bit[base + j] != expect;
+            expect = b.piece_end[base + j];
+        }
+    }
+    if (__syncthreads_or(need)) {
+        stage_luts(b, ts, s_lut, kPieceThreads);
+        __syncthreads();
+    }
+    if (!valid) return;
+    uint32_t dcp, acp;
+    table_slots(ts, S, dcp, acp);
+    const uint32_t nmcu_seg = S.nblk / S.bpm;
+    bool bad = false;
+    uint32_t expect = 0, mcu_run = 0, ent_run = S.ent0;
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t u = base + j;
+        uint32_t pbit = b.piece_bit[u], pend = b.piece_end[u], pm = b.piece_nmcu[u], pe = b.piece_nent[u];
+        bool pbad = (pm >> 31) != 0;  // the piece's scan hit an error while counting
+        pm &= 0x7FFFFFFFu;
+        if (pbit != expect) {  // the speculative start had not synchronised: re-scan from the truth
+            Walk W;
+            W.start = W.warm_to = expect;
+            W.stop_at = (j + 1 == n) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
+            W.nmcu = W.ent0 = 0;
+            W.blk0 = 0;
+            walk<kWalkScan>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
+                            true, W);
+            pbit = expect;
+            pend = W.m_end;
+            pm = W.mcus;
+            pe = W.ents;
+            pbad = W.bad;
+            b.piece_bit[u] = pbit;
+        }
+        // counting from a verified start is exact, so an error there is the stream's; the last
+        // piece's scan runs past the data on purpose (its write lane checks it exactly)
+        if (j + 1 < n) {
+            bad |= pbad;
+        } else {  // the last piece takes the interval's remaining MCUs
+            if (mcu_run > nmcu_seg) bad = true;
+            pm = nmcu_seg >= mcu_run ? nmcu_seg - mcu_run : 0u;
+        }
+        b.piece_mcu0[u] = mcu_run;
+        b.piece_nmcu[u] = pm;
+        b.piece_ent0[u] = ent_run;
+        mcu_run += pm;
+        ent_run += pe;
+        expect = pend;
+    }
+    if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+}
+
+// One wave per interval: DC differences -> DC values, per component (parser.cpp:106-111: the
+// predictor restarts at 0 at every interval), with the reference's int16 range check.
+__global__ __launch_bounds__(64) void k_dpcm(BatchDev b) {
     const uint32_t s = blockIdx.x;
-    const int lane = threadIdx.x;
     SegInfo S;
     seg_info(b, s, S);
-    const ImgDesc& im = b.imgs[b.seg_img[s]];
-    const TableSet& ts = b.tablesets[im.tableset];
-    const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
-    if (n == 0) return;  // interval decoded by k_seg
-    bool luts = false;
-    SubState carry{0u, 0u};  // true exit of the previous chunk's last subsequence
-    uint32_t blk_run = 0, ent_run = S.ent0;
-    int pr0 = 0, pr1 = 0, pr2 = 0;
-    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+    const uint32_t lane = threadIdx.x;
+    int run0 = 0, run1 = 0, run2 = 0;
+    bool bad = false;
+    uint32_t bb0 = 0;  // MCU position of the chunk's first block
+    for (uint32_t c0 = 0; c0 < S.nblk; c0 += 64) {
         const uint32_t j = c0 + lane;
-        const bool in = j < n;
-        const uint32_t u = base + j;
-        SubState ex = in ? b.exit_cnt[u] : SubState{0u, 0u};
-        SubCount ct = in ? b.sub_cnt[u] : SubCount{0u, 0u, {0, 0, 0}, 0u};
-        const SubState used = (in && j > 0) ? b.exit_spec[u - 1] : SubState{0u, 0u};
-        SubState te;  // true entry = true exit of the predecessor
-        te.p = uint32_t(__shfl_up(int(ex.p), 1, 64));
-        te.sk = uint32_t(__shfl_up(int(ex.sk), 1, 64));
-        if (lane == 0) te = (j == 0) ? SubState{0u, 0u} : carry;
-        bool mm = in && (te.p != used.p || te.sk != used.sk);
-        uint64_t mask = __ballot(mm);
-        while (mask) {
-            const int v = __builtin_ctzll(mask);
-            if (!luts) {  // wave-uniform
-                stage_luts(b, ts, s_lut, 64);
-                luts = true;
-            }
-            const uint32_t jv = c0 + uint32_t(v);
-            const uint32_t tp = uint32_t(__shfl(int(te.p), v, 64)), tsk = uint32_t(__shfl(int(te.sk), v, 64));
-            __syncthreads();
-            int off0 = 0;
-            if (lane == 0) off0 = load_row(s_row, 1, S.data, jv, S.last);
-            off0 = __shfl(off0, 0, 64);
-            __syncthreads();
-            const int sub0 = int(jv) * kSubBits;
-            const bool lastv = (jv + 1 == n);
-            DecIn din;
-            din.bpos = int(tp) - sub0 + off0;
-            din.bend = (lastv ? int(S.bits) : sub0 + kSubBits) - sub0 + off0;
-            din.bi = int(tsk >> 16);
-            din.k = int((tsk >> 8) & 0xFFu);
-            din.ncur = int(tsk & 0xFFu);
-            din.blk = din.ent = 0;
-            din.pred0 = din.pred1 = din.pred2 = 0;
-            const int dsl[3] = {ts.dc_slot[0], ts.dc_slot[1], ts.dc_slot[2]};
-            const int asl[3] = {ts.ac_slot[0], ts.ac_slot[1], ts.ac_slot[2]};
-            DecOut o;
-            decode_run<1>(din, s_row, 1, s_lut, dsl, asl, S, b, o);  // every lane: same result
-            const SubState nex{uint32_t(o.bpos - off0 + sub0), pack_sk(o.bi, o.k, o.ncur)};
-            if (lane == v) {
-                ex = nex;
-                ct = SubCount{o.nblocks, o.nent, {o.dc0, o.dc1, o.dc2}, 0u};
-                mm = false;
-            }
-            if (lane == v + 1) {
-                te = nex;
-                mm = in && (te.p != used.p || te.sk != used.sk);
-            }
-            if (v == 63) carry = nex;  // next chunk's lane 0 compares against it
-            mask = __ballot(mm);
-        }
-        // prefix sums over the chunk
-        const uint32_t ib = wave_incl_scan(ct.blocks), ie = wave_incl_scan(ct.entries);
-        const uint32_t i0 = wave_incl_scan(uint32_t(ct.dc[0])), i1 = wave_incl_scan(uint32_t(ct.dc[1])),
-                       i2 = wave_incl_scan(uint32_t(ct.dc[2]));
+        const bool in = j < S.nblk;
+        const uint32_t bq = (bb0 + lane) % S.bpm;  // MCU block index of block j
+        const uint32_t comp = (S.pattern >> (2 * bq)) & 3u;
+        BlockInfo bi = in ? b.blocks[S.blk0 + j] : BlockInfo{0u, 0u};
+        const int d = int32_t(bi.cnt_dc << 6) >> 6;
+        const int i0 = int(wave_incl_scan(uint32_t(comp == 0 ? d : 0)));
+        const int i1 = int(wave_incl_scan(uint32_t(comp == 1 ? d : 0)));
+        const int i2 = int(wave_incl_scan(uint32_t(comp == 2 ? d : 0)));
+        const int v = comp == 0 ? run0 + i0 : (comp == 1 ? run1 + i1 : run2 + i2);
         if (in) {
-            SubEntry e;
-            e.p = te.p;
-            e.sk = te.sk;
-            e.blk = blk_run + ib - ct.blocks;
-            e.ent = ent_run + ie - ct.entries;
-            e.pred[0] = pr0 + int(i0 - uint32_t(ct.dc[0]));
-            e.pred[1] = pr1 + int(i1 - uint32_t(ct.dc[1]));
-            e.pred[2] = pr2 + int(i2 - uint32_t(ct.dc[2]));
-            e.pad = 0;
-            b.sub_entry[u] = e;
+            bad |= v < -32768 || v > 32767;
+            bi.cnt_dc = (bi.cnt_dc & 0xFC000000u) | (uint32_t(v) & 0x3FFFFFFu);
+            b.blocks[S.blk0 + j] = bi;
         }
-        blk_run += uint32_t(__shfl(int(ib), 63, 64));
-        ent_run += uint32_t(__shfl(int(ie), 63, 64));
-        pr0 += __shfl(int(i0), 63, 64);
-        pr1 += __shfl(int(i1), 63, 64);
-        pr2 += __shfl(int(i2), 63, 64);
-        const uint32_t cp = uint32_t(__shfl(int(ex.p), 63, 64)), csk = uint32_t(__shfl(int(ex.sk), 63, 64));
-        carry = SubState{cp, csk};
+        run0 += __shfl(i0, 63, 64);
+        run1 += __shfl(i1, 63, 64);
+        run2 += __shfl(i2, 63, 64);
+        bb0 = (bb0 + 64) % S.bpm;
     }
+    if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1233,13 +1132,13 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
         const uint64_t gb = im.block_base + uint64_t((r0 + mr) * im.mcux + m0 + mi) * bpm + bb;
         const BlockInfo bi = b.blocks[gb];
         // a block of a corrupt stream may never have been written: never index past the entries
-        int cnt = min(int(bi.cnt_dc >> 16), 63);
+        int cnt = int(bi.cnt_dc >> 26);
         if (uint64_t(bi.entry_start) + uint64_t(cnt) > b.entries_cap) cnt = 0;
-        row[0] = int(int16_t(bi.cnt_dc & 0xFFFFu)) * int(s_tab[comp][0] >> 6);
+        row[0] = (int32_t(bi.cnt_dc << 6) >> 6) * int(s_tab[comp][0] >> 6);
         // entries in 16-byte loads, four in flight at a time (the entry buffer is padded by 64 B)
         const uint32_t lead = bi.entry_start & 3u;
         const uint32_t* ep = b.entries + (bi.entry_start - lead);
-        const int n4 = int(lead + uint32_t(cnt) + 3u) >> 2;
+        const int n4 = cnt > 0 ? int(lead + uint32_t(cnt) + 3u) >> 2 : 0;  // cnt == 0: touch nothing
         for (int c = 0; c < n4; c += 4) {
             uint4 v[4];
 #pragma unroll
@@ -1414,30 +1313,20 @@ hipError_t launch_compact(const BatchDev& b, hipStream_t s) {
     return hipGetLastError();
 }
 
-size_t huffman_lds_bytes(uint32_t max_slots) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(kSubStride) * kHuffThreads * 4;
-}
+size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots); }
 
 hipError_t launch_huffman(const BatchDev& b, hipStream_t s) {
-    if (!b.nimg) return hipSuccess;
-    if (b.nseg_lane) {
-        static const int variant = getenv("JD_SEG_VARIANT") ? atoi(getenv("JD_SEG_VARIANT")) : 0;  // A/B experiments
-        if (variant == 1)
-            hipLaunchKernelGGL(k_seg<1>, dim3(b.nseg_lane / kSegThreads), dim3(kSegThreads), seg_lds_bytes(b.max_slots), s, b);
-        else
-            hipLaunchKernelGGL(k_seg<0>, dim3(b.nseg_lane / kSegThreads), dim3(kSegThreads), seg_lds_bytes(b.max_slots), s, b);
-    }
-    if (!b.nsub) return hipGetLastError();
-    const size_t lds = huffman_lds_bytes(b.max_slots);
-    const size_t lds_chain = size_t(b.max_slots) * sizeof(HuffLut) + size_t(kSubStride + 1) * 4;
-    // every slot not claimed by a segment (per-image slack, workgroup padding) must read invalid
+    if (!b.nimg || !b.nsub) return hipSuccess;
+    const size_t lds = piece_lds_bytes(b.max_slots);
+    // every slot not claimed by an interval (per-image slack, workgroup padding) must read invalid
     hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_subplan, dim3(b.nimg), dim3(64), 0, s, b);
-    hipLaunchKernelGGL(k_decode<0>, dim3(b.nsub / kHuffThreads), dim3(kHuffThreads), lds, s, b);
-    hipLaunchKernelGGL(k_decode<1>, dim3(b.nsub / kHuffThreads), dim3(kHuffThreads), lds, s, b);
-    hipLaunchKernelGGL(k_chain, dim3(b.nseg), dim3(64), lds_chain, s, b);
-    hipLaunchKernelGGL(k_decode<2>, dim3(b.nsub / kHuffThreads), dim3(kHuffThreads), lds, s, b);
+    hipLaunchKernelGGL(k_piece<kWalkScan>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+    hipLaunchKernelGGL(k_rescan, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+    hipLaunchKernelGGL(k_chain, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+    hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+    hipLaunchKernelGGL(k_dpcm, dim3(b.nseg), dim3(64), 0, s, b);
     return hipGetLastError();
 }
 

@@ -151,11 +151,6 @@ done:
     return JD_OK;
 }
 
-static inline int extend(int v, int s) {
-    if (s == 0) return 0;
-    const int l = 1 << (s - 1);
-    return v >= l ? v : v - ((l << 1) - 1);
-}
 
 bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
     memset(lut, 0, sizeof(*lut));
@@ -179,22 +174,10 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
     for (int i = 0; i < k; i++) {
         const int l = lens[i];
         if (l > kLutBits) continue;
-        const int sym = h.vals[i];
-        const int s = is_dc ? sym : (sym & 15);
+        const uint32_t e = lut_entry(uint32_t(l), h.vals[i], is_dc);  // 0: decoded (and rejected) by the slow path
         const int shift = kLutBits - l;
         const int first = codes[i] << shift, last = ((codes[i] + 1) << shift) - 1;
-        for (int idx = first; idx <= last; idx++) {
-            uint32_t e;
-            if (s <= 16 && l + s <= kLutBits) {
-                const int bits = (idx >> (kLutBits - l - s)) & ((1 << s) - 1);
-                const int val = extend(bits, s);
-                e = uint32_t(l + s) | kLutFlagComplete | (uint32_t(sym) << 8) |
-                    (uint32_t(uint16_t(int16_t(val))) << 16);
-            } else {
-                e = uint32_t(l) | (uint32_t(sym) << 8);
-            }
-            lut->fast[idx] = e;
-        }
+        for (int idx = first; idx <= last; idx++) lut->fast[idx] = e;
     }
     return true;
 }

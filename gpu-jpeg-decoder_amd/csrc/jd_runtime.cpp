@@ -164,7 +164,8 @@ struct Plan {
     std::vector<TableSet> tablesets;
     std::vector<uint16_t> qtabs;
     std::vector<uint32_t> seg_img, seg_entry, wg_tableset;
-    std::vector<uint32_t> seg_lane, lane_wg_tableset;  // k_seg lanes, grouped by table set
+    uint32_t piece_bits = kPieceBits;
+    std::vector<uint32_t> chain_seg, chain_wg_tableset;  // k_chain lanes, grouped by table set
     uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, max_slots = 1, nsub = 0;
     uint64_t total_blocks = 0, total_entry_cap = 0, comp_bytes = 0;
     double pixels = 0, ecs_bytes = 0;
@@ -332,33 +333,23 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     for (size_t i = 0; i < order.size(); i++) order[i] = uint32_t(i);
     std::stable_sort(order.begin(), order.end(),
                      [&](uint32_t a, uint32_t b) { return ts_of_img[a] < ts_of_img[b]; });
-    // images with enough restart intervals: one k_seg lane per interval; the others are cut
-    // into subsequences for the self-synchronising passes
-    auto lane_mode = [&](const ImgDesc& d) {
-        if (ctx->flags & JD_FLAG_FORCE_SYNC) return false;
-        if (ctx->flags & JD_FLAG_FORCE_LANES) return true;
-        return d.restart_interval != 0 && d.nseg >= kMinLaneSegments;
-    };
+    // piece slots: per image ceil(ECS bits / piece_bits) + nseg (interval lengths are only known
+    // on the GPU), grouped by table set so each k_piece workgroup stages one table set
+    P.piece_bits = (ctx->flags & JD_FLAG_FORCE_SYNC) ? 1024u : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u : kPieceBits;
     uint64_t sub = 0;
     for (size_t oi = 0; oi < order.size();) {
         const int ts = ts_of_img[order[oi]];
-        size_t oj = oi;
-        for (; oj < order.size() && ts_of_img[order[oj]] == ts; oj++) {
-            ImgDesc& d = P.imgs[order[oj]];
+        for (; oi < order.size() && ts_of_img[order[oi]] == ts; oi++) {
+            ImgDesc& d = P.imgs[order[oi]];
             d.sub_base = uint32_t(sub);
-            if (lane_mode(d)) {
-                d.sub_cap = 0;
-                for (uint32_t k = 0; k < d.nseg; k++) P.seg_lane.push_back(d.seg_base + k);
-            } else {
-                d.sub_cap = uint32_t((uint64_t(d.len - d.ecs_off) * 8 + kSubBits - 1) / kSubBits + d.nseg);
-                sub += d.sub_cap;
-            }
+            d.sub_cap = uint32_t((uint64_t(d.len - d.ecs_off) * 8 + P.piece_bits - 1) / P.piece_bits + d.nseg);
+            sub += d.sub_cap;
+            for (uint32_t k = 0; k < d.nseg; k++) P.chain_seg.push_back(d.seg_base + k);
         }
-        oi = oj;
-        sub = align_up(sub, kHuffThreads);
-        while (P.wg_tableset.size() < sub / kHuffThreads) P.wg_tableset.push_back(uint32_t(ts));
-        while (P.seg_lane.size() % kSegThreads) P.seg_lane.push_back(kInvalidImage);
-        while (P.lane_wg_tableset.size() < P.seg_lane.size() / kSegThreads) P.lane_wg_tableset.push_back(uint32_t(ts));
+        sub = align_up(sub, kPieceThreads);
+        while (P.wg_tableset.size() < sub / kPieceThreads) P.wg_tableset.push_back(uint32_t(ts));
+        while (P.chain_seg.size() % kPieceThreads) P.chain_seg.push_back(kInvalidImage);
+        while (P.chain_wg_tableset.size() < P.chain_seg.size() / kPieceThreads) P.chain_wg_tableset.push_back(uint32_t(ts));
     }
     if (sub > 0x7FFFFFFFull) return JD_ERR_CAPACITY;
     P.nsub = uint32_t(sub);
@@ -439,8 +430,8 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         const size_t o_segimg = put(blob, P.seg_img);
         const size_t o_segent = put(blob, P.seg_entry);
         const size_t o_wgts = put(blob, P.wg_tableset);
-        const size_t o_lane = put(blob, P.seg_lane);
-        const size_t o_lanets = put(blob, P.lane_wg_tableset);
+        const size_t o_chain = put(blob, P.chain_seg);
+        const size_t o_chts = put(blob, P.chain_wg_tableset);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
         const size_t o_ctr = put(blob, std::vector<unsigned long long>(2, 0));
         const size_t upload = blob.size();
@@ -454,10 +445,8 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         const size_t o_ssb = reserve(end, nseg * 4);
         const size_t o_sns = reserve(end, nseg * 4);
         const size_t o_subseg = reserve(end, nsub * 4);
-        const size_t o_exs = reserve(end, nsub * sizeof(SubState));
-        const size_t o_exc = reserve(end, nsub * sizeof(SubState));
-        const size_t o_cnt = reserve(end, nsub * sizeof(SubCount));
-        const size_t o_sent = reserve(end, nsub * sizeof(SubEntry));
+        size_t o_piece[6];
+        for (int q = 0; q < 6; q++) o_piece[q] = reserve(end, nsub * 4);
         HIPCHK(ctx, ensure_dev(ctx->plan, end));
         HIPCHK(ctx, ensure_pin(ctx->plan_host, upload));
         memcpy(ctx->plan_host.p, blob.data(), upload);
@@ -483,14 +472,21 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         b.seg_nsub = reinterpret_cast<uint32_t*>(base + o_sns);
         b.sub_seg = reinterpret_cast<uint32_t*>(base + o_subseg);
         b.nsub = uint32_t(nsub);
-        b.exit_spec = reinterpret_cast<SubState*>(base + o_exs);
-        b.exit_cnt = reinterpret_cast<SubState*>(base + o_exc);
-        b.sub_cnt = reinterpret_cast<SubCount*>(base + o_cnt);
-        b.sub_entry = reinterpret_cast<SubEntry*>(base + o_sent);
         b.wg_tableset = reinterpret_cast<const uint32_t*>(base + o_wgts);
-        b.seg_lane = reinterpret_cast<const uint32_t*>(base + o_lane);
-        b.nseg_lane = uint32_t(P.seg_lane.size());
-        b.lane_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_lanets);
+        b.chain_seg = reinterpret_cast<const uint32_t*>(base + o_chain);
+        b.nchain = uint32_t(P.chain_seg.size());
+        b.chain_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_chts);
+        b.piece_bits = P.piece_bits;
+        b.piece_overlap = kPieceOverlap;
+        uint32_t* const pc[6] = {reinterpret_cast<uint32_t*>(base + o_piece[0]), reinterpret_cast<uint32_t*>(base + o_piece[1]),
+                                 reinterpret_cast<uint32_t*>(base + o_piece[2]), reinterpret_cast<uint32_t*>(base + o_piece[3]),
+                                 reinterpret_cast<uint32_t*>(base + o_piece[4]), reinterpret_cast<uint32_t*>(base + o_piece[5])};
+        b.piece_bit = pc[0];
+        b.piece_end = pc[1];
+        b.piece_nmcu = pc[2];
+        b.piece_nent = pc[3];
+        b.piece_mcu0 = pc[4];
+        b.piece_ent0 = pc[5];
         b.max_slots = P.max_slots;
         b.max_chunks = P.max_chunks;
         b.chunk_nbrk = reinterpret_cast<uint32_t*>(base + o_nbrk);
@@ -774,13 +770,15 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
         case 2: src = b.seg_cend; n = size_t(b.nseg) * 4; break;
         case 3: src = b.seg_sub_base; n = size_t(b.nseg) * 4; break;
         case 4: src = b.seg_nsub; n = size_t(b.nseg) * 4; break;
-        case 5: src = b.exit_spec; n = size_t(b.nsub) * sizeof(SubState); break;
-        case 6: src = b.exit_cnt; n = size_t(b.nsub) * sizeof(SubState); break;
-        case 7: src = b.sub_cnt; n = size_t(b.nsub) * sizeof(SubCount); break;
-        case 8: src = b.sub_entry; n = size_t(b.nsub) * sizeof(SubEntry); break;
+        case 5: src = b.piece_bit; n = size_t(b.nsub) * 4; break;
+        case 6: src = b.piece_end; n = size_t(b.nsub) * 4; break;
+        case 7: src = b.piece_nmcu; n = size_t(b.nsub) * 4; break;
+        case 8: src = b.piece_nent; n = size_t(b.nsub) * 4; break;
         case 9: src = b.sub_seg; n = size_t(b.nsub) * 4; break;
         case 10: src = b.status; n = size_t(b.nimg) * 4; break;
         case 11: src = b.entries; n = ctx->last_entries * 4; break;
+        case 12: src = b.piece_mcu0; n = size_t(b.nsub) * 4; break;
+        case 13: src = b.piece_ent0; n = size_t(b.nsub) * 4; break;
         default: return JD_ERR_INVALID_ARG;
     }
     *nbytes = n;

@@ -312,7 +312,7 @@ class Decoder:
         items, results = batch
         st = self.lib.jd_decode_batch(self.ctx, items, len(items), results, 1, stream)
         if st != JD_OK:
-            raise JDError(st, "jd_decode_batch")
+            raise JDError(st, "jd_decode_batch " + (self.last_error() if st == JD_ERR_HIP else ""))
 
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
@@ -340,9 +340,10 @@ class Decoder:
         self.lib.jd_reset_stats(self.ctx)
 
     DEBUG_ARRAYS = {"blocks": (0, np.uint32, 2), "seg_cstart": (1, np.uint32, 1), "seg_cend": (2, np.uint32, 1),
-                    "seg_sub_base": (3, np.uint32, 1), "seg_nsub": (4, np.uint32, 1), "exit_spec": (5, np.uint32, 2),
-                    "exit_cnt": (6, np.uint32, 2), "sub_cnt": (7, np.int32, 6), "sub_entry": (8, np.int32, 8),
-                    "sub_seg": (9, np.uint32, 1), "status": (10, np.uint32, 1), "entries": (11, np.uint32, 1)}
+                    "seg_sub_base": (3, np.uint32, 1), "seg_nsub": (4, np.uint32, 1), "piece_bit": (5, np.uint32, 1),
+                    "piece_end": (6, np.uint32, 1), "piece_nmcu": (7, np.uint32, 1), "piece_nent": (8, np.uint32, 1),
+                    "sub_seg": (9, np.uint32, 1), "status": (10, np.uint32, 1), "entries": (11, np.uint32, 1),
+                    "piece_mcu0": (12, np.uint32, 1), "piece_ent0": (13, np.uint32, 1)}
 
     def debug_fetch(self, name: str) -> np.ndarray:
         """Internal array of the most recent batch (white-box tests and debugging)."""

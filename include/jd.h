@@ -43,11 +43,10 @@ typedef struct jd_ctx jd_ctx;
 
 /* jd_opts.flags */
 #define JD_FLAG_TIMING 1u /* record hipEvents around every kernel launch (jd_get_stats) */
-/* Entropy-decode path selection (default: images with >= 4 restart intervals are decoded one
- * interval per lane, the others by the self-synchronising subsequence passes).  Results are
- * identical either way; the flags exist so tests can drive each path over every input. */
-#define JD_FLAG_FORCE_SYNC 2u  /* every image through the self-synchronising passes */
-#define JD_FLAG_FORCE_LANES 4u /* every image one lane per interval (whole image if no DRI) */
+/* Entropy-decode piece size (default: 8192-bit pieces).  Results are identical for every
+ * setting; the flags exist so tests can stress the two extremes of the piece-parallel decode. */
+#define JD_FLAG_FORCE_SYNC 2u  /* 1024-bit pieces: many speculative starts, exercises re-scans */
+#define JD_FLAG_FORCE_LANES 4u /* one piece per restart interval (the whole scan if no DRI) */
 
 typedef struct jd_opts {
     unsigned flags;

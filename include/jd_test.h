@@ -22,9 +22,9 @@ jd_status jd_test_color(jd_ctx* ctx, const int32_t* ycc_dev, uint8_t* rgb_dev, i
 
 /* Copies an internal array of the most recent batch to the host (debugging / white-box tests).
  * what: 0 blocks (8 B each), 1 seg_cstart, 2 seg_cend, 3 seg_sub_base, 4 seg_nsub (u32 each),
- *       5 exit_spec, 6 exit_cnt (8 B each), 7 sub_cnt (24 B), 8 sub_entry (32 B), 9 sub_seg (u32),
- *       10 status (u32 per image), 11 entries (u32).  *nbytes receives the array size; at most
- *       cap bytes are copied. */
+ *       5 piece_bit, 6 piece_end, 7 piece_nmcu, 8 piece_nent, 9 sub_seg (u32 per piece slot),
+ *       10 status (u32 per image), 11 entries (u32), 12 piece_mcu0, 13 piece_ent0 (u32 per piece
+ *       slot).  *nbytes receives the array size; at most cap bytes are copied. */
 jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* host_dst, size_t cap, size_t* nbytes);
 
 #ifdef __cplusplus

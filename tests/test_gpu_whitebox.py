@@ -1,9 +1,12 @@
-"""White-box checks of the self-synchronising decode (GPU): intermediate arrays of the last batch
-(jd_debug_fetch) against an independent sequential bit-level trace (tools/jd_trace.py).
+"""White-box checks of the piece-parallel Huffman decode (GPU): intermediate arrays of the last
+batch (jd_debug_fetch) against an independent sequential bit-level trace (tools/jd_trace.py).
+The decoder uses 1024-bit pieces here (path="sync"), so many pieces start speculatively and
+some need the chain's re-scan.
 
-  seg_cstart/seg_cend  -> un-stuffed interval lengths
-  sub_entry            -> true entry state of every subsequence + block / DC prefix sums
-  blocks               -> per-block AC-entry counts and DC values vs the oracle's coefficients
+  seg_cstart/seg_cend          -> un-stuffed interval lengths
+  piece_bit/mcu0/ent0          -> every piece starts on a true MCU boundary, with the right MCU
+                                  index and AC-entry offset
+  blocks                       -> per-block AC-entry counts and DC values vs the oracle
 """
 import os
 import sys
@@ -29,40 +32,49 @@ def _load(name):
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_intervals_and_entry_states(sync_decoder, name):
+def test_intervals_and_piece_starts(sync_decoder, name):
     data = _load(name)
     try:
         sync_decoder.decode(data)
     except Exception:
         pass  # inspect the intermediate state even when the decode reports an error
-    tr = jd_trace.trace(data, jd_trace.SUB_BITS)
+    truth = jd_trace.mcu_starts(data)
     cs = sync_decoder.debug_fetch("seg_cstart")
     ce = sync_decoder.debug_fetch("seg_cend")
     ssb = sync_decoder.debug_fetch("seg_sub_base")
     nsub = sync_decoder.debug_fetch("seg_nsub")
-    ent = sync_decoder.debug_fetch("sub_entry")
+    pbit = sync_decoder.debug_fetch("piece_bit")
+    pm0 = sync_decoder.debug_fetch("piece_mcu0")
+    pnm = sync_decoder.debug_fetch("piece_nmcu")
+    pe0 = sync_decoder.debug_fetch("piece_ent0")
+    ent0 = 0
     errs = []
-    for s, seg in enumerate(tr):
+    for s, seg in enumerate(truth):
         if (int(ce[s]) - int(cs[s])) * 8 != seg["bits"]:
             errs.append(f"seg {s}: bits gpu {(int(ce[s]) - int(cs[s])) * 8} want {seg['bits']}")
             continue
-        if int(nsub[s]) != seg["nsub"]:
-            errs.append(f"seg {s}: nsub gpu {nsub[s]} want {seg['nsub']}")
+        want_n = max(1, -(-seg["bits"] // 1024))
+        if int(nsub[s]) != want_n:
+            errs.append(f"seg {s}: pieces gpu {nsub[s]} want {want_n}")
             continue
-        blk = 0
-        dc = [0, 0, 0]
-        for j in range(seg["nsub"]):
-            e = ent[int(ssb[s]) + j]
-            p, sk = int(e[0]) & 0xFFFFFFFF, int(e[1]) & 0xFFFFFFFF
-            got = (p, sk >> 16, (sk >> 8) & 0xFF, sk & 0xFF)
-            want = seg["entry"][j]
-            if got != tuple(want):
-                errs.append(f"seg {s} sub {j}: entry gpu {got} want {want}")
-            if int(e[2]) != blk or [int(x) for x in e[4:7]] != dc:
-                errs.append(f"seg {s} sub {j}: blk/pred gpu {int(e[2])} {list(e[4:7])} want {blk} {dc}")
-            c = seg["counts"][j]
-            blk += c[0]
-            dc = [dc[0] + c[2], dc[1] + c[3], dc[2] + c[4]]
+        starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
+        nm = 0
+        for j in range(want_n):
+            u = int(ssb[s]) + j
+            b = int(pbit[u])
+            if b not in starts:
+                errs.append(f"seg {s} piece {j}: bit {b} is not an MCU boundary")
+                continue
+            m, e = starts[b]
+            if int(pm0[u]) != m and not (j == want_n - 1 and int(pnm[u]) == 0):
+                errs.append(f"seg {s} piece {j}: mcu0 gpu {pm0[u]} want {m}")
+            if j == 0:
+                ent0 = int(pe0[u])
+            elif int(pe0[u]) - ent0 != e and int(pnm[u]) > 0:
+                errs.append(f"seg {s} piece {j}: ent0 gpu {int(pe0[u]) - ent0} want {e}")
+            nm += int(pnm[u])
+        if nm != len(seg["starts"]) - 1:
+            errs.append(f"seg {s}: MCUs gpu {nm} want {len(seg['starts']) - 1}")
         if len(errs) > 20:
             break
     assert not errs, "\n".join(errs[:20])
@@ -84,7 +96,7 @@ def test_block_coefficients(sync_decoder, name):
     bad = []
     for i in range(nb):
         start, cd = int(blocks[i, 0]), int(blocks[i, 1])
-        cnt, dc = cd >> 16, _s16(cd & 0xFFFF)
+        cnt, dc = cd >> 26, ((cd & 0x3FFFFFF) ^ 0x2000000) - 0x2000000  # 6-bit count, 26-bit DC
         got = np.zeros(64, np.int32)
         got[0] = dc
         for e in entries[start:start + cnt]:

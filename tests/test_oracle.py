@@ -191,13 +191,14 @@ def test_restart_interval_invariance(ss):
         assert st == 0 and np.array_equal(rgb, base), kw
 
 
-def test_self_sync_emulation_matches_oracle(golden):
-    """The GPU's four-pass self-synchronising decode (spec -> count -> chain -> write), restated
-    in Python (tools/jd_trace.emulate), reproduces the oracle's coefficients exactly."""
-    for e in golden[:30]:
-        if e["status"] != 0:
-            continue
-        blocks, _ = jd_trace.emulate(e["data"])
+def test_piece_decode_emulation_matches_oracle(golden):
+    """The GPU's piece-parallel decode (speculative scan with overlap -> chain verify/re-scan ->
+    write), restated in Python (tools/jd_trace.emulate), reproduces the oracle's coefficients.
+    Small pieces force many speculative starts that do not synchronise (re-scans)."""
+    rescans = 0
+    for e in [e for e in golden if e["status"] == 0][:8]:
+        blocks, r = jd_trace.emulate(e["data"], 1024, 512)
+        rescans += r
         st, coef = jdoracle.decode_coefs(e["data"])
         assert len(blocks) == coef.shape[0], e["file"]
         for i, (dc, ents) in enumerate(blocks):
@@ -206,6 +207,7 @@ def test_self_sync_emulation_matches_oracle(golden):
             for z, v in ents:
                 got[z] = v
             assert np.array_equal(got, coef[i]), (e["file"], i)
+    assert rescans > 0  # the verification/re-scan path was exercised
 
 
 def test_corrupt_and_unsupported_statuses():

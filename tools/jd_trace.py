@@ -196,111 +196,151 @@ def _layout(t: Tables):
     return pattern, mcux * mcuy
 
 
-def _decode_range(t, pattern, val, total, p, bi, k, ncur, end, mode, nblk=0, blk=0, ent=0, pred=None,
-                  entries=None, blocks=None):
-    """The GPU decode_run (jd_kernels.hip) restated: decode symbols that start before `end`.
-    mode 0/1: exit (+ counts); mode 2: also writes entries[ent..] and blocks[blk] = (start, cnt, dc)."""
-    bpm = len(pattern)
+def _symbol(t, pattern, val, total, p, bi, k):
+    """Decodes the symbol at bit p in state (bi, k): (code+magnitude bits, symbol, value) or None."""
     comp = pattern[bi]
-    nblocks = nent = 0
-    dcs = [0, 0, 0]
-    pred = list(pred or [0, 0, 0])
-    cur_blk = blk - 1
-    ent_blk = ent - ncur
-    dc = pred[comp]
+    tab = t.dht[(0, t.td[comp])] if k == 0 else t.dht[(1, t.ta[comp])]
 
     def peek(q, n):
         if n == 0:
             return 0
         return (val >> (total - q - n)) & ((1 << n) - 1) if q + n <= total else 0
 
-    while p < end:
-        if mode == 2 and k == 0 and blk >= nblk:
-            break
-        tab = t.dht[(0, t.td[comp])] if k == 0 else t.dht[(1, t.ta[comp])]
-        sym, ln = 0, 16
-        for L in range(1, 17):
-            if (L, peek(p, L)) in tab:
-                sym, ln = tab[(L, peek(p, L))], L
-                break
-        s = min(sym if k == 0 else sym & 15, 16)
-        v = peek(p + ln, s)
-        if s and v < (1 << (s - 1)):
-            v -= (1 << s) - 1
-        p += ln + s
-        if k == 0:
-            nblocks += 1
-            dcs[comp] += v
-            if mode == 2:
-                pred[comp] += v
-                dc = pred[comp]
-                cur_blk = blk
-                blk += 1
-                ent_blk = ent
-            k, ncur = 1, 0
-        elif sym == 0:
-            k = 64
-        else:
-            k += sym >> 4
-            if k < 64:
-                if sym & 15:
-                    ncur += 1
-                    nent += 1
-                    if mode == 2:
-                        entries[ent] = (k, v)
-                        ent += 1
-                k += 1
-        if k >= 64:
-            if mode == 2:
-                blocks[cur_blk] = (ent_blk, ent - ent_blk, dc)
-            bi = 0 if bi + 1 == bpm else bi + 1
-            comp = pattern[bi]
-            k = 0
-    return (p, bi, k, ncur), (nblocks, nent, dcs), blk
+    for ln in range(1, 17):
+        if (ln, peek(p, ln)) in tab:
+            sym = tab[(ln, peek(p, ln))]
+            s = sym if k == 0 else sym & 15
+            v = peek(p + ln, s)
+            if s and v < (1 << (s - 1)):
+                v -= (1 << s) - 1
+            return ln + s, sym, v
+    return None
 
 
-def emulate(d: bytes, sub_bits: int = SUB_BITS):
-    """Runs spec -> count -> chain -> write exactly as the GPU does; returns per-block
-    (dc, [(zz, value)...]) in scan order and the number of chain re-decodes."""
+def _step(k, sym):
+    """(next k, block finished, coefficient index emitted or None) — parser.cpp:114-134."""
+    if k == 0:
+        return 1, False, None
+    if sym == 0:
+        return 0, True, None
+    knew = k + (sym >> 4)
+    emit = knew if (sym & 15) and knew < 64 else None
+    kn = knew + 1 if knew < 64 else knew
+    return (0, True, emit) if kn >= 64 else (kn, False, emit)
+
+
+def mcu_starts(d: bytes):
+    """Per interval: [(bit, AC entries before)] of every MCU start (ground truth for the pieces)."""
     t = parse(d)
     pattern, nmcu = _layout(t)
-    bpm = len(pattern)
     ri = t.ri or nmcu
-    result = []
-    redecodes = 0
+    out = []
     for si, data in enumerate(segments(d, t.ecs)):
         m0 = si * ri
         if m0 >= nmcu:
             break
-        nblk = (min(m0 + ri, nmcu) - m0) * bpm
+        n = min(m0 + ri, nmcu) - m0
+        val = int.from_bytes(data + b"\xff" * 16, "big")
+        total = (len(data) + 16) * 8
+        p, bi, k, ents, starts = 0, 0, 0, 0, [(0, 0)]
+        while len(starts) <= n:
+            L, sym, _ = _symbol(t, pattern, val, total, p, bi, k)
+            p += L
+            k, fin, emit = _step(k, sym)
+            ents += emit is not None
+            if fin:
+                bi = (bi + 1) % len(pattern)
+                if bi == 0:
+                    starts.append((p, ents))
+        out.append({"bits": len(data) * 8, "starts": starts[:n + 1]})
+    return out
+
+
+def _walk_scan(t, pattern, val, total, bits, start, warm_to, stop_at):
+    """The GPU's walk<kWalkScan> (jd_kernels.hip) restated: (m_start, m_end, mcus, entries)."""
+    p, bi, k = start, 0, 0
+    counting = warm_to == start
+    m_start = start if counting else None
+    mcus = ents = 0
+    if counting and start + 8 > bits:  # starts at the data end: an empty piece
+        return start, start, 0, 0
+    while True:
+        r = _symbol(t, pattern, val, total, p, bi, k)
+        L, sym, _ = r if r else (16, 0, 0)
+        p += L
+        k, fin, emit = _step(k, sym) if r else (k, False, None)
+        if counting and emit is not None:
+            ents += 1
+        mcu_end = fin and (bi + 1) % len(pattern) == 0
+        if fin:
+            bi = (bi + 1) % len(pattern)
+        if not counting and mcu_end and p >= warm_to:
+            counting, m_start = True, p
+            if p + 8 > bits:
+                return m_start, p, 0, 0
+        elif counting and mcu_end:
+            mcus += 1
+            if p >= stop_at or p + 8 > bits:
+                return m_start, p, mcus, ents
+        if p > bits or (counting and r is None):
+            return m_start, p, mcus, ents
+
+
+def emulate(d: bytes, piece_bits: int = 8192, overlap: int = 4096):
+    """Runs scan -> chain -> write as the GPU does; returns per-block (dc, [(zz, value)...]) in
+    scan order (DC already predicted) and the number of chain re-scans."""
+    t = parse(d)
+    pattern, nmcu = _layout(t)
+    bpm = len(pattern)
+    ri = t.ri or nmcu
+    result, rescans = [], 0
+    for si, data in enumerate(segments(d, t.ecs)):
+        m0 = si * ri
+        if m0 >= nmcu:
+            break
+        nm = min(m0 + ri, nmcu) - m0
         bits = len(data) * 8
         val = int.from_bytes(data + b"\xff" * 16, "big")
         total = (len(data) + 16) * 8
-        n = max(1, -(-bits // sub_bits))
-
-        def end(j):
-            return bits if j == n - 1 else (j + 1) * sub_bits
-
-        spec = [_decode_range(t, pattern, val, total, j * sub_bits, 0, 0, 0, end(j), 0)[0] for j in range(n)]
-        used = [(0, 0, 0, 0)] + spec[:-1]
-        cnt = [_decode_range(t, pattern, val, total, *used[j], end(j), 1)[:2] for j in range(n)]
-        true_entry = [(0, 0, 0, 0)]
-        for j in range(1, n):  # chain: verify, re-decode broken links
-            te = cnt[j - 1][0]
-            true_entry.append(te)
-            if te != used[j]:
-                redecodes += 1
-                cnt[j] = _decode_range(t, pattern, val, total, *te, end(j), 1)[:2]
-        entries, blocks = {}, {}
-        blk, ent, pred = 0, 0, [0, 0, 0]
-        for j in range(n):  # write pass from verified entries + prefix sums
-            _decode_range(t, pattern, val, total, *true_entry[j], bits + 64 if j == n - 1 else end(j), 2, nblk,
-                          blk, ent, pred, entries, blocks)
-            c = cnt[j][1]
-            blk += c[0]
-            ent += c[1]
-            pred = [pred[q] + c[2][q] for q in range(3)]
-        for b in range(nblk):
-            st, n_e, dc = blocks.get(b, (0, 0, None))
-            result.append((dc, [entries.get(st + i) for i in range(n_e)]))
-    return result, redecodes
+        n = max(1, -(-bits // piece_bits))
+        big = 1 << 40
+        pcs = []
+        for j in range(n):  # scan
+            pstart = j * piece_bits
+            warm_to = 0 if j == 0 else min(pstart, bits)
+            start = 0 if pstart <= overlap else min(pstart - overlap, warm_to)
+            stop_at = big if j == n - 1 else pstart + piece_bits
+            ms, me, mc, en = _walk_scan(t, pattern, val, total, bits, start, warm_to, stop_at)
+            pcs.append([0 if j == 0 else ms, me, mc, en])
+        for j in range(1, n):  # chain: verify, re-scan from the verified boundary
+            if pcs[j][0] != pcs[j - 1][1]:
+                rescans += 1
+                st = pcs[j - 1][1]
+                stop_at = big if j == n - 1 else (j + 1) * piece_bits
+                ms, me, mc, en = _walk_scan(t, pattern, val, total, bits, st, st, stop_at)
+                pcs[j] = [st, me, mc, en]
+        blocks = []
+        pred = [0, 0, 0]
+        mcu_run = 0
+        for j in range(n):  # write
+            cnt = pcs[j][2] if j < n - 1 else nm - mcu_run
+            mcu_run += cnt
+            p, bi, k = pcs[j][0], 0, 0
+            ents = []
+            for _ in range(cnt * bpm):
+                while True:
+                    L, sym, v = _symbol(t, pattern, val, total, p, bi, k)
+                    p += L
+                    if k == 0:
+                        c = pattern[bi]
+                        pred[c] += v
+                        dc, ents = pred[c], []
+                    k, fin, emit = _step(k, sym)
+                    if emit is not None:
+                        ents.append((emit, v))
+                    if fin:
+                        bi = (bi + 1) % bpm
+                        blocks.append((dc, ents))
+                        break
+        result.extend(blocks)
+    return result, rescans
