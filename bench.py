@@ -34,6 +34,19 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def measured_traffic(config: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC profile of this config
+    (profiles/<round>_traffic.json, written by tools/profile_summary.py), or None."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        with open(f) as fh:
+            t = json.load(fh)
+        if t.get("config") == config and kernel in t.get("kernels", {}):
+            return t["kernels"][kernel]["hbm_bytes"], os.path.relpath(f, ROOT)
+    return None
+
+
 def rank_seed(rank: int, batch: int) -> int:
     """First synthetic-image seed of a rank: ranks decode disjoint images (weak scaling)."""
     return rank * batch
@@ -180,6 +193,7 @@ def main():
     if rank == 0:
         kern = st["kernels"]
         dom = max(kern, key=lambda k: kern[k]["total_ms"])
+        traffic = measured_traffic(args.config, dom)
         kd = kern[dom]
         avg_ms = kd["total_ms"] / max(1, kd["launches"])
         per_launch_bytes = kd["bytes"] / max(1, kd["launches"])
@@ -208,7 +222,9 @@ def main():
             "jpeg_MB_per_s": tot_bytes / t_max / 1e6,
             "ecs_MB_per_s": tot_ecs / t_max / 1e6,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic[0] if traffic else None,
+                         "traffic_source": traffic[1] if traffic else None,
                          "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
             "kernels_ms_per_step": {k: v["total_ms"] / max(1, v["launches"]) for k, v in kern.items()},
             "path_roofline_frac": ((ecs + 3 * pixels) / (t_max / args.steps) / 1e9) / HBM_PEAK_GBS,

@@ -1295,44 +1295,45 @@ __global__ void k_test_color(const int32_t* ycc, uint8_t* rgb, int n) {
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-hipError_t launch_scan(const BatchDev& b, hipStream_t s) {
-    if (!b.nimg || !b.max_chunks) return hipSuccess;
-    hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
-    return hipGetLastError();
-}
-
-hipError_t launch_index(const BatchDev& b, hipStream_t s) {
-    if (!b.nimg) return hipSuccess;
-    hipLaunchKernelGGL(k_index, dim3(b.nimg), dim3(64), 0, s, b);
-    return hipGetLastError();
-}
-
-hipError_t launch_compact(const BatchDev& b, hipStream_t s) {
-    if (!b.nimg || !b.max_chunks) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
-    return hipGetLastError();
-}
-
 size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots); }
 
-hipError_t launch_huffman(const BatchDev& b, hipStream_t s) {
-    if (!b.nimg || !b.nsub) return hipSuccess;
+hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
+    if (!b.nimg) return hipSuccess;
     const size_t lds = piece_lds_bytes(b.max_slots);
-    // every slot not claimed by an interval (per-image slack, workgroup padding) must read invalid
-    hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_subplan, dim3(b.nimg), dim3(64), 0, s, b);
-    hipLaunchKernelGGL(k_piece<kWalkScan>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
-    hipLaunchKernelGGL(k_rescan, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
-    hipLaunchKernelGGL(k_chain, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
-    hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
-    hipLaunchKernelGGL(k_dpcm, dim3(b.nseg), dim3(64), 0, s, b);
-    return hipGetLastError();
-}
-
-hipError_t launch_idct_color(const BatchDev& b, hipStream_t s) {
-    if (!b.nimg || !b.max_tiles) return hipSuccess;
-    hipLaunchKernelGGL(k_idct_color, dim3(b.max_tiles, b.nimg), dim3(kIdctThreads), 0, s, b);
+    switch (k) {
+        case 0:
+            if (b.max_chunks) hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
+            break;
+        case 1: hipLaunchKernelGGL(k_index, dim3(b.nimg), dim3(64), 0, s, b); break;
+        case 2:
+            if (b.max_chunks) hipLaunchKernelGGL(k_compact, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
+            break;
+        case 3: {
+            if (!b.nsub) break;
+            // every slot not claimed by an interval (per-image slack, padding) must read invalid
+            const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_subplan, dim3(b.nimg), dim3(64), 0, s, b);
+            break;
+        }
+        case 4:
+            if (b.nsub) hipLaunchKernelGGL(k_piece<kWalkScan>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            break;
+        case 5:
+            if (b.nsub) hipLaunchKernelGGL(k_rescan, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            break;
+        case 6:
+            if (b.nchain) hipLaunchKernelGGL(k_chain, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            break;
+        case 7:
+            if (b.nsub) hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            break;
+        case 8: hipLaunchKernelGGL(k_dpcm, dim3(b.nseg), dim3(64), 0, s, b); break;
+        case 9:
+            if (b.max_tiles) hipLaunchKernelGGL(k_idct_color, dim3(b.max_tiles, b.nimg), dim3(kIdctThreads), 0, s, b);
+            break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -504,11 +504,9 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         ctx->last_blocks = P.total_blocks;
         ctx->last_entries = P.total_entry_cap;
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
-        hipError_t (*launch[JD_NUM_KERNELS])(const BatchDev&, hipStream_t) = {
-            launch_scan, launch_index, launch_compact, launch_huffman, launch_idct_color};
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
             if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][0], s));
-            HIPCHK(ctx, launch[k](b, s));
+            HIPCHK(ctx, launch_kernel(k, b, s));
             if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][1], s));
         }
         std::vector<uint32_t> status(nimg);
@@ -524,12 +522,19 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         const double entries = double(ctr[0]);
         const double blocks = double(P.total_blocks);
         const double ecs = P.ecs_bytes;
+        const double nsubd = double(nsub), nsegd = double(nseg);
+        const double overlap_factor = (double(P.piece_bits) + kPieceOverlap) / double(P.piece_bits);
         const double bytes[JD_NUM_KERNELS] = {
-            ecs,                                               // scan: read the ECS once
-            double(P.total_chunks) * 12 + double(nseg) * 8,    // index: per-chunk counters, boundaries
-            2 * ecs,                                           // compact: read + write the ECS
-            ecs + blocks * 8 + entries * 4,                    // huffman: ECS in, sparse coefficients out
-            blocks * 8 + entries * 4 + P.pixels * 3};          // idct_color: coefficients in, RGB out
+            ecs,                                               // k_scan: read the ECS once
+            double(P.total_chunks) * 12 + nsegd * 8,           // k_index: per-chunk counters, boundaries
+            2 * ecs,                                           // k_compact: read + write the ECS
+            nsubd * 4 + nsegd * 16,                            // k_subplan: piece map
+            ecs * std::min(overlap_factor, 2.0) + nsubd * 16,  // k_piece_scan: bits incl. overlap, counts out
+            nsubd * 8,                                         // k_rescan: start/end check per piece
+            nsubd * 28,                                        // k_chain: counts in, offsets out
+            ecs + blocks * 8 + entries * 4,                    // k_piece_write: ECS in, sparse coefficients out
+            blocks * 16,                                       // k_dpcm: BlockInfo read + write
+            blocks * 8 + entries * 4 + P.pixels * 3};          // k_idct_color: coefficients in, RGB out
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
             S.launches[k]++;
             S.bytes[k] += bytes[k];
@@ -589,7 +594,8 @@ const char* jd_status_str(jd_status st) {
 const char* jd_ctx_last_error(jd_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
 
 const char* jd_kernel_name(int k) {
-    static const char* names[JD_NUM_KERNELS] = {"k_scan", "k_index", "k_compact", "k_huffman", "k_idct_color"};
+    static const char* names[JD_NUM_KERNELS] = {"k_scan",      "k_index", "k_compact",     "k_subplan", "k_piece_scan",
+                                                "k_rescan",    "k_chain", "k_piece_write", "k_dpcm",    "k_idct_color"};
     return (k >= 0 && k < JD_NUM_KERNELS) ? names[k] : "?";
 }
 

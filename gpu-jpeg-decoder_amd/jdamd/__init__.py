@@ -31,8 +31,9 @@ JD_FLAG_TIMING = 1
 JD_FLAG_FORCE_SYNC = 2
 JD_FLAG_FORCE_LANES = 4
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES}
-JD_NUM_KERNELS = 5
-KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_huffman", "k_idct_color"]
+JD_NUM_KERNELS = 10
+KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece_scan", "k_rescan", "k_chain",
+                "k_piece_write", "k_dpcm", "k_idct_color"]
 
 
 class JDError(RuntimeError):

@@ -132,7 +132,7 @@ jd_status jd_synchronize(jd_ctx* ctx);
 
 /* Per-kernel timing (JD_FLAG_TIMING).
  * Kernels: 0 k_scan, 1 k_index, 2 k_compact, 3 k_huffman, 4 k_idct_color. */
-#define JD_NUM_KERNELS 5
+#define JD_NUM_KERNELS 10
 typedef struct jd_stats {
     int launches[JD_NUM_KERNELS];
     double total_ms[JD_NUM_KERNELS]; /* hipEvent time, summed over launches                     */

@@ -1,0 +1,54 @@
+"""Reduces a tools/profile_round.sh run to the committed profile artifacts.
+
+    python tools/profile_summary.py r01 gpurun_out/r01 [--config c2]
+
+profiles/<tag>_kernel_stats.csv : rocprofv3 --kernel-trace --stats summary of the bench command
+profiles/<tag>_traffic.json     : per kernel, HBM bytes per launch from the PMC passes, corrected as
+                                  /opt/skills/guides/MI355X_MICROARCH.md (HBM section) prescribes:
+                                  FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts
+                                  half of a wide (16 B/lane) streaming read, so reads are doubled.
+bench.py reads the traffic file for roofline.traffic (same config only).
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+
+ap = argparse.ArgumentParser()
+ap.add_argument("tag")
+ap.add_argument("run_dir")
+ap.add_argument("--config", default="c2")
+a = ap.parse_args()
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+prof = os.path.join(root, "profiles")
+os.makedirs(prof, exist_ok=True)
+
+stats = glob.glob(os.path.join(a.run_dir, "stats", "**", "*kernel_stats.csv"), recursive=True)
+if stats:
+    shutil.copy(stats[0], os.path.join(prof, f"{a.tag}_kernel_stats.csv"))
+
+
+def per_launch(pass_dir, counter):
+    vals = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(a.run_dir, pass_dir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                vals[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)  # KiB -> bytes
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+fetch, write = per_launch("fetch", "FETCH_SIZE"), per_launch("write", "WRITE_SIZE")
+out = {"config": a.config, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
+       "bytes = 2 * FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE halves 16 B/lane streaming reads)",
+       "kernels": {}}
+for k in sorted(set(fetch) | set(write)):
+    name = k.split("(")[0].replace("void ", "").replace("jd::", "")
+    name = {"k_piece<0>": "k_piece_scan", "k_piece<1>": "k_piece_write"}.get(name, name)
+    f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+    out["kernels"][name] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes": 2 * f + w}
+with open(os.path.join(prof, f"{a.tag}_traffic.json"), "w") as fh:
+    json.dump(out, fh, indent=1)
+print(json.dumps(out["kernels"], indent=1))
