@@ -642,6 +642,114 @@ __device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const 
     }
 }
 
+// The scan walk on its own: per symbol only the table lookup, the bit buffer and the block state
+// machine; everything else happens at MCU boundaries (a branch taken by ~half the wave-steps) or
+// once per window round.  Entry counts are differences of a running count, the error flag is
+// one OR of the entry's error bit, and running past the data is checked per round (the scan
+// stores nothing, so decoding a little garbage past the end is harmless).
+__device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
+                                          uint32_t* row, bool active_in, Walk& W) {
+    const uintptr_t a_start = S.data + (W.start >> 3);
+    uintptr_t wa = a_start & ~uintptr_t(15);
+#pragma unroll
+    for (int q = 0; q < kWinLoads; q++) {
+        const u32x4 v = load16(wa + 16 * q, S.last);
+        row[4 * q + 0] = __builtin_bswap32(v.x);
+        row[4 * q + 1] = __builtin_bswap32(v.y);
+        row[4 * q + 2] = __builtin_bswap32(v.z);
+        row[4 * q + 3] = __builtin_bswap32(v.w);
+    }
+    const uint32_t off = uint32_t(a_start & 15) * 8 + (W.start & 7u);
+    int rp = int(off >> 5);
+    uint64_t bb = ((uint64_t(row[rp]) << 32) | row[rp + 1]) << (off & 31);
+    int nb = 64 - int(off & 31);
+    rp += 2;
+    uint32_t nextw = row[rp];
+    uint32_t consumed = W.start;
+    const uint32_t sbits = S.bits;
+    const int bpm = int(S.bpm);
+    int k = 0, bi = 0;
+    uint32_t actab = (acp & 7u) * uint32_t(kLutWords);
+    uint32_t tab = (dcp & 7u) * uint32_t(kLutWords);
+    uint32_t counting = (W.warm_to == W.start) ? 1u : 0u;
+    uint32_t mcus = 0, ents = 0, ents0 = 0, m_start = counting ? W.start : kNoPiece, m_end = W.start;
+    uint32_t errs = 0;  // bit 16: a bad code since counting began
+    bool active = active_in;
+    if (counting && W.start + 8 > sbits) active = false;  // starts at the data end: empty
+    while (true) {
+        const uintptr_t na = wa + kWinAdv;
+        u32x4 nx[kWinLoads];
+#pragma unroll
+        for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
+        while (active && rp <= kWinAdv / 4) {
+            const uint32_t peek = uint32_t(bb >> 32);
+            uint32_t e = s_lutw[tab + (peek >> (32 - kLutBits))];
+            if ((e & 31u) == 0) e = huff_slow(s_lutw + tab, peek, k == 0);  // 0.3 % of symbols
+            errs |= e;
+            const uint32_t L = e & 31u;
+            bb <<= L;
+            nb -= int(L);
+            const bool need = nb < 32;
+            bb |= need ? (uint64_t(nextw) << (32 - nb)) : 0ull;
+            nb += need ? 32 : 0;
+            rp += need ? 1 : 0;
+            nextw = row[rp];
+            consumed += L;
+            // EOB / ZRL / run-size (parser.cpp:114-134); DC entries have run 0, no EOB/emit bits
+            const int knew = k + int(__builtin_amdgcn_ubfe(e, 5u, 4u));
+            const bool fin = k != 0 && ((e & 512u) != 0 || knew >= 63);
+            ents += ((e & 1024u) != 0 && knew < 64) ? 1u : 0u;
+            const int nbi = (bi + 1 == bpm) ? 0 : bi + 1;
+            bi = fin ? nbi : bi;
+            actab = fin ? __builtin_amdgcn_ubfe(acp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
+            tab = fin ? __builtin_amdgcn_ubfe(dcp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
+            k = fin ? 0 : knew + 1;
+            if (fin && nbi == 0) {  // an MCU ends here
+                const bool at_end = consumed + 8 > sbits;
+                if (!counting) {
+                    if (consumed >= W.warm_to) {  // synchronised: the piece starts here
+                        counting = 1u;
+                        m_start = consumed;
+                        ents0 = ents;
+                        errs = 0;
+                        if (at_end) {
+                            m_end = consumed;
+                            active = false;
+                        }
+                    }
+                } else {
+                    mcus++;
+                    if (consumed >= W.stop_at || at_end) {  // the piece ends here
+                        m_end = consumed;
+                        active = false;
+                    }
+                }
+            }
+        }
+        if (active && consumed > sbits) {  // past the data
+            m_end = consumed;
+            if (counting) errs |= 1u << 16;
+            active = false;
+        }
+        if (__ballot(active) == 0) break;  // wave-uniform
+#pragma unroll
+        for (int q = 0; q < kWinLoads; q++) {
+            row[4 * q + 0] = __builtin_bswap32(nx[q].x);
+            row[4 * q + 1] = __builtin_bswap32(nx[q].y);
+            row[4 * q + 2] = __builtin_bswap32(nx[q].z);
+            row[4 * q + 3] = __builtin_bswap32(nx[q].w);
+        }
+        rp -= kWinAdv / 4;
+        wa = na;
+    }
+    W.end = consumed;
+    W.bad = counting && ((errs >> 16) & 1u);
+    W.m_start = m_start;
+    W.m_end = m_end;
+    W.mcus = mcus;
+    W.ents = ents - ents0;
+}
+
 __device__ __forceinline__ void table_slots(const TableSet& ts, const SegInfo& S, uint32_t& dcp, uint32_t& acp) {
     dcp = acp = 0;  // 3-bit table slot per MCU block
     for (uint32_t q = 0; q < S.bpm && q < 10; q++) {
@@ -705,7 +813,10 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
             W.nmcu = 0;
         }
     }
-    walk<MODE>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
+    if (MODE == kWalkScan)
+        walk_scan(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
+    else
+        walk<kWalkWrite>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
     if (!valid) return;
     if (MODE == kWalkScan) {
         // piece 0 starts at bit 0 whatever its walk found (it is the true state)
@@ -762,7 +873,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_rescan(BatchDev b) {
     W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
     W.nmcu = W.ent0 = 0;
     W.blk0 = 0;
-    walk<kWalkScan>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, need, W);
+    walk_scan(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, need, W);
     if (!need) return;
     b.piece_bit[u] = W.start;
     b.piece_end[u] = W.m_end;
@@ -821,8 +932,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain(BatchDev b) {
             W.stop_at = (j + 1 == n) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
             W.nmcu = W.ent0 = 0;
             W.blk0 = 0;
-            walk<kWalkScan>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
-                            true, W);
+            walk_scan(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, true, W);
             pbit = expect;
             pend = W.m_end;
             pm = W.mcus;
