@@ -397,6 +397,10 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
     S.bpm = im.bpm;
 }
 
+// AC-entry slots of an interval: 63 per block (a block stores at most 63) plus 3 per MCU for
+// aligning every piece's first entry to a 16-byte quad (at most one pad per non-empty piece).
+__device__ __forceinline__ uint32_t seg_entry_cap(const SegInfo& S) { return 63u * S.nblk + 3u * (S.nblk / S.bpm); }
+
 __device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
     S.data = S.last = uintptr_t(b.imgs) & ~uintptr_t(15);
     S.bits = 0;
@@ -494,7 +498,6 @@ __device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const 
     uint32_t nextw = row[rp];
     int consumed = int(W.start);  // interval bit of the next symbol
     const int sbits = int(S.bits);
-    const uint32_t ent_end = S.ent0 + 63u * S.nblk;
     BlockInfo* const bout = b.blocks + (W.blk0 - 1);  // bout[blk] after blk++ = this block
     uint32_t* const eout = b.entries;
     const int bpm = int(S.bpm);
@@ -516,8 +519,8 @@ __device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const 
     int dcd = 0;
     // AC entries are write-combined into the aligned quad [ent & ~3, +4): one 16-byte store per
     // four entries (a wave's 64 lanes store to 64 unrelated places, so store instructions, not
-    // bytes, are what the write pass is bound by).  The piece's first and last quads may be
-    // shared with neighbouring pieces: their entries are stored one by one.
+    // bytes, are what the write pass is bound by).  Pieces start on a quad (k_chain aligns
+    // them); the last, partial quad is stored dword by dword.
     uint32_t wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;
     uint32_t bad = 0;
     bool active = active_in && (MODE == kWalkScan || nblk > 0);
@@ -532,24 +535,13 @@ __device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const 
         dcd = q_dc ? val_ : dcd;                                                                               \
         ent_blk = q_dc ? ent : ent_blk;                                                                        \
         blk += q_dc ? 1u : 0u;                                                                                 \
-        const bool st_ = q_emit && ent < ent_end;                                                              \
         const uint32_t ev_ = (uint32_t(val_) << 16) | q_k, sl_ = ent & 3u;                                     \
-        wq0 = (st_ && sl_ == 0u) ? ev_ : wq0;                                                                  \
-        wq1 = (st_ && sl_ == 1u) ? ev_ : wq1;                                                                  \
-        wq2 = (st_ && sl_ == 2u) ? ev_ : wq2;                                                                  \
-        wq3 = (st_ && sl_ == 3u) ? ev_ : wq3;                                                                  \
-        if (st_ && sl_ == 3u) {                                                                                \
-            const uint32_t qb_ = ent - 3u;                                                                     \
-            if (qb_ >= W.ent0) {                                                                               \
-                *reinterpret_cast<uint4*>(eout + qb_) = make_uint4(wq0, wq1, wq2, wq3);                        \
-            } else {                                                                                           \
-                if (qb_ + 1u >= W.ent0) eout[qb_ + 1u] = wq1;                                                  \
-                if (qb_ + 2u >= W.ent0) eout[qb_ + 2u] = wq2;                                                  \
-                eout[qb_ + 3u] = wq3;                                                                          \
-            }                                                                                                  \
-        }                                                                                                      \
-        bad |= (q_emit && !st_) ? 1u : 0u;                                                                     \
-        ent += st_ ? 1u : 0u;                                                                                  \
+        wq0 = (q_emit && sl_ == 0u) ? ev_ : wq0;                                                               \
+        wq1 = (q_emit && sl_ == 1u) ? ev_ : wq1;                                                               \
+        wq2 = (q_emit && sl_ == 2u) ? ev_ : wq2;                                                               \
+        wq3 = (q_emit && sl_ == 3u) ? ev_ : wq3;                                                               \
+        if (q_emit && sl_ == 3u) *reinterpret_cast<uint4*>(eout + ent - 3u) = make_uint4(wq0, wq1, wq2, wq3);  \
+        ent += q_emit ? 1u : 0u;                                                                               \
         if (qf & kQFin) bout[blk] = BlockInfo{ent_blk, pack_cnt_dc(ent - ent_blk, dcd)};                       \
     } while (0)
     while (true) {
@@ -625,9 +617,9 @@ __device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const 
 #undef JD_WALK_BOOK
     if (MODE == kWalkWrite && (ent & 3u)) {  // the last, partial quad
         const uint32_t qb = ent & ~3u;
-        if (qb >= W.ent0) eout[qb] = wq0;
-        if (ent > qb + 1u && qb + 1u >= W.ent0) eout[qb + 1u] = wq1;
-        if (ent > qb + 2u && qb + 2u >= W.ent0) eout[qb + 2u] = wq2;
+        eout[qb] = wq0;
+        if (ent > qb + 1u) eout[qb + 1u] = wq1;
+        if (ent > qb + 2u) eout[qb + 2u] = wq2;
     }
     W.end = uint32_t(consumed);
     W.bad = bad != 0;
@@ -803,7 +795,8 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
             W.nmcu = b.piece_nmcu[u];
             W.ent0 = b.piece_ent0[u];
             // never write outside the interval (the chain flagged inconsistent counts as corrupt)
-            if (W.start == kNoPiece || W.start > S.bits || m0 + W.nmcu > nmcu_seg || W.ent0 > S.ent0 + 63u * S.nblk)
+            if (W.start == kNoPiece || W.start > S.bits || m0 + W.nmcu > nmcu_seg || (W.ent0 & 3u) ||
+                uint64_t(W.ent0) + 63ull * W.nmcu * S.bpm > uint64_t(S.ent0) + seg_entry_cap(S))
                 valid = false;
             W.blk0 = S.blk0 + uint64_t(m0) * S.bpm;
         }
@@ -947,6 +940,12 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain(BatchDev b) {
         } else {  // the last piece takes the interval's remaining MCUs
             if (mcu_run > nmcu_seg) bad = true;
             pm = nmcu_seg >= mcu_run ? nmcu_seg - mcu_run : 0u;
+        }
+        ent_run = (ent_run + 3u) & ~3u;  // pieces start on a 16-byte quad of entries
+        // a piece stores at most 63 entries per block: if that cannot fit, the counts are corrupt
+        if (uint64_t(ent_run) + 63ull * pm * S.bpm > uint64_t(S.ent0) + seg_entry_cap(S)) {
+            bad = true;
+            pm = 0;
         }
         b.piece_mcu0[u] = mcu_run;
         b.piece_nmcu[u] = pm;
@@ -1186,7 +1185,6 @@ __device__ __forceinline__ void colour8(const int (&Yv)[8], const int16_t* s_pl,
 //  4. lane = 8 consecutive output pixels: replicate chroma upsampling from the planes, colour
 //     (color.cpp:8-19), 24 contiguous output bytes per lane
 // Every LDS access pattern is conflict-free or 16-byte-vectorised; no LDS traffic in the IDCT.
-constexpr int kIdctPitch = 65;
 
 // 8 horizontally consecutive output samples of one plane row, replicate-upsampled by 2^shx:
 // one aligned 16-byte LDS read, then register selects only (no dynamically indexed arrays).
@@ -1212,9 +1210,12 @@ __device__ __forceinline__ void load8_samples(const int16_t* pl, uint32_t off, u
     v[7] = s0 ? x7 : (s1 ? h1 : h0);
 }
 
-__global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
-    __shared__ __attribute__((aligned(16))) int s_buf[64 * kIdctPitch + 3];
-    __shared__ uint32_t s_tab[3][64];  // (q << 6) | natural index, per component and zig-zag index
+__global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
+    // staging (64 rows of 66 int16 = 33 words: odd pitch, conflict-free read-back) and then the
+    // component planes share s_buf; planes need at most 64*64 + 64*2*6 int16 (§ host tile choice)
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2464];
+    __shared__ int s_qn[3 * 65];  // quant step per component, natural order (pitch 65: no bank clash)
+    __shared__ uint8_t s_nat[64];  // zig-zag -> natural
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t tile = blockIdx.x;
     const uint32_t tiles_x = im.tiles_x;
@@ -1224,27 +1225,30 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
     const uint32_t TM = im.tile_mcus, TR = im.tile_mrows, bpm = im.bpm, nc = im.ncomp;
     const uint32_t m0 = tx * TM, r0 = ty * TR;
     const uint32_t nm = min(TM, im.mcux - m0), nr = min(TR, im.mcuy - r0);
+    s_nat[lane] = kNatOfZz[lane];
     for (uint32_t i = lane; i < nc * 64; i += kIdctThreads) {
         const uint32_t c = i >> 6, z = i & 63u;
-        s_tab[c][z] = (uint32_t(b.qtabs[size_t(im.qslot[c]) * 64 + z]) << 6) | kNatOfZz[z];
+        s_qn[c * 65 + kNatOfZz[z]] = int(b.qtabs[size_t(im.qslot[c]) * 64 + z]);
     }
-    int4* z4 = reinterpret_cast<int4*>(s_buf);
-    for (uint32_t i = lane; i < (64 * kIdctPitch + 3) / 4; i += kIdctThreads) z4[i] = make_int4(0, 0, 0, 0);
+    constexpr int kRow16 = 33;  // words per staging row
+    uint4* z4 = reinterpret_cast<uint4*>(s_buf);
+    for (uint32_t i = lane; i < (64 * kRow16 + 3) / 4; i += kIdctThreads) z4[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
 
-    // 1. sparse -> dense (my block)
+    // 1. sparse -> dense (my block): quantised coefficients, natural order (parser.cpp:111,130:
+    //    the dequantisation happens on read-back, in zig-zag correspondence)
     const uint32_t m = lane / bpm, bb = lane - m * bpm;
     const uint32_t mr = m / TM, mi = m - mr * TM;
     const bool have = mr < nr && mi < nm;
     const uint32_t comp = (im.block_pattern >> (2 * bb)) & 3u;
-    int* row = s_buf + lane * kIdctPitch;
+    int16_t* row = reinterpret_cast<int16_t*>(s_buf + lane * kRow16);
     if (have) {
         const uint64_t gb = im.block_base + uint64_t((r0 + mr) * im.mcux + m0 + mi) * bpm + bb;
         const BlockInfo bi = b.blocks[gb];
         // a block of a corrupt stream may never have been written: never index past the entries
         int cnt = int(bi.cnt_dc >> 26);
         if (uint64_t(bi.entry_start) + uint64_t(cnt) > b.entries_cap) cnt = 0;
-        row[0] = (int32_t(bi.cnt_dc << 6) >> 6) * int(s_tab[comp][0] >> 6);
+        row[0] = int16_t(int32_t(bi.cnt_dc << 6) >> 6);  // DC: int16 by k_dpcm's range check
         // entries in 16-byte loads, four in flight at a time (the entry buffer is padded by 64 B)
         const uint32_t lead = bi.entry_start & 3u;
         const uint32_t* ep = b.entries + (bi.entry_start - lead);
@@ -1260,20 +1264,25 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int i = 4 * (c + u) + q - int(lead);
-                    if (i >= 0 && i < cnt) {
-                        const uint32_t t = s_tab[comp][w[q] & 63u];
-                        row[t & 63u] = (int32_t(w[q]) >> 16) * int(t >> 6);
-                    }
+                    if (i >= 0 && i < cnt) row[s_nat[w[q] & 63u]] = int16_t(w[q] >> 16);
                 }
             }
         }
     }
     __syncthreads();
 
-    // 2. IDCT in registers
+    // 2. dequantise (24-bit multiplies: |coef| < 2^15, q < 2^16) and IDCT in registers
     int blk[64];
+    {
+        const uint32_t* rw = s_buf + lane * kRow16;
+        const int* qn = s_qn + comp * 65;
 #pragma unroll
-    for (int p = 0; p < 64; p++) blk[p] = row[p];
+        for (int p = 0; p < 32; p++) {
+            const uint32_t w = rw[p];
+            blk[2 * p] = __mul24(int(int16_t(w & 0xFFFFu)), qn[2 * p]);
+            blk[2 * p + 1] = __mul24(int32_t(w) >> 16, qn[2 * p + 1]);
+        }
+    }
 #pragma unroll
     for (int r = 0; r < 8; r++) idct_row(blk + 8 * r);
 #pragma unroll
@@ -1281,7 +1290,7 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color(BatchDev b) {
     __syncthreads();  // every row read back before the planes overwrite the staging area
 
     // 3. component planes (int16), pitch = plane width + 8 samples
-    int16_t* s_pl = reinterpret_cast<int16_t*>(s_buf);
+    int16_t* s_pl = reinterpret_cast<int16_t*>(s_buf);  // planes reuse the staging area
     uint32_t pbase[3] = {0u, 0u, 0u}, ppitch[3] = {8u, 8u, 8u};
     {
         uint32_t off = 0;

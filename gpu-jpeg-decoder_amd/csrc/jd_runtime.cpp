@@ -326,7 +326,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             const uint32_t m1 = d.restart_interval ? std::min(m0 + d.restart_interval, nmcu) : nmcu;
             P.seg_img.push_back(uint32_t(i));
             P.seg_entry.push_back(uint32_t(entry_cursor));
-            entry_cursor += uint64_t(m1 - m0) * d.bpm * 63;
+            entry_cursor += uint64_t(m1 - m0) * (d.bpm * 63 + 3);  // + alignment of piece starts
         }
     }
     std::vector<uint32_t> order(P.imgs.size());

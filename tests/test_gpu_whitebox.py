@@ -47,7 +47,7 @@ def test_intervals_and_piece_starts(sync_decoder, name):
     pm0 = sync_decoder.debug_fetch("piece_mcu0")
     pnm = sync_decoder.debug_fetch("piece_nmcu")
     pe0 = sync_decoder.debug_fetch("piece_ent0")
-    ent0 = 0
+    prev_e0 = prev_e = 0
     errs = []
     for s, seg in enumerate(truth):
         if (int(ce[s]) - int(cs[s])) * 8 != seg["bits"]:
@@ -68,10 +68,11 @@ def test_intervals_and_piece_starts(sync_decoder, name):
             m, e = starts[b]
             if int(pm0[u]) != m and not (j == want_n - 1 and int(pnm[u]) == 0):
                 errs.append(f"seg {s} piece {j}: mcu0 gpu {pm0[u]} want {m}")
-            if j == 0:
-                ent0 = int(pe0[u])
-            elif int(pe0[u]) - ent0 != e and int(pnm[u]) > 0:
-                errs.append(f"seg {s} piece {j}: ent0 gpu {int(pe0[u]) - ent0} want {e}")
+            # every piece's first entry slot is the previous piece's end rounded up to a quad
+            want_e0 = (prev_e0 + (e - prev_e) + 3) // 4 * 4 if j > 0 else int(pe0[u])
+            if int(pe0[u]) != want_e0 or int(pe0[u]) % 4:
+                errs.append(f"seg {s} piece {j}: ent0 gpu {int(pe0[u])} want {want_e0}")
+            prev_e0, prev_e = int(pe0[u]), e
             nm += int(pnm[u])
         if nm != len(seg["starts"]) - 1:
             errs.append(f"seg {s}: MCUs gpu {nm} want {len(seg['starts']) - 1}")
