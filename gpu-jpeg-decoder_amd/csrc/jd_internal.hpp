@@ -11,7 +11,10 @@ namespace jd {
 
 // Fast Huffman lookup width: one LDS read resolves every code of <= kLutBits bits (and, when the
 // magnitude bits fit too, the coefficient value).  Longer codes take the canonical slow path.
-constexpr int kLutBits = 10;
+#ifndef JD_LUT_BITS
+#define JD_LUT_BITS 10
+#endif
+constexpr int kLutBits = JD_LUT_BITS;
 constexpr int kLutSize = 1 << kLutBits;
 
 #if defined(__HIPCC__)
@@ -125,6 +128,17 @@ constexpr int kScanBytesPerThread = 64;
 constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
 constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cannot hold more
 
+constexpr int kCpMax = 8;          // checkpoints per piece (k_rescan / k_chain shortcuts)
+constexpr int kCpRecords = kCpMax + 1;
+
+// Speculative-scan checkpoints, kCpRecords per piece slot: kCpMax checkpoints, then the totals.
+//   checkpoint: {bit of an MCU boundary, MCUs and AC entries counted up to it, error so far}
+//   totals:     {end, MCUs, AC entries, error | checkpoints << 8}
+// A re-scan from the true start that reaches a checkpoint's bit at an MCU boundary is in the
+// speculative walk's state there, so it joins it: counts = its own + (totals - checkpoint).
+struct alignas(16) CpRec {
+    uint32_t bit, mcus, ents, flags;
+};
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
 constexpr int kTileMaxBlocks = 64;   // blocks per IDCT/colour tile (one lane each)
 
@@ -159,6 +173,7 @@ struct BatchDev {
     uint32_t* piece_nent;         // scan: AC entries in the piece
     uint32_t* piece_mcu0;         // chain: first MCU of the piece within its segment
     uint32_t* piece_ent0;         // chain: first AC-entry slot of the piece
+    CpRec* piece_cp;              // scan: kCpRecords per piece slot (CpRec)
     const uint32_t* chain_seg;    // k_chain: segment of each lane, grouped by table set
     uint32_t nchain;              // multiple of kPieceThreads
     const uint32_t* chain_wg_tableset;

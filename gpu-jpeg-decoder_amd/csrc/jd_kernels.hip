@@ -451,7 +451,10 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     for (uint32_t u = used + lane; u < im.sub_cap; u += 64) b.sub_seg[im.sub_base + u] = kInvalidImage;
 }
 
-constexpr int kWinAdv = 64;                       // bytes a round advances
+#ifndef JD_WIN_ADV
+#define JD_WIN_ADV 64
+#endif
+constexpr int kWinAdv = JD_WIN_ADV;               // bytes a round advances
 constexpr int kWinLoads = kWinAdv / 16 + 1;       // 16-byte loads per window (advance + overlap)
 constexpr int kRowWords = 1 + 4 * kWinLoads;      // 21: odd pitch (last word unused)
 static_assert(kRowWords % 2 == 1, "row pitch must be odd");
@@ -473,6 +476,7 @@ struct Walk {
     uint64_t blk0;                      // write: global block of the first MCU's first block
     uint32_t m_start, m_end, mcus, ents;  // scan results (m_start = kNoPiece: none found)
     uint32_t end;                       // bit after the last symbol decoded
+    uint32_t ncp;                       // scan: checkpoints recorded
     bool bad;
 };
 
@@ -639,8 +643,29 @@ __device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const 
 // once per window round.  Entry counts are differences of a running count, the error flag is
 // one OR of the entry's error bit, and running past the data is checked per round (the scan
 // stores nothing, so decoding a little garbage past the end is harmless).
+//
+// KIND kScanSpec records a checkpoint (CpRec) at the first MCU boundary after every cp_bits counted
+// bits; kScanJoin (a re-scan from the true start) stops at the first MCU boundary that is one of
+// those checkpoints and takes the rest of the counts from the speculative walk's totals.
+constexpr int kScanSpec = 0, kScanJoin = 1;
+template <int KIND>
 __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
-                                          uint32_t* row, bool active_in, Walk& W) {
+                                          uint32_t* row, bool active_in, Walk& W, CpRec* cp, uint32_t cp_bits) {
+    uint32_t cpb[kCpMax];  // join: checkpoint bits (0xFFFFFFFF: none / taken after an error)
+    CpRec tot = {0u, 0u, 0u, 0u};
+    if (KIND == kScanJoin) {
+        if (active_in) tot = cp[kCpMax];
+        const uint32_t ncp = tot.flags >> 8;
+#pragma unroll
+        for (int c = 0; c < kCpMax; c++) {
+            cpb[c] = 0xFFFFFFFFu;
+            if (active_in && uint32_t(c) < ncp) {
+                const CpRec r = cp[c];
+                if (!(r.flags & 1u)) cpb[c] = r.bit;
+            }
+        }
+    }
+    uint32_t joined = 0, ncp = 0, next_cp = 0;
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
@@ -668,6 +693,7 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
     uint32_t errs = 0;  // bit 16: a bad code since counting began
     bool active = active_in;
     if (counting && W.start + 8 > sbits) active = false;  // starts at the data end: empty
+    next_cp = W.start + cp_bits;
     while (true) {
         const uintptr_t na = wa + kWinAdv;
         u32x4 nx[kWinLoads];
@@ -702,6 +728,7 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
                     if (consumed >= W.warm_to) {  // synchronised: the piece starts here
                         counting = 1u;
                         m_start = consumed;
+                        next_cp = consumed + cp_bits;
                         ents0 = ents;
                         errs = 0;
                         if (at_end) {
@@ -714,6 +741,19 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
                     if (consumed >= W.stop_at || at_end) {  // the piece ends here
                         m_end = consumed;
                         active = false;
+                    } else if (KIND == kScanSpec && consumed >= next_cp && ncp < uint32_t(kCpMax)) {
+                        cp[ncp] = CpRec{consumed, mcus, ents - ents0, (errs >> 16) & 1u};
+                        ncp++;
+                        next_cp = consumed + cp_bits;
+                    } else if (KIND == kScanJoin) {
+                        uint32_t hit = 0;
+#pragma unroll
+                        for (int c = 0; c < kCpMax; c++) hit = (cpb[c] == consumed) ? uint32_t(c + 1) : hit;
+                        if (hit) {  // in the speculative walk's state: join it
+                            joined = hit;
+                            m_end = consumed;
+                            active = false;
+                        }
                     }
                 }
             }
@@ -740,6 +780,14 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
     W.m_end = m_end;
     W.mcus = mcus;
     W.ents = ents - ents0;
+    W.ncp = ncp;
+    if (KIND == kScanJoin && joined) {
+        const CpRec c = cp[joined - 1];
+        W.m_end = tot.bit;
+        W.mcus += tot.mcus - c.mcus;
+        W.ents += tot.ents - c.ents;
+        W.bad = W.bad || (tot.flags & 1u);
+    }
 }
 
 __device__ __forceinline__ void table_slots(const TableSet& ts, const SegInfo& S, uint32_t& dcp, uint32_t& acp) {
@@ -806,8 +854,10 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
             W.nmcu = 0;
         }
     }
+    CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     if (MODE == kWalkScan)
-        walk_scan(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
+        walk_scan<kScanSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
+                             valid, W, cp, b.piece_bits / kCpMax);
     else
         walk<kWalkWrite>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
     if (!valid) return;
@@ -817,6 +867,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
         b.piece_end[u] = W.m_end;
         b.piece_nmcu[u] = W.mcus | (W.bad ? 0x80000000u : 0u);  // bit 31: error while counting
         b.piece_nent[u] = W.ents;
+        cp[kCpMax] = CpRec{W.m_end, W.mcus, W.ents, (W.bad ? 1u : 0u) | (W.ncp << 8)};
     } else {
         bool bad = W.bad;
         if (j + 1 == npc && !bad) {
@@ -866,7 +917,8 @@ __global__ __launch_bounds__(kPieceThreads) void k_rescan(BatchDev b) {
     W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
     W.nmcu = W.ent0 = 0;
     W.blk0 = 0;
-    walk_scan(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, need, W);
+    walk_scan<kScanJoin>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, need, W,
+                         b.piece_cp + size_t(u) * kCpRecords, b.piece_bits / kCpMax);
     if (!need) return;
     b.piece_bit[u] = W.start;
     b.piece_end[u] = W.m_end;
@@ -925,7 +977,8 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain(BatchDev b) {
             W.stop_at = (j + 1 == n) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
             W.nmcu = W.ent0 = 0;
             W.blk0 = 0;
-            walk_scan(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, true, W);
+            walk_scan<kScanJoin>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
+                                 true, W, b.piece_cp + size_t(u) * kCpRecords, b.piece_bits / kCpMax);
             pbit = expect;
             pend = W.m_end;
             pm = W.mcus;

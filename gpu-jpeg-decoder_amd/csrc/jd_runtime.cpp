@@ -447,6 +447,7 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         const size_t o_subseg = reserve(end, nsub * 4);
         size_t o_piece[6];
         for (int q = 0; q < 6; q++) o_piece[q] = reserve(end, nsub * 4);
+        const size_t o_cp = reserve(end, nsub * kCpRecords * sizeof(CpRec));
         HIPCHK(ctx, ensure_dev(ctx->plan, end));
         HIPCHK(ctx, ensure_pin(ctx->plan_host, upload));
         memcpy(ctx->plan_host.p, blob.data(), upload);
@@ -487,6 +488,7 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         b.piece_nent = pc[3];
         b.piece_mcu0 = pc[4];
         b.piece_ent0 = pc[5];
+        b.piece_cp = reinterpret_cast<CpRec*>(base + o_cp);
         b.max_slots = P.max_slots;
         b.max_chunks = P.max_chunks;
         b.chunk_nbrk = reinterpret_cast<uint32_t*>(base + o_nbrk);
@@ -785,6 +787,7 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
         case 11: src = b.entries; n = ctx->last_entries * 4; break;
         case 12: src = b.piece_mcu0; n = size_t(b.nsub) * 4; break;
         case 13: src = b.piece_ent0; n = size_t(b.nsub) * 4; break;
+        case 14: src = b.piece_cp; n = size_t(b.nsub) * kCpRecords * sizeof(CpRec); break;
         default: return JD_ERR_INVALID_ARG;
     }
     *nbytes = n;

@@ -88,7 +88,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("JDAMD_LIB") or LIB_PATH  # JDAMD_LIB: an experiment build
     if not os.path.exists(p):
         raise FileNotFoundError(f"{p} not built: run `make -C gpu-jpeg-decoder_amd` or __graft_entry__.build()")
     lib = ctypes.CDLL(p)
@@ -344,7 +344,8 @@ class Decoder:
                     "seg_sub_base": (3, np.uint32, 1), "seg_nsub": (4, np.uint32, 1), "piece_bit": (5, np.uint32, 1),
                     "piece_end": (6, np.uint32, 1), "piece_nmcu": (7, np.uint32, 1), "piece_nent": (8, np.uint32, 1),
                     "sub_seg": (9, np.uint32, 1), "status": (10, np.uint32, 1), "entries": (11, np.uint32, 1),
-                    "piece_mcu0": (12, np.uint32, 1), "piece_ent0": (13, np.uint32, 1)}
+                    "piece_mcu0": (12, np.uint32, 1), "piece_ent0": (13, np.uint32, 1),
+                    "piece_cp": (14, np.uint32, 36)}
 
     def debug_fetch(self, name: str) -> np.ndarray:
         """Internal array of the most recent batch (white-box tests and debugging)."""

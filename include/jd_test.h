@@ -24,7 +24,9 @@ jd_status jd_test_color(jd_ctx* ctx, const int32_t* ycc_dev, uint8_t* rgb_dev, i
  * what: 0 blocks (8 B each), 1 seg_cstart, 2 seg_cend, 3 seg_sub_base, 4 seg_nsub (u32 each),
  *       5 piece_bit, 6 piece_end, 7 piece_nmcu, 8 piece_nent, 9 sub_seg (u32 per piece slot),
  *       10 status (u32 per image), 11 entries (u32), 12 piece_mcu0, 13 piece_ent0 (u32 per piece
- *       slot).  *nbytes receives the array size; at most cap bytes are copied. */
+ *       slot), 14 piece_cp (9 x 16 B per piece slot: 8 scan checkpoints {bit, MCUs, entries,
+ *       error} and the totals {end, MCUs, entries, error | checkpoints << 8}).
+ *       *nbytes receives the array size; at most cap bytes are copied. */
 jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* host_dst, size_t cap, size_t* nbytes);
 
 #ifdef __cplusplus

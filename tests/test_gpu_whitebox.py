@@ -81,6 +81,43 @@ def test_intervals_and_piece_starts(sync_decoder, name):
     assert not errs, "\n".join(errs[:20])
 
 
+@pytest.mark.parametrize("name", CASES)
+def test_scan_checkpoints(sync_decoder, name):
+    """Checkpoints (k_piece scan) sit on true MCU boundaries with the counts from the piece start,
+    for every piece whose speculative start synchronised (the join shortcut relies on both)."""
+    data = _load(name)
+    try:
+        sync_decoder.decode(data)
+    except Exception:
+        pass
+    truth = jd_trace.mcu_starts(data)
+    ssb = sync_decoder.debug_fetch("seg_sub_base")
+    nsub = sync_decoder.debug_fetch("seg_nsub")
+    pbit = sync_decoder.debug_fetch("piece_bit")
+    cp = sync_decoder.debug_fetch("piece_cp").reshape(-1, 9, 4)
+    checked = bad = 0
+    for s, seg in enumerate(truth):
+        starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
+        for j in range(int(nsub[s])):
+            u = int(ssb[s]) + j
+            tot = cp[u, 8]
+            ncp = int(tot[3]) >> 8
+            assert ncp <= 8
+            b0 = int(pbit[u])
+            if b0 not in starts or ncp == 0:
+                continue
+            m0, e0 = starts[b0]
+            for c in range(ncp):
+                bit, mcus, ents, err = (int(x) for x in cp[u, c])
+                if bit in starts and (starts[bit][0] - m0, starts[bit][1] - e0) == (mcus, ents) and err == 0:
+                    checked += 1
+                else:
+                    bad += 1
+    # a piece whose speculative start did not synchronise records its checkpoints on a wrong
+    # trajectory (k_rescan ignores them unless it meets one at an MCU boundary)
+    assert checked > 0 and bad <= checked // 20, (checked, bad)
+
+
 def _s16(x):
     return ((x + 0x8000) & 0xFFFF) - 0x8000
 

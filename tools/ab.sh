@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B: bench C2 with each experiment build given as an argument (libjdamd_<V>.so; "base" = libjdamd.so).
+# Usage: bash tools/ab.sh OUTDIR V1 V2 ...   (each run under its own time limit; stops at the first failure)
+set -e
+out=$1; shift
+mkdir -p "$out"
+for v in "$@"; do
+  lib=gpu-jpeg-decoder_amd/libjdamd_$v.so; [ "$v" = base ] && lib=gpu-jpeg-decoder_amd/libjdamd.so
+  JDAMD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-sample 0 > "$out/$v.json" 2> "$out/$v.err"
+  python - "$out/$v.json" "$v" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], round(d["value"]), round(d["ms_per_step"], 3), {k: round(v, 3) for k, v in d.get("kernels_ms_per_step", {}).items()})
+PY
+done
