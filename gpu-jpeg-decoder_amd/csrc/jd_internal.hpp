@@ -26,14 +26,19 @@ constexpr int kLutSize = 1 << kLutBits;
 // Device Huffman table (built on the host from a DHT table, uploaded once, cached by content).
 //   fast[i]: entry for the symbol whose code starts the next kLutBits stream bits (= i):
 //     bits 0..4   L    bits the symbol consumes, code + magnitude (0: code longer than kLutBits)
-//     bits 5..8   run  AC zero run (symbol >> 4); 0 for DC
-//     bit  9      eob  AC end-of-block (symbol 0x00)
-//     bit  10     emit AC coefficient stored (size != 0)
-//     bits 11..15 sz   magnitude bits (DC: symbol, AC: symbol & 15)
+//     bit  6      emit AC coefficient stored (size != 0)
+//     bits 8..14  adv  advance of the coefficient index z (the last position decoded, DC = 0):
+//                      DC 0, AC run + 1 (ZRL 16), EOB 64.  A block ends when z + adv >= 63, and
+//                      a coefficient lands at z + adv unless that is past 63 (parser.cpp:120-131:
+//                      its magnitude bits are consumed, the value dropped, the block ends)
+//     bit  15     dc   DC symbol
+//     bits 16..20 sz   magnitude bits (DC: symbol, AC: symbol & 15)
+//     bit  21     bad  corrupt code (slow path only)
 //   The coefficient is always EXTEND(the last sz of the L bits), so a decode step is one lookup
 //   plus bit-field extracts.  Codes longer than kLutBits take the canonical slow path:
 //   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not
 //                < lim[l-1]) — the canonical DECODE procedure of JPEG Annex F.2.2.3
+//   lim[19]    : 1 for a DC table
 //   base[l]    : valptr[l] - mincode[l]; vals[] the symbols in code order
 struct alignas(16) HuffLut {
     uint32_t fast[kLutSize];
@@ -43,14 +48,16 @@ struct alignas(16) HuffLut {
 };
 static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
 constexpr int kLutWords = int(sizeof(HuffLut) / 4);
+constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 21;
 
 // Entry of a code of length l for symbol sym; 0 when it cannot be represented (l + sz > 31 or a
 // DC size beyond 16 bits: corrupt for 8-bit baseline, whose DC sizes are <= 11).
 JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
     const uint32_t sz = is_dc ? sym : (sym & 15u);
     if (sz > 16u || l + sz > 31u || l == 0u) return 0u;
-    if (is_dc) return (l + sz) | (sz << 11);
-    return (l + sz) | ((sym >> 4) << 5) | (sym == 0u ? 512u : 0u) | (sz ? 1024u : 0u) | (sz << 11);
+    if (is_dc) return (l + sz) | kEntDc | (sz << 16);
+    const uint32_t adv = sym == 0u ? 64u : (sym >> 4) + 1u;
+    return (l + sz) | (sz ? kEntEmit : 0u) | (adv << 8) | (sz << 16);
 }
 
 // Maximum Huffman tables a table set (one workgroup of the Huffman kernel) stages into LDS.

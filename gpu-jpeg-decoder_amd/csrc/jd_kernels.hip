@@ -339,9 +339,9 @@ __device__ __forceinline__ u32x4 load16(uintptr_t a, uintptr_t last) {
 // of left-justified limits <= v16: F.2.2.3 restated, independent LDS reads), then the symbol.
 // Returns the entry in the fast-table format.  Codes that match nothing and symbols the format
 // cannot represent (corrupt streams/tables) give kEntryBad: 16 bits consumed (decoding always
-// advances) and bit 16 set.
-constexpr uint32_t kEntryBad = 16u | (1u << 16);
-__device__ __forceinline__ uint32_t huff_slow(const uint32_t* lutw, uint32_t peek, bool is_dc) {
+// advances), the bad bit set.
+constexpr uint32_t kEntryBad = 16u | kEntBad;
+__device__ __forceinline__ uint32_t huff_slow(const uint32_t* lutw, uint32_t peek) {
     const HuffLut* t = reinterpret_cast<const HuffLut*>(lutw);
     const uint32_t v16 = peek >> 16;
     uint32_t l = kLutBits + 1;
@@ -350,14 +350,14 @@ __device__ __forceinline__ uint32_t huff_slow(const uint32_t* lutw, uint32_t pee
     uint32_t e = 0;
     if (l <= 16 && v16 >= t->lim[kLutBits]) {
         const uint32_t sym = t->vals[uint32_t(t->base[l] + int(v16 >> (16 - l))) & 255u];
-        e = lut_entry(l, sym, is_dc);
+        e = lut_entry(l, sym, t->lim[19] != 0);
     }
     return e ? e : kEntryBad;
 }
 
 // EXTEND (utils/stream.cpp:44-52) of the last sz bits of the L bits at the top of peek.
 __device__ __forceinline__ int huff_value(uint32_t peek, uint32_t e) {
-    const uint32_t L = e & 31u, sz = __builtin_amdgcn_ubfe(e, 11u, 5u);
+    const uint32_t L = e & 31u, sz = __builtin_amdgcn_ubfe(e, 16u, 5u);
     const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - L, sz);  // width 0 -> 0
     const uint32_t half = (1u << sz) >> 1;
     return int(mag) - (mag < half ? int(2 * half - 1) : 0);
@@ -480,169 +480,154 @@ struct Walk {
     bool bad;
 };
 
-template <int MODE>
-__device__ __forceinline__ void walk(const BatchDev& b, const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp,
-                                     uint32_t acp, uint32_t* row, bool active_in, Walk& W) {
+// Stream reader over a lane's LDS row of big-endian words.  A and B are the words under the read
+// position and s = 32 - (bits of A consumed), 0..31 (s = 0: A is used up, the next symbol starts
+// at B), so the next 32 stream bits are alignbit(A, B, s).  nextw = row[rp] is the word after B,
+// read one symbol ahead; wb places row[0] in the interval: bit of the next symbol =
+// rp * 32 + wb - s.  A symbol advances the reader by at most 31 bits, so by at most one word.
+struct BitRow {
+    uint32_t A, B, nextw;
+    int s, rp, wb;
+    __device__ __forceinline__ void init(const uint32_t* row, uint32_t off, uint32_t start) {
+        const uint32_t w0 = off >> 5, o = off & 31u;
+        A = o ? row[w0] : 0u;
+        B = row[w0 + (o ? 1u : 0u)];
+        rp = int(w0 + (o ? 2u : 1u));
+        nextw = row[rp];
+        s = int((32u - o) & 31u);
+        wb = int(start) - int(off) - 32;
+    }
+    __device__ __forceinline__ uint32_t peek() const { return __builtin_amdgcn_alignbit(A, B, uint32_t(s)); }
+    __device__ __forceinline__ void skip(uint32_t L, const uint32_t* row) {
+        s -= int(L);
+        const bool need = s < 0;
+        s &= 31;  // s + 32 when negative (L <= 31)
+        A = need ? B : A;
+        B = need ? nextw : B;
+        rp += need ? 1 : 0;
+        nextw = row[rp];
+    }
+    __device__ __forceinline__ uint32_t bit() const { return uint32_t((rp << 5) + wb - s); }
+    __device__ __forceinline__ void next_window() {
+        rp -= kWinAdv / 4;
+        wb += kWinAdv * 8;
+    }
+};
+
+#define JD_ROW_FILL(row, v, q)                        \
+    do {                                              \
+        (row)[4 * (q) + 0] = __builtin_bswap32(v.x);  \
+        (row)[4 * (q) + 1] = __builtin_bswap32(v.y);  \
+        (row)[4 * (q) + 2] = __builtin_bswap32(v.z);  \
+        (row)[4 * (q) + 3] = __builtin_bswap32(v.w);  \
+    } while (0)
+
+// Decoder state per symbol (both walks): z = coefficient index of the last symbol (DC: 0), b3 =
+// 3 x block within the MCU, tab = LDS byte offset of the next symbol's table (DC table of the
+// block after a block ends, else the block's AC table).
+constexpr uint32_t kLutBytes = sizeof(HuffLut);
+// tab is an LDS address: lut_fast is one v_lshl_add of the index onto it and the LDS read (the
+// empty asm keeps the compiler from re-associating (peek >> 22) << 2 into a shift-and-mask).
+typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return uint32_t(size_t((lds_u32*)p)); }
+__device__ __forceinline__ const uint32_t* lut_at(uint32_t tab) { return (const uint32_t*)(lds_u32*)size_t(tab); }
+__device__ __forceinline__ uint32_t lut_fast(uint32_t tab, uint32_t peek) {
+    uint32_t idx = peek >> (32 - kLutBits);
+    asm("" : "+v"(idx));
+    return *reinterpret_cast<lds_u32*>(size_t((idx << 2) + tab));
+}
+//
+// The write walk: nmcu MCUs from the MCU boundary `start`: BlockInfo (DC difference) + AC entries.
+// AC entries shift through a 4-entry register queue and leave as one 16-byte store per aligned
+// quad [ent - 4, ent): a wave's 64 lanes store to 64 unrelated places, so store instructions, not
+// bytes, bound this pass.  Pieces start on a quad (k_chain aligns them); the last, partial quad
+// is stored dword by dword.  The walk stops after its last block; running past the interval's
+// data is checked once per window round (writes stay inside the piece's slots either way).
+__device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp,
+                                           uint32_t acp, uint32_t* row, bool active_in, Walk& W) {
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
     for (int q = 0; q < kWinLoads; q++) {
         const u32x4 v = load16(wa + 16 * q, S.last);
-        row[4 * q + 0] = __builtin_bswap32(v.x);
-        row[4 * q + 1] = __builtin_bswap32(v.y);
-        row[4 * q + 2] = __builtin_bswap32(v.z);
-        row[4 * q + 3] = __builtin_bswap32(v.w);
+        JD_ROW_FILL(row, v, q);
     }
-    // 64-bit bit buffer: the next symbol is always in its top 32 bits (nb >= 32 between steps)
-    const uint32_t off = uint32_t(a_start & 15) * 8 + (W.start & 7u);
-    int rp = int(off >> 5);
-    uint64_t bb = ((uint64_t(row[rp]) << 32) | row[rp + 1]) << (off & 31);
-    int nb = 64 - int(off & 31);
-    rp += 2;
-    uint32_t nextw = row[rp];
-    int consumed = int(W.start);  // interval bit of the next symbol
-    const int sbits = int(S.bits);
-    BlockInfo* const bout = b.blocks + (W.blk0 - 1);  // bout[blk] after blk++ = this block
+    BitRow R;
+    R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
+    BlockInfo* const bout = b.blocks + W.blk0;
     uint32_t* const eout = b.entries;
-    const int bpm = int(S.bpm);
     const uint32_t nblk = W.nmcu * S.bpm;
-    // decode state: k = next coefficient index (0: DC next), bi = block in MCU, tab = LDS word
-    // offset of the next symbol's table
-    int k = 0, bi = 0;
-    uint32_t actab = (acp & 7u) * uint32_t(kLutWords);
-    uint32_t tab = (dcp & 7u) * uint32_t(kLutWords);
-    uint32_t nblk_seen = 0;
-    // scan: phase 0 = synchronising, 1 = counting
-    uint32_t counting = (W.warm_to == W.start) ? 1u : 0u;
-    uint32_t mcus = 0, ents = 0, m_start = counting ? W.start : kNoPiece, m_end = 0;
-    // write: pending symbol whose bookkeeping runs while the next lookup is in flight.  Flags are
-    // integer bits in VGPRs (boolean lane masks would need SALU merges at divergent loop exits).
-    constexpr uint32_t kQValid = 1u, kQDc = 2u, kQEmit = 4u, kQFin = 8u;
-    uint32_t qf = 0, q_peek = 0, q_e = 0, q_k = 0;
+    const uint32_t bpm3 = 3u * S.bpm;
+    const uint32_t lbase = lds_addr(s_lutw);
+    const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
+    uint32_t z = 0, b3 = 0, tab = tab_dc0;
     uint32_t ent = W.ent0, ent_blk = W.ent0, blk = 0;
     int dcd = 0;
-    // AC entries are write-combined into the aligned quad [ent & ~3, +4): one 16-byte store per
-    // four entries (a wave's 64 lanes store to 64 unrelated places, so store instructions, not
-    // bytes, are what the write pass is bound by).  Pieces start on a quad (k_chain aligns
-    // them); the last, partial quad is stored dword by dword.
     uint32_t wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;
-    uint32_t bad = 0;
-    bool active = active_in && (MODE == kWalkScan || nblk > 0);
-    if (MODE == kWalkScan && counting && W.start + 8 > S.bits) {  // starts at the data end: empty
-        active = false;
-        m_end = W.start;
-    }
-#define JD_WALK_BOOK()                                                                                         \
-    do {                                                                                                       \
-        const bool q_dc = (qf & kQDc) != 0, q_emit = (qf & kQEmit) != 0;                                       \
-        const int val_ = huff_value(q_peek, q_e);                                                              \
-        dcd = q_dc ? val_ : dcd;                                                                               \
-        ent_blk = q_dc ? ent : ent_blk;                                                                        \
-        blk += q_dc ? 1u : 0u;                                                                                 \
-        const uint32_t ev_ = (uint32_t(val_) << 16) | q_k, sl_ = ent & 3u;                                     \
-        wq0 = (q_emit && sl_ == 0u) ? ev_ : wq0;                                                               \
-        wq1 = (q_emit && sl_ == 1u) ? ev_ : wq1;                                                               \
-        wq2 = (q_emit && sl_ == 2u) ? ev_ : wq2;                                                               \
-        wq3 = (q_emit && sl_ == 3u) ? ev_ : wq3;                                                               \
-        if (q_emit && sl_ == 3u) *reinterpret_cast<uint4*>(eout + ent - 3u) = make_uint4(wq0, wq1, wq2, wq3);  \
-        ent += q_emit ? 1u : 0u;                                                                               \
-        if (qf & kQFin) bout[blk] = BlockInfo{ent_blk, pack_cnt_dc(ent - ent_blk, dcd)};                       \
-    } while (0)
+    uint32_t errs = 0;
+    bool active = active_in && nblk > 0;
     while (true) {
         const uintptr_t na = wa + kWinAdv;
         u32x4 nx[kWinLoads];
 #pragma unroll
         for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
-        while (active && rp <= kWinAdv / 4) {
-            const uint32_t peek = uint32_t(bb >> 32);
-            const bool is_dc = k == 0;
-            uint32_t e = s_lutw[tab + (peek >> (32 - kLutBits))];
-            if (MODE == kWalkWrite && (qf & kQValid)) JD_WALK_BOOK();  // overlaps the lookup
-            if ((e & 31u) == 0) e = huff_slow(s_lutw + tab, peek, is_dc);  // 0.3 % of symbols
-            bad |= (MODE == kWalkWrite || counting) ? ((e >> 16) & 1u) : 0u;
-            const uint32_t L = e & 31u;
-            bb <<= L;
-            nb -= int(L);
-            const bool need = nb < 32;
-            bb |= need ? (uint64_t(nextw) << (32 - nb)) : 0ull;
-            nb += need ? 32 : 0;
-            rp += need ? 1 : 0;
-            nextw = row[rp];
-            consumed += int(L);
+        while (active && R.rp <= kWinAdv / 4) {
+            const uint32_t peek = R.peek();
+            uint32_t e = lut_fast(tab, peek);
+            if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
+            errs |= e;
+            const int val = huff_value(peek, e);
+            R.skip(e & 31u, row);
             // EOB / ZRL / run-size (parser.cpp:114-134)
-            const int knew = k + int(__builtin_amdgcn_ubfe(e, 5u, 4u));
-            const bool fin = !is_dc && ((e & 512u) != 0 || knew >= 63);
-            const bool emit = !is_dc && (e & 1024u) != 0 && knew < 64;
-            const int nbi = (bi + 1 == bpm) ? 0 : bi + 1;
-            if (MODE == kWalkWrite) {
-                qf = kQValid | (is_dc ? kQDc : 0u) | (emit ? kQEmit : 0u) | (fin ? kQFin : 0u);
-                q_peek = peek;
-                q_e = e;
-                q_k = uint32_t(knew);
-                nblk_seen += is_dc ? 1u : 0u;
-                bad |= consumed > sbits ? 1u : 0u;  // consumed bits past the interval's data
-                active = !bad && !(fin && nblk_seen >= nblk);
-            } else {
-                ents += (counting && emit) ? 1u : 0u;
-                const bool mcu_end = fin && nbi == 0;
-                const bool sync_done = !counting && mcu_end && uint32_t(consumed) >= W.warm_to;
-                // stop at the first MCU boundary at/after stop_at, or within the last byte (the data
-                // ends there: later pieces are empty; an early stop only costs a chain re-scan)
-                const bool at_end = consumed + 8 > sbits;
-                const bool count_done =
-                    (counting && mcu_end && (uint32_t(consumed) >= W.stop_at || at_end)) || (sync_done && at_end);
-                mcus += (counting && mcu_end) ? 1u : 0u;
-                m_start = sync_done ? uint32_t(consumed) : m_start;
-                m_end = count_done ? uint32_t(consumed) : m_end;
-                counting = sync_done ? 1u : counting;
-                const bool over = consumed > sbits;  // past the data: the walk cannot go on
-                bad |= (counting && over && !count_done) ? 1u : 0u;
-                const bool stop = count_done || over || bad;
-                m_end = stop ? uint32_t(consumed) : m_end;
-                active = !stop;
+            const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+            const bool fin = zn >= 63u;
+            const bool emit = (e & ~zn & kEntEmit) != 0;  // zn < 64 (bit 6 of zn clear)
+            dcd = (e & kEntDc) ? val : dcd;
+            const uint32_t ev = (uint32_t(val) << 16) | zn;
+            wq0 = emit ? wq1 : wq0;
+            wq1 = emit ? wq2 : wq1;
+            wq2 = emit ? wq3 : wq2;
+            wq3 = emit ? ev : wq3;
+            ent += emit ? 1u : 0u;
+            if (emit && (ent & 3u) == 0u) *reinterpret_cast<uint4*>(eout + ent - 4u) = make_uint4(wq0, wq1, wq2, wq3);
+            if (fin) {
+                bout[blk] = BlockInfo{ent_blk, pack_cnt_dc(ent - ent_blk, dcd)};
+                blk++;
+                ent_blk = ent;
+                active = blk < nblk;
             }
-            bi = fin ? nbi : bi;
-            actab = fin ? __builtin_amdgcn_ubfe(acp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
-            tab = fin ? __builtin_amdgcn_ubfe(dcp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
-            k = fin ? 0 : (is_dc ? 1 : knew + 1);
+            z = fin ? 0u : zn;
+            b3 += fin ? 3u : 0u;
+            tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
+            tab = (b3 == bpm3) ? tab_dc0 : tab;  // an MCU ends here
+            b3 = (b3 == bpm3) ? 0u : b3;
+        }
+        if (active && R.bit() > S.bits) {  // past the interval's data
+            errs |= kEntBad;
+            active = false;
         }
         if (__ballot(active) == 0) break;  // wave-uniform
 #pragma unroll
-        for (int q = 0; q < kWinLoads; q++) {
-            row[4 * q + 0] = __builtin_bswap32(nx[q].x);
-            row[4 * q + 1] = __builtin_bswap32(nx[q].y);
-            row[4 * q + 2] = __builtin_bswap32(nx[q].z);
-            row[4 * q + 3] = __builtin_bswap32(nx[q].w);
-        }
-        rp -= kWinAdv / 4;
+        for (int q = 0; q < kWinLoads; q++) JD_ROW_FILL(row, nx[q], q);
+        R.next_window();
         wa = na;
     }
-    if (MODE == kWalkWrite && (qf & kQValid)) JD_WALK_BOOK();
-#undef JD_WALK_BOOK
-    if (MODE == kWalkWrite && (ent & 3u)) {  // the last, partial quad
-        const uint32_t qb = ent & ~3u;
-        eout[qb] = wq0;
-        if (ent > qb + 1u) eout[qb + 1u] = wq1;
-        if (ent > qb + 2u) eout[qb + 2u] = wq2;
+    if (ent & 3u) {  // the last, partial quad: its r entries are the newest, wq[4-r..3]
+        const uint32_t r = ent & 3u, qb = ent - r;
+        eout[qb] = r == 3u ? wq1 : r == 2u ? wq2 : wq3;
+        if (r >= 2u) eout[qb + 1u] = r == 3u ? wq2 : wq3;
+        if (r == 3u) eout[qb + 2u] = wq3;
     }
-    W.end = uint32_t(consumed);
-    W.bad = bad != 0;
-    if (MODE == kWalkWrite) {
-        W.bad = W.bad || (nblk > 0 && (nblk_seen != nblk || k != 0));
-        W.ents = ent - W.ent0;
-    } else {
-        W.m_start = m_start;
-        W.m_end = m_end;
-        W.mcus = mcus;
-        W.ents = ents;
-    }
+    W.end = R.bit();
+    W.bad = (errs & kEntBad) != 0 || (nblk > 0 && blk != nblk) || W.end > S.bits;
+    W.ents = ent - W.ent0;
 }
 
-// The scan walk on its own: per symbol only the table lookup, the bit buffer and the block state
-// machine; everything else happens at MCU boundaries (a branch taken by ~half the wave-steps) or
-// once per window round.  Entry counts are differences of a running count, the error flag is
-// one OR of the entry's error bit, and running past the data is checked per round (the scan
-// stores nothing, so decoding a little garbage past the end is harmless).
+// The scan walk: per symbol only the table lookup, the reader and the block state machine;
+// everything else happens at MCU boundaries (a branch taken by ~half the wave-steps) or once per
+// window round.  Entry counts are differences of a running count, the error flag is one OR of
+// the entry's bad bit, and running past the data is checked per round (the scan stores nothing
+// per symbol, so decoding a little garbage past the end is harmless).
 //
 // KIND kScanSpec records a checkpoint (CpRec) at the first MCU boundary after every cp_bits counted
 // bits; kScanJoin (a re-scan from the true start) stops at the first MCU boundary that is one of
@@ -671,26 +656,18 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
 #pragma unroll
     for (int q = 0; q < kWinLoads; q++) {
         const u32x4 v = load16(wa + 16 * q, S.last);
-        row[4 * q + 0] = __builtin_bswap32(v.x);
-        row[4 * q + 1] = __builtin_bswap32(v.y);
-        row[4 * q + 2] = __builtin_bswap32(v.z);
-        row[4 * q + 3] = __builtin_bswap32(v.w);
+        JD_ROW_FILL(row, v, q);
     }
-    const uint32_t off = uint32_t(a_start & 15) * 8 + (W.start & 7u);
-    int rp = int(off >> 5);
-    uint64_t bb = ((uint64_t(row[rp]) << 32) | row[rp + 1]) << (off & 31);
-    int nb = 64 - int(off & 31);
-    rp += 2;
-    uint32_t nextw = row[rp];
-    uint32_t consumed = W.start;
+    BitRow R;
+    R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
     const uint32_t sbits = S.bits;
-    const int bpm = int(S.bpm);
-    int k = 0, bi = 0;
-    uint32_t actab = (acp & 7u) * uint32_t(kLutWords);
-    uint32_t tab = (dcp & 7u) * uint32_t(kLutWords);
+    const uint32_t bpm3 = 3u * S.bpm;
+    const uint32_t lbase = lds_addr(s_lutw);
+    const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
+    uint32_t z = 0, b3 = 0, tab = tab_dc0;
     uint32_t counting = (W.warm_to == W.start) ? 1u : 0u;
     uint32_t mcus = 0, ents = 0, ents0 = 0, m_start = counting ? W.start : kNoPiece, m_end = W.start;
-    uint32_t errs = 0;  // bit 16: a bad code since counting began
+    uint32_t errs = 0;  // kEntBad: a bad code since counting began
     bool active = active_in;
     if (counting && W.start + 8 > sbits) active = false;  // starts at the data end: empty
     next_cp = W.start + cp_bits;
@@ -699,30 +676,23 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
         u32x4 nx[kWinLoads];
 #pragma unroll
         for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
-        while (active && rp <= kWinAdv / 4) {
-            const uint32_t peek = uint32_t(bb >> 32);
-            uint32_t e = s_lutw[tab + (peek >> (32 - kLutBits))];
-            if ((e & 31u) == 0) e = huff_slow(s_lutw + tab, peek, k == 0);  // 0.3 % of symbols
+        while (active && R.rp <= kWinAdv / 4) {
+            const uint32_t peek = R.peek();
+            uint32_t e = lut_fast(tab, peek);
+            if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
             errs |= e;
-            const uint32_t L = e & 31u;
-            bb <<= L;
-            nb -= int(L);
-            const bool need = nb < 32;
-            bb |= need ? (uint64_t(nextw) << (32 - nb)) : 0ull;
-            nb += need ? 32 : 0;
-            rp += need ? 1 : 0;
-            nextw = row[rp];
-            consumed += L;
-            // EOB / ZRL / run-size (parser.cpp:114-134); DC entries have run 0, no EOB/emit bits
-            const int knew = k + int(__builtin_amdgcn_ubfe(e, 5u, 4u));
-            const bool fin = k != 0 && ((e & 512u) != 0 || knew >= 63);
-            ents += ((e & 1024u) != 0 && knew < 64) ? 1u : 0u;
-            const int nbi = (bi + 1 == bpm) ? 0 : bi + 1;
-            bi = fin ? nbi : bi;
-            actab = fin ? __builtin_amdgcn_ubfe(acp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
-            tab = fin ? __builtin_amdgcn_ubfe(dcp, uint32_t(3 * nbi), 3u) * uint32_t(kLutWords) : actab;
-            k = fin ? 0 : knew + 1;
-            if (fin && nbi == 0) {  // an MCU ends here
+            R.skip(e & 31u, row);
+            // EOB / ZRL / run-size (parser.cpp:114-134)
+            const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+            const bool fin = zn >= 63u;
+            ents += __builtin_amdgcn_ubfe(e & ~zn, 6u, 1u);  // emit flag, unless past index 63
+            z = fin ? 0u : zn;
+            b3 += fin ? 3u : 0u;
+            tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
+            if (b3 == bpm3) {  // an MCU ends here
+                b3 = 0;
+                tab = tab_dc0;
+                const uint32_t consumed = R.bit();
                 const bool at_end = consumed + 8 > sbits;
                 if (!counting) {
                     if (consumed >= W.warm_to) {  // synchronised: the piece starts here
@@ -742,7 +712,7 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
                         m_end = consumed;
                         active = false;
                     } else if (KIND == kScanSpec && consumed >= next_cp && ncp < uint32_t(kCpMax)) {
-                        cp[ncp] = CpRec{consumed, mcus, ents - ents0, (errs >> 16) & 1u};
+                        cp[ncp] = CpRec{consumed, mcus, ents - ents0, (errs & kEntBad) ? 1u : 0u};
                         ncp++;
                         next_cp = consumed + cp_bits;
                     } else if (KIND == kScanJoin) {
@@ -758,24 +728,19 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
                 }
             }
         }
-        if (active && consumed > sbits) {  // past the data
-            m_end = consumed;
-            if (counting) errs |= 1u << 16;
+        if (active && R.bit() > sbits) {  // past the data
+            m_end = R.bit();
+            if (counting) errs |= kEntBad;
             active = false;
         }
         if (__ballot(active) == 0) break;  // wave-uniform
 #pragma unroll
-        for (int q = 0; q < kWinLoads; q++) {
-            row[4 * q + 0] = __builtin_bswap32(nx[q].x);
-            row[4 * q + 1] = __builtin_bswap32(nx[q].y);
-            row[4 * q + 2] = __builtin_bswap32(nx[q].z);
-            row[4 * q + 3] = __builtin_bswap32(nx[q].w);
-        }
-        rp -= kWinAdv / 4;
+        for (int q = 0; q < kWinLoads; q++) JD_ROW_FILL(row, nx[q], q);
+        R.next_window();
         wa = na;
     }
-    W.end = consumed;
-    W.bad = counting && ((errs >> 16) & 1u);
+    W.end = R.bit();
+    W.bad = counting && (errs & kEntBad);
     W.m_start = m_start;
     W.m_end = m_end;
     W.mcus = mcus;
@@ -859,7 +824,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
         walk_scan<kScanSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
                              valid, W, cp, b.piece_bits / kCpMax);
     else
-        walk<kWalkWrite>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
+        walk_write(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
     if (!valid) return;
     if (MODE == kWalkScan) {
         // piece 0 starts at bit 0 whatever its walk found (it is the true state)

@@ -170,6 +170,7 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
         code <<= 1;
     }
     lut->lim[17] = 0xFFFFFFFFu;  // sentinel: unmatched 16-bit prefix -> corrupt
+    lut->lim[19] = is_dc ? 1u : 0u;
     for (int i = 0; i < h.nvals; i++) lut->vals[i] = h.vals[i];
     for (int i = 0; i < k; i++) {
         const int l = lens[i];
