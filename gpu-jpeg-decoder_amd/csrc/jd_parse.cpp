@@ -8,6 +8,8 @@
 // what the GPU path does not implement with JD_ERR_UNSUPPORTED instead of decoding garbage.
 #include "jd_parse.hpp"
 
+#include <algorithm>
+
 #include <string.h>
 
 namespace jd {
@@ -184,13 +186,23 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
 }
 
 uint64_t hash_huff(const HuffSpec& h, bool is_dc) {
-    uint64_t x = 1469598103934665603ull ^ (is_dc ? 0x9e3779b97f4a7c15ull : 0);
-    auto mix = [&](uint8_t b) {
-        x ^= b;
-        x *= 1099511628211ull;
+    // 8 bytes per round (tables are hashed per image per call: this runs in the parse workers)
+    uint64_t x = 0x9e3779b97f4a7c15ull ^ (is_dc ? 1u : 2u) ^ (uint64_t(h.nvals) << 8);
+    auto mix = [&](uint64_t w) {
+        x ^= w;
+        x *= 0xff51afd7ed558ccdull;
+        x ^= x >> 32;
     };
-    for (int l = 1; l <= 16; l++) mix(h.counts[l]);
-    for (int i = 0; i < h.nvals; i++) mix(h.vals[i]);
+    uint64_t w[2];
+    memcpy(w, h.counts + 1, 16);
+    mix(w[0]);
+    mix(w[1]);
+    const int n = h.nvals;
+    for (int i = 0; i < n; i += 8) {
+        uint64_t v = 0;
+        memcpy(&v, h.vals + i, size_t(std::min(8, n - i)));
+        mix(v);
+    }
     return x;
 }
 

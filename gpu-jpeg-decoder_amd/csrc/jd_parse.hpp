@@ -22,6 +22,7 @@ struct ParsedJpeg {
     HuffSpec dc[4], ac[4];
     uint16_t q[4][64] = {};      // zig-zag order, as stored in DQT
     bool qp[4] = {};
+    uint64_t hdc[4] = {}, hac[4] = {};  // hash_huff of each component's DC / AC table (parse workers)
 };
 
 // Walks SOI .. SOS.  Replaces the reference's extract() marker loop

@@ -7,9 +7,16 @@
 // (cuda-decoder/benchmark_thoughput/benchmark.cu:49-93) which cudaMalloc'ed every image.
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
+#include <chrono>
+#include <cstdlib>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <array>
 #include <map>
 #include <string>
@@ -44,6 +51,67 @@ struct CachedLut {
     bool is_dc;
 };
 
+// Persistent host workers for the per-image header work (a thread spawn per call would cost more
+// than the parsing): run(n, fn) calls fn(0..n-1) across the workers and the caller.
+class Pool {
+   public:
+    explicit Pool(int nworkers) {
+        for (int i = 0; i < nworkers; i++) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(int n, const std::function<void(int)>& fn) {
+        if (th_.empty() || n <= 1) {
+            for (int i = 0; i < n; i++) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> l(m_);
+            fn_ = &fn;
+            n_ = n;
+            next_ = 0;
+            active_ = int(th_.size());
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [&] { return active_ == 0; });
+    }
+
+   private:
+    void work() {
+        for (int i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> l(m_);
+        while (true) {
+            cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            l.unlock();
+            work();
+            l.lock();
+            if (--active_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int n_ = 0, active_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 }  // namespace
 
 struct jd_ctx {
@@ -51,6 +119,8 @@ struct jd_ctx {
     hipStream_t stream = nullptr;
     unsigned flags = 0;
     int parse_threads = 1;
+    std::unique_ptr<Pool> pool;  // parse_threads - 1 workers
+    bool host_timing = false;  // JD_HOST_TIMING=1: per-batch host phase times on stderr
     std::string last_error;
 
     // Huffman LUT cache (content-addressed, grows across calls)
@@ -110,8 +180,7 @@ hipError_t ensure_pin(PinBuf& b, size_t bytes) {
     return e;
 }
 
-int lut_id(jd_ctx* ctx, const HuffSpec& s, bool is_dc) {
-    const uint64_t h = hash_huff(s, is_dc);
+int lut_id(jd_ctx* ctx, const HuffSpec& s, bool is_dc, uint64_t h) {
     auto range = ctx->lut_by_hash.equal_range(h);
     for (auto it = range.first; it != range.second; ++it) {
         const CachedLut& c = ctx->lut_specs[size_t(it->second)];
@@ -141,21 +210,18 @@ jd_status sync_luts(jd_ctx* ctx) {
 void parse_all(jd_ctx* ctx, const jd_item* items, int n) {
     ctx->parsed.resize(size_t(n));
     ctx->pst.resize(size_t(n));
-    auto work = [&](int lo, int hi) {
-        for (int i = lo; i < hi; i++) ctx->pst[i] = parse_jpeg(items[i].jpeg, items[i].len, &ctx->parsed[i]);
-    };
-    int nt = std::min(ctx->parse_threads, std::max(1, n / 32));
-    if (nt <= 1) {
-        work(0, n);
-        return;
-    }
-    std::vector<std::thread> th;
-    const int per = (n + nt - 1) / nt;
-    for (int t = 0; t < nt; t++) {
-        const int lo = t * per, hi = std::min(n, lo + per);
-        if (lo < hi) th.emplace_back(work, lo, hi);
-    }
-    for (auto& t : th) t.join();
+    constexpr int kPer = 16;  // images per work item
+    ctx->pool->run((n + kPer - 1) / kPer, [&](int t) {
+        for (int i = t * kPer; i < std::min(n, (t + 1) * kPer); i++) {
+            ParsedJpeg& pj = ctx->parsed[i];
+            ctx->pst[i] = parse_jpeg(items[i].jpeg, items[i].len, &pj);
+            if (ctx->pst[i] != JD_OK) continue;
+            for (int c = 0; c < pj.hdr.ncomp; c++) {
+                pj.hdc[c] = hash_huff(pj.dc[pj.td[c]], true);
+                pj.hac[c] = hash_huff(pj.ac[pj.ta[c]], false);
+            }
+        }
+    });
 }
 
 struct Plan {
@@ -187,28 +253,49 @@ int batch_split(jd_ctx* ctx, int lo, int n) {
 
 jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const std::vector<uint64_t>& dev_addr,
                      const std::vector<uint64_t>& out_addr, Plan& P) {
+    const auto tb0 = std::chrono::steady_clock::now();
+    auto tbms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(); };
     std::map<std::array<int, 7>, int> ts_index;
     std::map<std::array<uint16_t, 64>, int> q_index;
     std::vector<int> ts_of_img;
+    // images of one encoder repeat their tables: the previous image's lookups are tried first
+    const ParsedJpeg* prev = nullptr;
+    int prev_ts = -1;
+    std::array<int, 7> prev_key{};
+    uint16_t prev_qslot[3] = {0, 0, 0};
     for (int it = lo; it < hi; it++) {
         if (ctx->pst[it] != JD_OK) continue;
         const ParsedJpeg& pj = ctx->parsed[it];
         const jd_header& h = pj.hdr;
+        bool same_tables = prev && prev->hdr.ncomp == h.ncomp;
+        for (int c = 0; same_tables && c < h.ncomp; c++) {
+            const HuffSpec &d0 = pj.dc[pj.td[c]], &d1 = prev->dc[prev->td[c]];
+            const HuffSpec &a0 = pj.ac[pj.ta[c]], &a1 = prev->ac[prev->ta[c]];
+            same_tables = pj.hdc[c] == prev->hdc[c] && pj.hac[c] == prev->hac[c] && d0.nvals == d1.nvals &&
+                          a0.nvals == a1.nvals && !memcmp(d0.counts, d1.counts, 17) && !memcmp(a0.counts, a1.counts, 17) &&
+                          !memcmp(d0.vals, d1.vals, d0.nvals) && !memcmp(a0.vals, a1.vals, a0.nvals);
+        }
         std::array<int, 7> key{};
-        key[0] = h.ncomp;
-        bool ok = true;
-        for (int c = 0; c < h.ncomp; c++) {
-            key[1 + c] = lut_id(ctx, pj.dc[pj.td[c]], true);
-            key[4 + c] = lut_id(ctx, pj.ac[pj.ta[c]], false);
-            if (key[1 + c] < 0 || key[4 + c] < 0) ok = false;
-        }
-        if (!ok) {
-            ctx->pst[it] = JD_ERR_CORRUPT;
-            continue;
-        }
-        auto f = ts_index.find(key);
         int ts;
-        if (f == ts_index.end()) {
+        if (same_tables) {
+            key = prev_key;
+            ts = prev_ts;
+        } else {
+            key[0] = h.ncomp;
+            bool ok = true;
+            for (int c = 0; c < h.ncomp; c++) {
+                key[1 + c] = lut_id(ctx, pj.dc[pj.td[c]], true, pj.hdc[c]);
+                key[4 + c] = lut_id(ctx, pj.ac[pj.ta[c]], false, pj.hac[c]);
+                if (key[1 + c] < 0 || key[4 + c] < 0) ok = false;
+            }
+            if (!ok) {
+                ctx->pst[it] = JD_ERR_CORRUPT;
+                continue;
+            }
+            ts = -1;
+        }
+        auto f = ts < 0 ? ts_index.find(key) : ts_index.end();
+        if (ts < 0 && f == ts_index.end()) {
             TableSet t;
             for (int s = 0; s < kSlotsPerSet; s++) t.lut[s] = -1;
             memset(t.dc_slot, 0, sizeof(t.dc_slot));
@@ -229,7 +316,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             ts = int(P.tablesets.size());
             P.tablesets.push_back(t);
             ts_index.emplace(key, ts);
-        } else {
+        } else if (ts < 0) {
             ts = f->second;
         }
         ImgDesc d;
@@ -252,6 +339,10 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             d.v[c] = uint8_t(h.v[c]);
             d.comp_block0[c] = uint8_t(b);
             for (int j = 0; j < h.h[c] * h.v[c]; j++, b++) pat |= uint32_t(c) << (2 * b);
+            if (prev && c < prev->hdr.ncomp && !memcmp(pj.q[h.tq[c]], prev->q[prev->hdr.tq[c]], 128)) {
+                d.qslot[c] = prev_qslot[c];
+                continue;
+            }
             std::array<uint16_t, 64> q;
             memcpy(q.data(), pj.q[h.tq[c]], sizeof(q));
             auto fq = q_index.find(q);
@@ -265,6 +356,10 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             }
             d.qslot[c] = uint16_t(qi);
         }
+        for (int c = 0; c < h.ncomp && c < 3; c++) prev_qslot[c] = d.qslot[c];
+        prev = &pj;
+        prev_key = key;
+        prev_ts = ts;
         d.block_pattern = pat;
         d.restart_interval = uint32_t(h.restart_interval);
         const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
@@ -314,6 +409,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         P.item_of_img.push_back(it);
         ts_of_img.push_back(ts);
     }
+    const double tb_imgs = tbms();
     // segments in image order; subsequence ranges grouped by table set, so each decode workgroup
     // (kHuffThreads subsequences) sees exactly one table set
     uint64_t entry_cursor = 0;
@@ -329,6 +425,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             entry_cursor += uint64_t(m1 - m0) * (d.bpm * 63 + 3);  // + alignment of piece starts
         }
     }
+    const double tb_segs = tbms();
     std::vector<uint32_t> order(P.imgs.size());
     for (size_t i = 0; i < order.size(); i++) order[i] = uint32_t(i);
     std::stable_sort(order.begin(), order.end(),
@@ -351,6 +448,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         while (P.chain_seg.size() % kPieceThreads) P.chain_seg.push_back(kInvalidImage);
         while (P.chain_wg_tableset.size() < P.chain_seg.size() / kPieceThreads) P.chain_wg_tableset.push_back(uint32_t(ts));
     }
+    if (ctx->host_timing) std::fprintf(stderr, "plan imgs %.3f segs %.3f pieces %.3f ms\n", tb_imgs, tb_segs - tb_imgs, tbms() - tb_segs);
     if (sub > 0x7FFFFFFFull) return JD_ERR_CAPACITY;
     P.nsub = uint32_t(sub);
     if (entry_cursor > 0xFFFFFFFFull) return JD_ERR_CAPACITY;
@@ -412,8 +510,11 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
     }
 
     // 2. plan
+    const auto tp0 = std::chrono::steady_clock::now();
+    auto tms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count(); };
     Plan P;
     jd_status st = build_plan(ctx, items, lo, hi, dev_addr, out_addr, P);
+    const double t_plan = tms();
     if (st != JD_OK) return st;
     st = sync_luts(ctx);
     if (st != JD_OK) return st;
@@ -506,16 +607,28 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         ctx->last_blocks = P.total_blocks;
         ctx->last_entries = P.total_entry_cap;
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
+        const double t_upload = tms();
+        double t_k[JD_NUM_KERNELS];
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
             if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][0], s));
             HIPCHK(ctx, launch_kernel(k, b, s));
             if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][1], s));
+            t_k[k] = tms();
+        }
+        if (ctx->host_timing) {
+            std::fprintf(stderr, "host launch returns:");
+            for (int k = 0; k < JD_NUM_KERNELS; k++) std::fprintf(stderr, " %.3f", t_k[k]);
+            std::fprintf(stderr, "\n");
         }
         std::vector<uint32_t> status(nimg);
         unsigned long long ctr[2] = {0, 0};
         HIPCHK(ctx, hipMemcpyAsync(status.data(), b.status, nimg * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipMemcpyAsync(ctr, b.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
+        const double t_launch = tms();
         HIPCHK(ctx, hipStreamSynchronize(s));
+        if (ctx->host_timing)
+            std::fprintf(stderr, "host plan %.3f upload %.3f launch %.3f sync %.3f ms\n", t_plan, t_upload - t_plan,
+                         t_launch - t_upload, tms() - t_launch);
         for (uint32_t i = 0; i < nimg; i++)
             if (status[i]) ctx->pst[P.item_of_img[i]] = JD_ERR_CORRUPT;
 
@@ -612,6 +725,8 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     int pt = opts ? opts->parse_threads : 0;
     if (pt <= 0) pt = int(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
     ctx->parse_threads = pt;
+    ctx->pool.reset(new Pool(pt - 1));
+    ctx->host_timing = std::getenv("JD_HOST_TIMING") != nullptr;
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return JD_ERR_HIP;
@@ -658,7 +773,11 @@ jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* r
         if (!items[i].jpeg || items[i].len > 0xFFFFFFF0ull) return JD_ERR_INVALID_ARG;
     if (hipSetDevice(ctx->device) != hipSuccess) return JD_ERR_HIP;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    const auto t0 = std::chrono::steady_clock::now();
     parse_all(ctx, items, n);
+    if (ctx->host_timing)
+        std::fprintf(stderr, "host parse %.3f ms\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     for (int lo = 0; lo < n;) {
         const int hi = batch_split(ctx, lo, n);
         jd_status st = run_batch(ctx, items, lo, hi, results, rgb_on_device, s);
