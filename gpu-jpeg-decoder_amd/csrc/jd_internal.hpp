@@ -125,8 +125,14 @@ constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
 // Stage 3; reference: parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208).  4:2:0 MCU
 // phase needs a few thousand bits to lock: speculative starts failed 45 % / 12 % / 0 % of the
 // time at 1024 / 2048 / 4096 bits on the bench images (tools/jd_trace.py emulate()).
-constexpr uint32_t kPieceBits = 8192;
-constexpr uint32_t kPieceOverlap = 4096;
+#ifndef JD_PIECE_BITS
+#define JD_PIECE_BITS 8192
+#endif
+#ifndef JD_PIECE_OVERLAP
+#define JD_PIECE_OVERLAP 4096
+#endif
+constexpr uint32_t kPieceBits = JD_PIECE_BITS;
+constexpr uint32_t kPieceOverlap = JD_PIECE_OVERLAP;
 constexpr int kPieceThreads = 256;  // one workgroup shares one copy of its table set in LDS
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.

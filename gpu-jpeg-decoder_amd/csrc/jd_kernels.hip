@@ -21,7 +21,8 @@
 namespace jd {
 
 // zig-zag index -> natural (row-major) position: inverse of src/idct.cpp:8-16.
-__constant__ uint8_t kNatOfZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
+// constexpr: fully unrolled loops index it at compile time (register naming, no lookups)
+constexpr uint8_t kNatOfZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
                                      11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20,
                                      13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43,
                                      36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45,
@@ -1121,13 +1122,19 @@ struct ChromaTerms {
     int r, b, g;
     bool exact;
 };
+// The three floors in float (full-rate conversions and multiplies instead of 32-bit mul_hi):
+// R and B as floor((2m + 1) / 2000) with m < 2^20, at least 1/4000 from an integer, where the
+// float error is < 1.1e-7 relative; G's quotient from float(n) / 587000 (|n| < 2^28, error
+// < 5e-5), its remainder exact in integers.  Equal to the integer definition above for every
+// (cb, cr) in [-256, 255]^2 (tests/test_oracle.py::test_chroma_terms_float_exhaustive, and the
+// GPU's all-2^27 test_color_exhaustive).
 __device__ __forceinline__ ChromaTerms chroma_terms(int cb, int cr) {
     ChromaTerms t;
-    t.r = int(uint32_t(1402 * cr + 1000 * 359) / 1000u) - 359 + 128;
-    t.b = int(uint32_t(1772 * cb + 1000 * 454) / 1000u) - 454 + 128;
-    const int n = 202008 * cb + 419198 * cr;
-    const int q = int(uint32_t(n + 587000 * 512) / 587000u) - 512;
-    const int rem = n - q * 587000;
+    t.r = int(floorf(float(__mul24(cr, 2804) + 718001) * 0.0005f)) - 359 + 128;
+    t.b = int(floorf(float(__mul24(cb, 3544) + 908001) * 0.0005f)) - 454 + 128;
+    const int n = __mul24(cb, 202008) + __mul24(cr, 419198);
+    const int q = int(floorf(float(n) * (1.0f / 587000.0f)));
+    const int rem = n - __mul24(q, 587000);
     t.exact = n != 0 && (rem < 64 || rem > 587000 - 64);
     t.g = n == 0 ? 128 : 127 - q;
     return t;
@@ -1195,6 +1202,61 @@ __device__ __forceinline__ void colour8(const int (&Yv)[8], const int16_t* s_pl,
     }
 }
 
+// 8 RGB pixels -> 24 bytes in 6 words (byte k of the group = word k / 4, bits 8 (k % 4)).
+__device__ __forceinline__ void pack24(const uint32_t (&rgb)[8][3], uint32_t (&w)[6]) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const int k = 4 * q;
+        w[q] = rgb[k / 3][k % 3] | (rgb[(k + 1) / 3][(k + 1) % 3] << 8) | (rgb[(k + 2) / 3][(k + 2) % 3] << 16) |
+               (rgb[(k + 3) / 3][(k + 3) % 3] << 24);
+    }
+}
+
+// n <= 8 pixels (24 bytes when n == 8) of a row: 8-byte stores when aligned, else words/bytes
+__device__ __forceinline__ void store24(uint8_t* dst, const uint32_t (&w)[6], uint32_t n) {
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
+    if (n == 8 && (ad & 3) == 0) {
+        if ((ad & 7) == 0) {
+            uint2* d2 = reinterpret_cast<uint2*>(dst);
+            d2[0] = make_uint2(w[0], w[1]);
+            d2[1] = make_uint2(w[2], w[3]);
+            d2[2] = make_uint2(w[4], w[5]);
+        } else {
+            uint32_t* d1 = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+            for (int q = 0; q < 6; q++) d1[q] = w[q];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 24; k++)
+            if (uint32_t(k) < 3 * n) dst[k] = uint8_t(w[k / 4] >> (8 * (k % 4)));
+    }
+}
+
+// Two rows of 8 pixels sharing their chroma samples (vertically subsampled chroma): the chroma
+// terms are computed once for both rows.
+template <int SH>
+__device__ __forceinline__ void colour16(const int (&Y0)[8], const int (&Y1)[8], const int16_t* s_pl, uint32_t cboff,
+                                         uint32_t croff, uint32_t (&w0)[6], uint32_t (&w1)[6]) {
+    constexpr int NU = 8 >> SH;
+    int cb[8], cr[8];
+    load_plane<SH>(s_pl, cboff, cb);
+    load_plane<SH>(s_pl, croff, cr);
+    uint32_t a[8][3], c[8][3];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const ChromaTerms t = chroma_terms(cb[u], cr[u]);
+#pragma unroll
+        for (int r = 0; r < (1 << SH); r++) {
+            const int j = (u << SH) + r;
+            colour_px(Y0[j], cb[u], cr[u], t, a[j][0], a[j][1], a[j][2]);
+            colour_px(Y1[j], cb[u], cr[u], t, c[j][0], c[j][1], c[j][2]);
+        }
+    }
+    pack24(a, w0);
+    pack24(c, w1);
+}
+
 // One wave per tile of tile_mcus x tile_mrows MCUs (host-chosen, <= 64 blocks):
 //  1. lane j owns block j: its LDS row (pitch 65 words) is filled with the block's DC and AC
 //     entries, dequantised in zig-zag order (parser.cpp:111,130) and placed at natural positions
@@ -1232,8 +1294,7 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     // staging (64 rows of 66 int16 = 33 words: odd pitch, conflict-free read-back) and then the
     // component planes share s_buf; planes need at most 64*64 + 64*2*6 int16 (§ host tile choice)
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[2464];
-    __shared__ int s_qn[3 * 65];  // quant step per component, natural order (pitch 65: no bank clash)
-    __shared__ uint8_t s_nat[64];  // zig-zag -> natural
+    __shared__ int s_qz[3 * 65];  // quant step per component, zig-zag order (pitch 65: no bank clash)
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t tile = blockIdx.x;
     const uint32_t tiles_x = im.tiles_x;
@@ -1243,18 +1304,17 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     const uint32_t TM = im.tile_mcus, TR = im.tile_mrows, bpm = im.bpm, nc = im.ncomp;
     const uint32_t m0 = tx * TM, r0 = ty * TR;
     const uint32_t nm = min(TM, im.mcux - m0), nr = min(TR, im.mcuy - r0);
-    s_nat[lane] = kNatOfZz[lane];
     for (uint32_t i = lane; i < nc * 64; i += kIdctThreads) {
         const uint32_t c = i >> 6, z = i & 63u;
-        s_qn[c * 65 + kNatOfZz[z]] = int(b.qtabs[size_t(im.qslot[c]) * 64 + z]);
+        s_qz[c * 65 + z] = int(b.qtabs[size_t(im.qslot[c]) * 64 + z]);
     }
     constexpr int kRow16 = 33;  // words per staging row
     uint4* z4 = reinterpret_cast<uint4*>(s_buf);
     for (uint32_t i = lane; i < (64 * kRow16 + 3) / 4; i += kIdctThreads) z4[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
 
-    // 1. sparse -> dense (my block): quantised coefficients, natural order (parser.cpp:111,130:
-    //    the dequantisation happens on read-back, in zig-zag correspondence)
+    // 1. sparse -> dense (my block): quantised coefficients at their zig-zag positions
+    //    (parser.cpp:111,130: the dequantisation happens on read-back, in zig-zag correspondence)
     const uint32_t m = lane / bpm, bb = lane - m * bpm;
     const uint32_t mr = m / TM, mi = m - mr * TM;
     const bool have = mr < nr && mi < nm;
@@ -1282,23 +1342,24 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int i = 4 * (c + u) + q - int(lead);
-                    if (i >= 0 && i < cnt) row[s_nat[w[q] & 63u]] = int16_t(w[q] >> 16);
+                    if (i >= 0 && i < cnt) row[w[q] & 63u] = int16_t(w[q] >> 16);
                 }
             }
         }
     }
     __syncthreads();
 
-    // 2. dequantise (24-bit multiplies: |coef| < 2^15, q < 2^16) and IDCT in registers
+    // 2. dequantise in zig-zag order (24-bit multiplies: |coef| < 2^15, q < 2^16) into natural
+    //    positions (a compile-time permutation of registers), then the IDCT in registers
     int blk[64];
     {
         const uint32_t* rw = s_buf + lane * kRow16;
-        const int* qn = s_qn + comp * 65;
+        const int* qz = s_qz + comp * 65;
 #pragma unroll
         for (int p = 0; p < 32; p++) {
             const uint32_t w = rw[p];
-            blk[2 * p] = __mul24(int(int16_t(w & 0xFFFFu)), qn[2 * p]);
-            blk[2 * p + 1] = __mul24(int32_t(w) >> 16, qn[2 * p + 1]);
+            blk[kNatOfZz[2 * p]] = __mul24(int(int16_t(w & 0xFFFFu)), qz[2 * p]);
+            blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, qz[2 * p + 1]);
         }
     }
 #pragma unroll
@@ -1340,7 +1401,8 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     }
     __syncthreads();
 
-    // 4. upsample + colour, 8 pixels per lane
+    // 4. upsample + colour: 8 pixels of one row per lane-step, or of two rows when both chroma
+    //    planes are vertically subsampled (the two rows share their chroma samples and terms)
     const uint32_t lg_mw = im.lg_mw, lg_mh = im.lg_mh;
     const uint32_t gpr = (TM << lg_mw) >> 3;  // 8-pixel groups per tile row
     const uint32_t th = TR << lg_mh;
@@ -1348,61 +1410,48 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     const uint32_t x_tile = m0 << lg_mw, y_tile = r0 << lg_mh;
     const uint32_t shx1 = im.shx[1], shy1 = im.shy[1], shx2 = im.shx[2], shy2 = im.shy[2];
     const uint32_t cmode = nc == 1 ? 3u : (shx1 == shx2 ? shx1 : 4u);
+    const bool pair = cmode <= 2u && shy1 >= 1u && shy2 >= 1u;  // wave-uniform; th is even then
+    const uint32_t rows = pair ? 2u : 1u, ngy = th / rows;
     uint8_t* out = reinterpret_cast<uint8_t*>(im.rgb);
-    for (uint32_t it = lane; it < th * gpr; it += kIdctThreads) {
-        const uint32_t py = it / gpr, gx = (it - py * gpr) << 3;
+    // lane -> (row group gy, column group gc), advanced by 64 groups per iteration
+    const uint32_t step_y = kIdctThreads / gpr, step_c = kIdctThreads - step_y * gpr;
+    uint32_t gy = lane / gpr, gc = lane - gy * gpr;
+    for (; gy < ngy; gy += step_y + (gc + step_c >= gpr ? 1u : 0u), gc = gc + step_c >= gpr ? gc + step_c - gpr : gc + step_c) {
+        const uint32_t py = gy * rows, gx = gc << 3;
         const uint32_t y = y_tile + py, x = x_tile + gx;
         if (y >= H || x >= W) continue;
-        int Yv[8];
-        load_plane<0>(s_pl, pbase[0] + py * ppitch[0] + gx, Yv);
+        int Y0[8], Y1[8];
+        load_plane<0>(s_pl, pbase[0] + py * ppitch[0] + gx, Y0);
+        if (pair) load_plane<0>(s_pl, pbase[0] + (py + 1) * ppitch[0] + gx, Y1);
         const uint32_t cboff = pbase[1] + (py >> shy1) * ppitch[1] + (gx >> shx1);
         const uint32_t croff = pbase[2] + (py >> shy2) * ppitch[2] + (gx >> shx2);
-        uint32_t rgb[8][3];
-        switch (cmode) {  // wave-uniform
-            case 0: colour8<0>(Yv, s_pl, cboff, croff, rgb); break;
-            case 1: colour8<1>(Yv, s_pl, cboff, croff, rgb); break;
-            case 2: colour8<2>(Yv, s_pl, cboff, croff, rgb); break;
-            case 3: colour8<3>(Yv, s_pl, cboff, croff, rgb); break;
-            default: {  // chroma planes with different horizontal factors
-                int Cb[8], Cr[8];
-                load8_samples(s_pl, cboff, shx1, Cb);
-                load8_samples(s_pl, croff, shx2, Cr);
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    colour_px(Yv[j], Cb[j], Cr[j], chroma_terms(Cb[j], Cr[j]), rgb[j][0], rgb[j][1], rgb[j][2]);
-            }
-        }
-        uint8_t* dst = out + (size_t(y) * W + x) * 3;
-        const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
-        if (x + 8 <= W && (ad & 3) == 0) {
-            uint32_t w[6];
-#pragma unroll
-            for (int q = 0; q < 6; q++) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) v |= rgb[(4 * q + k) / 3][(4 * q + k) % 3] << (8 * k);
-                w[q] = v;
-            }
-            if ((ad & 7) == 0) {
-                uint2* d2 = reinterpret_cast<uint2*>(dst);
-                d2[0] = make_uint2(w[0], w[1]);
-                d2[1] = make_uint2(w[2], w[3]);
-                d2[2] = make_uint2(w[4], w[5]);
-            } else {
-                uint32_t* d1 = reinterpret_cast<uint32_t*>(dst);
-#pragma unroll
-                for (int q = 0; q < 6; q++) d1[q] = w[q];
+        uint32_t w0[6], w1[6];
+        if (pair) {
+            switch (cmode) {  // wave-uniform
+                case 0: colour16<0>(Y0, Y1, s_pl, cboff, croff, w0, w1); break;
+                case 1: colour16<1>(Y0, Y1, s_pl, cboff, croff, w0, w1); break;
+                default: colour16<2>(Y0, Y1, s_pl, cboff, croff, w0, w1); break;
             }
         } else {
-            const uint32_t n = min(8u, W - x);
+            uint32_t rgb[8][3];
+            switch (cmode) {  // wave-uniform
+                case 0: colour8<0>(Y0, s_pl, cboff, croff, rgb); break;
+                case 1: colour8<1>(Y0, s_pl, cboff, croff, rgb); break;
+                case 2: colour8<2>(Y0, s_pl, cboff, croff, rgb); break;
+                case 3: colour8<3>(Y0, s_pl, cboff, croff, rgb); break;
+                default: {  // chroma planes with different horizontal factors
+                    int Cb[8], Cr[8];
+                    load8_samples(s_pl, cboff, shx1, Cb);
+                    load8_samples(s_pl, croff, shx2, Cr);
 #pragma unroll
-            for (int j = 0; j < 8; j++)
-                if (uint32_t(j) < n) {
-                    dst[3 * j] = uint8_t(rgb[j][0]);
-                    dst[3 * j + 1] = uint8_t(rgb[j][1]);
-                    dst[3 * j + 2] = uint8_t(rgb[j][2]);
+                    for (int j = 0; j < 8; j++)
+                        colour_px(Y0[j], Cb[j], Cr[j], chroma_terms(Cb[j], Cr[j]), rgb[j][0], rgb[j][1], rgb[j][2]);
                 }
+            }
+            pack24(rgb, w0);
         }
+        store24(out + (size_t(y) * W + x) * 3, w0, min(8u, W - x));
+        if (pair && y + 1 < H) store24(out + (size_t(y + 1) * W + x) * 3, w1, min(8u, W - x));
     }
 }
 
