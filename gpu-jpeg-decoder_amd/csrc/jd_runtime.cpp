@@ -251,18 +251,94 @@ int batch_split(jd_ctx* ctx, int lo, int n) {
     return hi;
 }
 
+// Per image of the plan: what the sequential pass decides (table set, quant slots, bases).
+struct PlanImg {
+    int item, ts;
+    uint16_t qslot[3];
+    uint64_t block_base, entry_base, comp;
+    uint32_t seg_base, nseg, chunk_base, nchunks;
+};
+
+// Fills d (everything but the piece ranges) for item it; pure function of the header + bases.
+void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uint64_t out_addr, const PlanImg& pi,
+               ImgDesc& d) {
+    const jd_header& h = pj.hdr;
+    memset(&d, 0, sizeof(d));
+    d.jpeg = dev_addr;
+    d.rgb = out_addr;
+    d.len = uint32_t(item.len);
+    d.ecs_off = uint32_t(h.ecs_offset);
+    d.width = uint32_t(h.width);
+    d.height = uint32_t(h.height);
+    d.mcux = uint32_t(h.mcux);
+    d.mcuy = uint32_t(h.mcuy);
+    d.ncomp = uint32_t(h.ncomp);
+    d.hmax = uint32_t(h.hmax);
+    d.vmax = uint32_t(h.vmax);
+    d.bpm = uint32_t(h.blocks_per_mcu);
+    uint32_t pat = 0, b = 0;
+    for (int c = 0; c < h.ncomp; c++) {
+        d.h[c] = uint8_t(h.h[c]);
+        d.v[c] = uint8_t(h.v[c]);
+        d.comp_block0[c] = uint8_t(b);
+        for (int j = 0; j < h.h[c] * h.v[c]; j++, b++) pat |= uint32_t(c) << (2 * b);
+        d.qslot[c] = pi.qslot[c];
+    }
+    d.block_pattern = pat;
+    d.restart_interval = uint32_t(h.restart_interval);
+    d.nseg = pi.nseg;
+    d.seg_base = pi.seg_base;
+    d.block_base = pi.block_base;
+    d.tableset = uint32_t(pi.ts);
+    {  // IDCT/colour tiles: one wave, one lane per block: the most blocks <= 64 over 1 or 2 MCU rows
+        uint32_t lw = 0, lh = 0;
+        while ((8u << lw) < 8u * d.hmax) lw++;
+        while ((8u << lh) < 8u * d.vmax) lh++;
+        d.lg_mw = 3 + lw;
+        d.lg_mh = 3 + lh;
+        uint32_t best = 0;
+        for (uint32_t tr = 1; tr <= 2; tr++) {
+            const uint32_t tm = std::max(1u, uint32_t(kTileMaxBlocks) / (tr * d.bpm));
+            if (tm * tr * d.bpm > best) {
+                best = tm * tr * d.bpm;
+                d.tile_mcus = tm;
+                d.tile_mrows = tr;
+            }
+        }
+        d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
+        d.tiles_y = (d.mcuy + d.tile_mrows - 1) / d.tile_mrows;
+        for (int c = 0; c < h.ncomp; c++) {
+            uint32_t sx = 0, sy = 0;
+            while ((uint32_t(h.h[c]) << sx) < d.hmax) sx++;
+            while ((uint32_t(h.v[c]) << sy) < d.vmax) sy++;
+            d.shx[c] = uint8_t(sx);
+            d.shy[c] = uint8_t(sy);
+        }
+    }
+    d.nchunks = pi.nchunks;  // scan chunks over [align16(file + ecs_off), file + len)
+    d.chunk_base = pi.chunk_base;
+    d.comp = pi.comp;  // offset for now; rebased onto the pool in run_batch
+}
+
+// Entry slots per MCU: 63 per block (a block stores at most 63) plus 3 for aligning piece starts
+// to 16-byte quads.
+inline uint64_t entry_slots_per_mcu(uint32_t bpm) { return uint64_t(bpm) * 63 + 3; }
+
 jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const std::vector<uint64_t>& dev_addr,
                      const std::vector<uint64_t>& out_addr, Plan& P) {
     const auto tb0 = std::chrono::steady_clock::now();
     auto tbms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(); };
+    // 1. sequential: table sets and quant tables (de-duplicated across the batch), bases
     std::map<std::array<int, 7>, int> ts_index;
     std::map<std::array<uint16_t, 64>, int> q_index;
-    std::vector<int> ts_of_img;
+    std::vector<PlanImg> pim;
+    pim.reserve(size_t(hi - lo));
     // images of one encoder repeat their tables: the previous image's lookups are tried first
     const ParsedJpeg* prev = nullptr;
     int prev_ts = -1;
-    std::array<int, 7> prev_key{};
     uint16_t prev_qslot[3] = {0, 0, 0};
+    uint64_t block_cursor = 0, entry_cursor = 0, comp_cursor = 0;
+    uint32_t seg_cursor = 0, chunk_cursor = 0;
     for (int it = lo; it < hi; it++) {
         if (ctx->pst[it] != JD_OK) continue;
         const ParsedJpeg& pj = ctx->parsed[it];
@@ -275,12 +351,9 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
                           a0.nvals == a1.nvals && !memcmp(d0.counts, d1.counts, 17) && !memcmp(a0.counts, a1.counts, 17) &&
                           !memcmp(d0.vals, d1.vals, d0.nvals) && !memcmp(a0.vals, a1.vals, a0.nvals);
         }
-        std::array<int, 7> key{};
-        int ts;
-        if (same_tables) {
-            key = prev_key;
-            ts = prev_ts;
-        } else {
+        int ts = same_tables ? prev_ts : -1;
+        if (ts < 0) {
+            std::array<int, 7> key{};
             key[0] = h.ncomp;
             bool ok = true;
             for (int c = 0; c < h.ncomp; c++) {
@@ -292,55 +365,38 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
                 ctx->pst[it] = JD_ERR_CORRUPT;
                 continue;
             }
-            ts = -1;
-        }
-        auto f = ts < 0 ? ts_index.find(key) : ts_index.end();
-        if (ts < 0 && f == ts_index.end()) {
-            TableSet t;
-            for (int s = 0; s < kSlotsPerSet; s++) t.lut[s] = -1;
-            memset(t.dc_slot, 0, sizeof(t.dc_slot));
-            memset(t.ac_slot, 0, sizeof(t.ac_slot));
-            int nslot = 0;
-            auto slot_of = [&](int id) {
-                for (int s = 0; s < nslot; s++)
-                    if (t.lut[s] == id) return s;
-                t.lut[nslot] = id;
-                return nslot++;
-            };
-            for (int c = 0; c < h.ncomp; c++) {
-                t.dc_slot[c] = uint8_t(slot_of(key[1 + c]));
-                t.ac_slot[c] = uint8_t(slot_of(key[4 + c]));
+            auto f = ts_index.find(key);
+            if (f != ts_index.end()) {
+                ts = f->second;
+            } else {
+                TableSet t;
+                for (int s = 0; s < kSlotsPerSet; s++) t.lut[s] = -1;
+                memset(t.dc_slot, 0, sizeof(t.dc_slot));
+                memset(t.ac_slot, 0, sizeof(t.ac_slot));
+                int nslot = 0;
+                auto slot_of = [&](int id) {
+                    for (int s = 0; s < nslot; s++)
+                        if (t.lut[s] == id) return s;
+                    t.lut[nslot] = id;
+                    return nslot++;
+                };
+                for (int c = 0; c < h.ncomp; c++) {
+                    t.dc_slot[c] = uint8_t(slot_of(key[1 + c]));
+                    t.ac_slot[c] = uint8_t(slot_of(key[4 + c]));
+                }
+                t.nslots = nslot;
+                P.max_slots = std::max(P.max_slots, uint32_t(nslot));
+                ts = int(P.tablesets.size());
+                P.tablesets.push_back(t);
+                ts_index.emplace(key, ts);
             }
-            t.nslots = nslot;
-            P.max_slots = std::max(P.max_slots, uint32_t(nslot));
-            ts = int(P.tablesets.size());
-            P.tablesets.push_back(t);
-            ts_index.emplace(key, ts);
-        } else if (ts < 0) {
-            ts = f->second;
         }
-        ImgDesc d;
-        memset(&d, 0, sizeof(d));
-        d.jpeg = dev_addr[it];
-        d.rgb = out_addr[it];
-        d.len = uint32_t(items[it].len);
-        d.ecs_off = uint32_t(h.ecs_offset);
-        d.width = uint32_t(h.width);
-        d.height = uint32_t(h.height);
-        d.mcux = uint32_t(h.mcux);
-        d.mcuy = uint32_t(h.mcuy);
-        d.ncomp = uint32_t(h.ncomp);
-        d.hmax = uint32_t(h.hmax);
-        d.vmax = uint32_t(h.vmax);
-        d.bpm = uint32_t(h.blocks_per_mcu);
-        uint32_t pat = 0, b = 0;
+        PlanImg pi;
+        pi.item = it;
+        pi.ts = ts;
         for (int c = 0; c < h.ncomp; c++) {
-            d.h[c] = uint8_t(h.h[c]);
-            d.v[c] = uint8_t(h.v[c]);
-            d.comp_block0[c] = uint8_t(b);
-            for (int j = 0; j < h.h[c] * h.v[c]; j++, b++) pat |= uint32_t(c) << (2 * b);
             if (prev && c < prev->hdr.ncomp && !memcmp(pj.q[h.tq[c]], prev->q[prev->hdr.tq[c]], 128)) {
-                d.qslot[c] = prev_qslot[c];
+                pi.qslot[c] = prev_qslot[c];
                 continue;
             }
             std::array<uint16_t, 64> q;
@@ -354,89 +410,70 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             } else {
                 qi = fq->second;
             }
-            d.qslot[c] = uint16_t(qi);
+            pi.qslot[c] = uint16_t(qi);
         }
-        for (int c = 0; c < h.ncomp && c < 3; c++) prev_qslot[c] = d.qslot[c];
+        for (int c = 0; c < h.ncomp && c < 3; c++) prev_qslot[c] = pi.qslot[c];
         prev = &pj;
-        prev_key = key;
         prev_ts = ts;
-        d.block_pattern = pat;
-        d.restart_interval = uint32_t(h.restart_interval);
         const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
-        d.nseg = h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
-        d.block_base = P.total_blocks;
-        P.total_blocks += nmcu * uint64_t(h.blocks_per_mcu);
-        d.tableset = uint32_t(ts);
-        {  // IDCT/colour tiles: one wave, one lane per block: the most blocks <= 64 over 1 or 2 MCU rows
-            uint32_t lw = 0, lh = 0;
-            while ((8u << lw) < 8u * d.hmax) lw++;
-            while ((8u << lh) < 8u * d.vmax) lh++;
-            d.lg_mw = 3 + lw;
-            d.lg_mh = 3 + lh;
-            uint32_t best = 0;
-            for (uint32_t tr = 1; tr <= 2; tr++) {
-                const uint32_t tm = std::max(1u, uint32_t(kTileMaxBlocks) / (tr * d.bpm));
-                if (tm * tr * d.bpm > best) {
-                    best = tm * tr * d.bpm;
-                    d.tile_mcus = tm;
-                    d.tile_mrows = tr;
-                }
-            }
-            d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
-            d.tiles_y = (d.mcuy + d.tile_mrows - 1) / d.tile_mrows;
-            for (int c = 0; c < h.ncomp; c++) {
-                uint32_t sx = 0, sy = 0;
-                while ((uint32_t(h.h[c]) << sx) < d.hmax) sx++;
-                while ((uint32_t(h.v[c]) << sy) < d.vmax) sy++;
-                d.shx[c] = uint8_t(sx);
-                d.shy[c] = uint8_t(sy);
-            }
-            P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.tiles_y);
-        }
-        {  // scan chunks over [align16(file + ecs_off), file + len) and the un-stuffed stream
-            const uint64_t a0 = (d.jpeg + d.ecs_off) & ~uint64_t(15);
-            const uint64_t span = d.jpeg + d.len - a0;
-            d.nchunks = uint32_t((span + kScanChunk - 1) / kScanChunk);
-            d.chunk_base = P.total_chunks;
-            P.total_chunks += d.nchunks;
-            P.max_chunks = std::max(P.max_chunks, d.nchunks);
-            d.comp = P.comp_bytes;  // offset for now; rebased onto the pool in run_batch
-            P.comp_bytes += align_up(size_t(d.len - d.ecs_off) + 64, 256);
-        }
+        pi.nseg = h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
+        pi.seg_base = seg_cursor;
+        seg_cursor += pi.nseg;
+        pi.block_base = block_cursor;
+        block_cursor += nmcu * uint64_t(h.blocks_per_mcu);
+        pi.entry_base = entry_cursor;
+        entry_cursor += nmcu * entry_slots_per_mcu(uint32_t(h.blocks_per_mcu));
+        const uint64_t a0 = (dev_addr[it] + uint64_t(h.ecs_offset)) & ~uint64_t(15);
+        pi.nchunks = uint32_t((dev_addr[it] + items[it].len - a0 + kScanChunk - 1) / kScanChunk);
+        pi.chunk_base = chunk_cursor;
+        chunk_cursor += pi.nchunks;
+        pi.comp = comp_cursor;
+        comp_cursor += align_up(size_t(items[it].len - h.ecs_offset) + 64, 256);
+        P.max_chunks = std::max(P.max_chunks, pi.nchunks);
         P.pixels += double(h.width) * h.height;
-        P.ecs_bytes += double(d.len - d.ecs_off);
-        P.imgs.push_back(d);
-        P.item_of_img.push_back(it);
-        ts_of_img.push_back(ts);
+        P.ecs_bytes += double(items[it].len - h.ecs_offset);
+        pim.push_back(pi);
     }
+    P.total_blocks = block_cursor;
+    P.total_chunks = chunk_cursor;
+    P.comp_bytes = comp_cursor;
     const double tb_imgs = tbms();
-    // segments in image order; subsequence ranges grouped by table set, so each decode workgroup
-    // (kHuffThreads subsequences) sees exactly one table set
-    uint64_t entry_cursor = 0;
-    for (size_t i = 0; i < P.imgs.size(); i++) {
-        ImgDesc& d = P.imgs[i];
-        d.seg_base = uint32_t(P.seg_img.size());
-        const uint32_t nmcu = d.mcux * d.mcuy;
-        for (uint32_t k = 0; k < d.nseg; k++) {
-            const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
-            const uint32_t m1 = d.restart_interval ? std::min(m0 + d.restart_interval, nmcu) : nmcu;
-            P.seg_img.push_back(uint32_t(i));
-            P.seg_entry.push_back(uint32_t(entry_cursor));
-            entry_cursor += uint64_t(m1 - m0) * (d.bpm * 63 + 3);  // + alignment of piece starts
+    // 2. parallel: image descriptors and segment lists
+    const size_t nimg = pim.size();
+    P.imgs.resize(nimg);
+    P.item_of_img.resize(nimg);
+    P.seg_img.resize(seg_cursor);
+    P.seg_entry.resize(seg_cursor);
+    constexpr int kPer = 32;
+    ctx->pool->run(int((nimg + kPer - 1) / kPer), [&](int t) {
+        for (size_t i = size_t(t) * kPer; i < std::min(nimg, size_t(t + 1) * kPer); i++) {
+            const PlanImg& pi = pim[i];
+            const ParsedJpeg& pj = ctx->parsed[pi.item];
+            ImgDesc& d = P.imgs[i];
+            fill_desc(pj, items[pi.item], dev_addr[pi.item], out_addr[pi.item], pi, d);
+            P.item_of_img[i] = pi.item;
+            const uint32_t nmcu = d.mcux * d.mcuy;
+            const uint64_t per = entry_slots_per_mcu(d.bpm);
+            for (uint32_t k = 0; k < d.nseg; k++) {
+                const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
+                P.seg_img[d.seg_base + k] = uint32_t(i);
+                P.seg_entry[d.seg_base + k] = uint32_t(pi.entry_base + uint64_t(std::min(m0, nmcu)) * per);
+            }
         }
-    }
+    });
+    for (const ImgDesc& d : P.imgs) P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.tiles_y);
     const double tb_segs = tbms();
-    std::vector<uint32_t> order(P.imgs.size());
-    for (size_t i = 0; i < order.size(); i++) order[i] = uint32_t(i);
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t a, uint32_t b) { return ts_of_img[a] < ts_of_img[b]; });
-    // piece slots: per image ceil(ECS bits / piece_bits) + nseg (interval lengths are only known
+    // 3. piece slots: per image ceil(ECS bits / piece_bits) + nseg (interval lengths are only known
     // on the GPU), grouped by table set so each k_piece workgroup stages one table set
+    std::vector<uint32_t> order(nimg);
+    for (size_t i = 0; i < order.size(); i++) order[i] = uint32_t(i);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return pim[a].ts < pim[b].ts; });
     P.piece_bits = (ctx->flags & JD_FLAG_FORCE_SYNC) ? 1024u : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u : kPieceBits;
     uint64_t sub = 0;
+    P.chain_seg.reserve(seg_cursor + kPieceThreads * P.tablesets.size());
     for (size_t oi = 0; oi < order.size();) {
-        const int ts = ts_of_img[order[oi]];
-        for (; oi < order.size() && ts_of_img[order[oi]] == ts; oi++) {
+        const int ts = pim[order[oi]].ts;
+        for (; oi < order.size() && pim[order[oi]].ts == ts; oi++) {
             ImgDesc& d = P.imgs[order[oi]];
             d.sub_base = uint32_t(sub);
             d.sub_cap = uint32_t((uint64_t(d.len - d.ecs_off) * 8 + P.piece_bits - 1) / P.piece_bits + d.nseg);
@@ -448,7 +485,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         while (P.chain_seg.size() % kPieceThreads) P.chain_seg.push_back(kInvalidImage);
         while (P.chain_wg_tableset.size() < P.chain_seg.size() / kPieceThreads) P.chain_wg_tableset.push_back(uint32_t(ts));
     }
-    if (ctx->host_timing) std::fprintf(stderr, "plan imgs %.3f segs %.3f pieces %.3f ms\n", tb_imgs, tb_segs - tb_imgs, tbms() - tb_segs);
+    if (ctx->host_timing) std::fprintf(stderr, "plan imgs %.3f descs %.3f pieces %.3f ms\n", tb_imgs, tb_segs - tb_imgs, tbms() - tb_segs);
     if (sub > 0x7FFFFFFFull) return JD_ERR_CAPACITY;
     P.nsub = uint32_t(sub);
     if (entry_cursor > 0xFFFFFFFFull) return JD_ERR_CAPACITY;
