@@ -61,6 +61,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_wsum
     return off;
 }
 
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[16], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
+
 // 64 raw bytes of a thread (16B-aligned loads never cross a page; bytes at/after fend read 0).
 __device__ __forceinline__ void load64(uintptr_t t0, uintptr_t fend, uint32_t (&w)[16]) {
 #pragma unroll
@@ -74,8 +76,6 @@ __device__ __forceinline__ void load64(uintptr_t t0, uintptr_t fend, uint32_t (&
         w[4 * q + 3] = v.w;
     }
 }
-
-__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[16], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
 
 // ------------------------------------------------------------------------------------------
 // Stage 0: scan.  In an ECS a data FF is always followed by a stuffed 00, so:
@@ -99,30 +99,36 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
 
     uint32_t ndrop = 0, nbrk = 0;
     if (t0 >= lo && t0 + 64 < fend) {
-        // interior thread: exact per-byte masks (high bit of each byte lane), 16 words at a time
-        //   ff[k]   : byte == 0xFF            zero[k]: byte == 0x00
-        //   drop    : 00 preceded by FF       brk    : FF followed by neither 00 nor FF
-        uint32_t ff[16], nz[16];
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const uint32_t x = w[q], t = ~x;
-            ff[q] = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+        // interior thread: exact per-byte masks (high bit of each byte lane), one word at a time
+        // with the neighbours' masks carried (few live registers: this pass is latency-bound)
+        //   ff   : byte == 0xFF            zero: byte == 0x00
+        //   drop : 00 preceded by FF       brk : FF followed by neither 00 nor FF
+        auto masks = [](uint32_t x, uint32_t& ff, uint32_t& nz) {
+            const uint32_t t = ~x;
+            ff = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
             const uint32_t zero = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-            nz[q] = ~(zero | ff[q]) & 0x80808080u;  // neither 00 nor FF
-        }
-        const uint32_t ffprev = (prevb == 0xFFu) ? 0x80u : 0u;            // byte before the thread
+            nz = ~(zero | ff) & 0x80808080u;  // neither 00 nor FF
+            return zero;
+        };
+        uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;  // only its top byte is used
+        uint32_t ff_cur, nz_cur;
+        uint32_t zero_cur = masks(w[0], ff_cur, nz_cur);
         const uint32_t nznext = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;  // byte after it
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            const uint32_t x = w[q];
-            const uint32_t zero = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-            const uint32_t pf = (ff[q] << 8) | (q ? (ff[q - 1] >> 24) : ffprev);
-            const uint32_t nn = (nz[q] >> 8) | ((q < 15 ? nz[q + 1] : nznext) << 24);
-            ndrop += __builtin_popcount(zero & pf);
-            nbrk += __builtin_popcount(ff[q] & nn);
+            uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = 0;
+            if (q < 15) zero_nx = masks(w[q + 1], ff_nx, nz_nx);
+            const uint32_t pf = (ff_cur << 8) | (ff_prev >> 24);
+            const uint32_t nn = (nz_cur >> 8) | (nz_nx << 24);
+            ndrop += __builtin_popcount(zero_cur & pf);
+            nbrk += __builtin_popcount(ff_cur & nn);
+            ff_prev = ff_cur;
+            ff_cur = ff_nx;
+            nz_cur = nz_nx;
+            zero_cur = zero_nx;
         }
     } else {
-#pragma unroll
+#pragma unroll 1
         for (int i = 0; i < 64; i++) {
             const uint32_t by = byte_of(w, i);
             const uint32_t pb = i ? byte_of(w, i - 1) : prevb;
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     if (nbrk) {
         Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
         uint32_t d = drop_before;
-#pragma unroll
+#pragma unroll 1
         for (int i = 0; i < 64; i++) {
             const uint32_t by = byte_of(w, i);
             const uint32_t pb = i ? byte_of(w, i - 1) : prevb;
@@ -281,9 +287,19 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
     uint32_t total;
     uint32_t off = block_excl_scan(uint32_t(__builtin_popcountll(keep)), s_wsum, &total);
     uint8_t* so = reinterpret_cast<uint8_t*>(s_out);
-    if (keep == ~0ull && (off & 3u) == 0u) {  // common case: whole thread kept, aligned in LDS
+    if (keep == ~0ull) {  // common case: whole thread kept
+        const uint32_t sh = off & 3u, wb = off >> 2;
+        if (sh == 0u) {
 #pragma unroll
-        for (int q = 0; q < 16; q++) s_out[(off >> 2) + q] = w[q];
+            for (int q = 0; q < 16; q++) s_out[wb + q] = w[q];
+        } else {
+            // words wb+1..wb+15 whole (funnel shifts of neighbouring words); the 4 - sh bytes
+            // before them and the sh after them share words with the neighbouring threads
+            for (uint32_t j = 0; j < 4u - sh; j++) so[off + j] = uint8_t(w[0] >> (8 * j));
+#pragma unroll
+            for (int k = 1; k < 16; k++) s_out[wb + k] = __builtin_amdgcn_alignbyte(w[k], w[k - 1], 4u - sh);
+            for (uint32_t j = 0; j < sh; j++) so[off + 64 - sh + j] = uint8_t(w[15] >> (8 * (4 - sh + j)));
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < 64; i++)
@@ -459,6 +475,10 @@ constexpr int kWinAdv = JD_WIN_ADV;               // bytes a round advances
 constexpr int kWinLoads = kWinAdv / 16 + 1;       // 16-byte loads per window (advance + overlap)
 constexpr int kRowWords = 1 + 4 * kWinLoads;      // 21: odd pitch (last word unused)
 static_assert(kRowWords % 2 == 1, "row pitch must be odd");
+#ifndef JD_ABL  // experiment builds: 1 skip colour, 2 skip IDCT math, 4 skip the entry scatter, 8 / 16 skip the
+                // write pass's entry / BlockInfo stores
+#define JD_ABL 0
+#endif
 constexpr int kWalkScan = 0, kWalkWrite = 1;
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 
@@ -565,6 +585,22 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
     uint32_t ent = W.ent0, ent_blk = W.ent0, blk = 0;
     int dcd = 0;
     uint32_t wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;
+    // Stores are deferred and issued every few loop iterations, so that one store instruction
+    // carries many lanes (a wave's store instructions, not its bytes, bound this pass): a lane
+    // completes at most one quad per 4 iterations (one entry per symbol) and one block per 2
+    // (a DC and at least one AC symbol), so one pending quad and one pending block suffice.
+    uint32_t pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0, pent = 0, pbi0 = 0, pbi1 = 0, pblk = 0;
+    bool pend_q = false, pend_b = false;
+#define JD_FLUSH_Q()                                                                              \
+    do {                                                                                          \
+        if (pend_q) *reinterpret_cast<uint4*>(eout + pent - 4u) = make_uint4(pq0, pq1, pq2, pq3); \
+        pend_q = false;                                                                           \
+    } while (0)
+#define JD_FLUSH_B()                                       \
+    do {                                                   \
+        if (pend_b) bout[pblk] = BlockInfo{pbi0, pbi1};    \
+        pend_b = false;                                    \
+    } while (0)
     uint32_t errs = 0;
     bool active = active_in && nblk > 0;
     while (true) {
@@ -572,7 +608,9 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
         u32x4 nx[kWinLoads];
 #pragma unroll
         for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
+        uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
         while (active && R.rp <= kWinAdv / 4) {
+            it++;
             const uint32_t peek = R.peek();
             uint32_t e = lut_fast(tab, peek);
             if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
@@ -590,9 +628,20 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
             wq2 = emit ? wq3 : wq2;
             wq3 = emit ? ev : wq3;
             ent += emit ? 1u : 0u;
-            if (emit && (ent & 3u) == 0u) *reinterpret_cast<uint4*>(eout + ent - 4u) = make_uint4(wq0, wq1, wq2, wq3);
+            const bool qdone = emit && (ent & 3u) == 0u;
+            pq0 = qdone ? wq0 : pq0;
+            pq1 = qdone ? wq1 : pq1;
+            pq2 = qdone ? wq2 : pq2;
+            pq3 = qdone ? wq3 : pq3;
+            pent = qdone ? ent : pent;
+            pend_q = pend_q || qdone;
+            pbi0 = fin ? ent_blk : pbi0;
+            pbi1 = fin ? pack_cnt_dc(ent - ent_blk, dcd) : pbi1;
+            pblk = fin ? blk : pblk;
+            pend_b = pend_b || fin;
+            if ((it & 3u) == 0u) JD_FLUSH_Q();
+            if ((it & 1u) == 0u) JD_FLUSH_B();
             if (fin) {
-                bout[blk] = BlockInfo{ent_blk, pack_cnt_dc(ent - ent_blk, dcd)};
                 blk++;
                 ent_blk = ent;
                 active = blk < nblk;
@@ -603,6 +652,8 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
             tab = (b3 == bpm3) ? tab_dc0 : tab;  // an MCU ends here
             b3 = (b3 == bpm3) ? 0u : b3;
         }
+        JD_FLUSH_Q();
+        JD_FLUSH_B();
         if (active && R.bit() > S.bits) {  // past the interval's data
             errs |= kEntBad;
             active = false;
@@ -613,6 +664,8 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
         R.next_window();
         wa = na;
     }
+#undef JD_FLUSH_Q
+#undef JD_FLUSH_B
     if (ent & 3u) {  // the last, partial quad: its r entries are the newest, wq[4-r..3]
         const uint32_t r = ent & 3u, qb = ent - r;
         eout[qb] = r == 3u ? wq1 : r == 2u ? wq2 : wq3;
@@ -1331,6 +1384,9 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
         const uint32_t lead = bi.entry_start & 3u;
         const uint32_t* ep = b.entries + (bi.entry_start - lead);
         const int n4 = cnt > 0 ? int(lead + uint32_t(cnt) + 3u) >> 2 : 0;  // cnt == 0: touch nothing
+#if JD_ABL & 4
+        if (lane == 1000)
+#endif
         for (int c = 0; c < n4; c += 4) {
             uint4 v[4];
 #pragma unroll
@@ -1362,10 +1418,12 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
             blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, qz[2 * p + 1]);
         }
     }
+#if !(JD_ABL & 2)
 #pragma unroll
     for (int r = 0; r < 8; r++) idct_row(blk + 8 * r);
 #pragma unroll
     for (int c = 0; c < 8; c++) idct_col(blk + c);
+#endif
     __syncthreads();  // every row read back before the planes overwrite the staging area
 
     // 3. component planes (int16), pitch = plane width + 8 samples
@@ -1416,6 +1474,9 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     // lane -> (row group gy, column group gc), advanced by 64 groups per iteration
     const uint32_t step_y = kIdctThreads / gpr, step_c = kIdctThreads - step_y * gpr;
     uint32_t gy = lane / gpr, gc = lane - gy * gpr;
+#if JD_ABL & 1
+    if (lane < 1000) return;
+#endif
     for (; gy < ngy; gy += step_y + (gc + step_c >= gpr ? 1u : 0u), gc = gc + step_c >= gpr ? gc + step_c - gpr : gc + step_c) {
         const uint32_t py = gy * rows, gx = gc << 3;
         const uint32_t y = y_tile + py, x = x_tile + gx;
@@ -1450,8 +1511,13 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
             }
             pack24(rgb, w0);
         }
+#if JD_ABL & 32
+        if (w0[0] == 0x12345678u && w1[3] == 0x9abcdef0u)
+#endif
+        {
         store24(out + (size_t(y) * W + x) * 3, w0, min(8u, W - x));
         if (pair && y + 1 < H) store24(out + (size_t(y + 1) * W + x) * 3, w1, min(8u, W - x));
+        }
     }
 }
 
