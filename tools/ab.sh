@@ -6,7 +6,8 @@ out=$1; shift
 mkdir -p "$out"
 for v in "$@"; do
   lib=gpu-jpeg-decoder_amd/libjdamd_$v.so; [ "$v" = base ] && lib=gpu-jpeg-decoder_amd/libjdamd.so
-  JDAMD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-sample 0 > "$out/$v.json" 2> "$out/$v.err"
+  ver=2; case "$v" in abl*) ver=0;; esac  # ablation builds compute wrong pixels on purpose
+  JDAMD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-sample 0 --verify $ver ${AB_ARGS:-} > "$out/$v.json" 2> "$out/$v.err"
   python - "$out/$v.json" "$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

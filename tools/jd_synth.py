@@ -31,8 +31,17 @@ def synth_pixels(w: int, h: int, seed: int, gray: bool = False) -> np.ndarray:
     return chans[0] if gray else np.stack(chans, -1)
 
 
+def default_encoder() -> str:
+    return os.environ.get("JD_ENCODER", "jdenc")
+
+
 def encode(pixels: np.ndarray, quality: int = 90, subsampling: str = "4:2:0", restart_rows: int = 0,
-           restart_blocks: int = 0, optimize: bool = False) -> bytes:
+           restart_blocks: int = 0, optimize: bool = False, encoder: Optional[str] = None) -> bytes:
+    encoder = encoder or default_encoder()
+    if encoder == "jdenc" and not optimize:
+        import jdenc
+
+        return jdenc.encode(pixels, quality, subsampling, restart_rows, restart_blocks)
     from PIL import Image
 
     img = Image.fromarray(pixels, "L" if pixels.ndim == 2 else "RGB")
@@ -49,14 +58,15 @@ def encode(pixels: np.ndarray, quality: int = 90, subsampling: str = "4:2:0", re
 
 
 def _one(args):
-    w, h, seed, quality, subsampling, rrows, rblocks = args
+    w, h, seed, quality, subsampling, rrows, rblocks, encoder = args
     gray = subsampling == "gray"
-    return encode(synth_pixels(w, h, seed, gray), quality, "4:4:4" if gray else subsampling, rrows, rblocks)
+    return encode(synth_pixels(w, h, seed, gray), quality, "4:4:4" if gray else subsampling, rrows, rblocks,
+                  encoder=encoder)
 
 
 def make_batch(n: int, w: int, h: int, quality: int = 90, subsampling: str = "4:2:0", restart_rows: int = 0,
                restart_blocks: int = 0, seed0: int = 0, workers: Optional[int] = None,
-               mixed: bool = False) -> List[bytes]:
+               mixed: bool = False, encoder: Optional[str] = None) -> List[bytes]:
     """n synthetic JPEGs.  mixed=True cycles 4:4:4 / 4:2:2 / 4:2:0 and draws quality from
     {50, 75, 90, 95} by seed (BASELINE config 5), without restart markers."""
     jobs = []
@@ -65,9 +75,9 @@ def make_batch(n: int, w: int, h: int, quality: int = 90, subsampling: str = "4:
         if mixed:
             ss = ("4:4:4", "4:2:2", "4:2:0")[i % 3]
             q = (50, 75, 90, 95)[np.random.default_rng(s + 7777).integers(0, 4)]
-            jobs.append((w, h, s, int(q), ss, 0, 0))
+            jobs.append((w, h, s, int(q), ss, 0, 0, encoder))
         else:
-            jobs.append((w, h, s, quality, subsampling, restart_rows, restart_blocks))
+            jobs.append((w, h, s, quality, subsampling, restart_rows, restart_blocks, encoder))
     workers = workers or min(16, os.cpu_count() or 1, max(1, n))
     if workers <= 1 or n < 4:
         return [_one(j) for j in jobs]
