@@ -213,7 +213,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic (seeded sinusoid + noise, Pillow baseline encode q{args.quality}, std Huffman)",
+            "data": f"synthetic (seeded sinusoid + noise, baseline encode q{args.quality} by "
+                    f"{'tools/jdenc.c' if jd_synth.default_encoder() == 'jdenc' else 'Pillow'}, std Huffman tables)",
             "config": {"workload": desc, "config": args.config, "images_per_rank": batch,
                        "global_batch": batch * world, "width": W, "height": H, "subsampling": ss,
                        "restart_rows": rrows, "parallelism": f"dp{world} (image sharding)",

@@ -97,7 +97,9 @@ struct alignas(16) ImgDesc {
     uint8_t comp_block0[4];           // first MCU block of each component
     uint8_t shx[4], shy[4];           // log2(hmax / h[c]), log2(vmax / v[c])
     uint32_t pad[1];
+    uint64_t planes;                  // fancy upsampling: device address of the int16 component planes
 };
+static_assert(sizeof(ImgDesc) % 16 == 0, "ImgDesc must stay 16-byte aligned");
 
 // Per-block result of the Huffman kernel (sparse coefficient representation):
 //   entry_start = index of the block's first AC entry in the entry array
@@ -203,6 +205,10 @@ struct BatchDev {
     uint32_t* status;             // per image
     unsigned long long* counters; // [0] AC entries written
     uint32_t max_tiles;
+    // fancy upsampling (JD_FLAG_FANCY_UPSAMPLING): k_idct_color writes component planes to HBM
+    // (ImgDesc::planes), k_colour_fancy filters and colours them
+    uint32_t fancy;
+    uint32_t max_fancy_wgs;       // k_colour_fancy workgroups per image (grid x)
 };
 
 }  // namespace jd

@@ -1343,6 +1343,14 @@ __device__ __forceinline__ void load8_samples(const int16_t* pl, uint32_t off, u
     v[7] = s0 ? x7 : (s1 ? h1 : h0);
 }
 
+// Fancy-upsampling planes in HBM: component c of an image at int16 offset fancy_plane_off, pitch
+// mcux * h[c] * 8 samples, mcuy * v[c] * 8 rows (the padded MCU grid).
+__device__ __forceinline__ size_t fancy_plane_off(const ImgDesc& im, uint32_t c) {
+    size_t off = 0;
+    for (uint32_t k = 0; k < c; k++) off += size_t(im.mcux * im.h[k] * 8) * (im.mcuy * im.v[k] * 8);
+    return off;
+}
+
 __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     // staging (64 rows of 66 int16 = 33 words: odd pitch, conflict-free read-back) and then the
     // component planes share s_buf; planes need at most 64*64 + 64*2*6 int16 (§ host tile choice)
@@ -1424,6 +1432,25 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
 #pragma unroll
     for (int c = 0; c < 8; c++) idct_col(blk + c);
 #endif
+    if (b.fancy) {  // wave-uniform: component planes to HBM, k_colour_fancy takes it from there
+        if (have) {
+            const uint32_t hc = im.h[comp], vc = im.v[comp];
+            const uint32_t t = bb - im.comp_block0[comp];
+            const uint32_t tyb = t / hc, txb = t - tyb * hc;
+            int16_t* dst = reinterpret_cast<int16_t*>(im.planes) + fancy_plane_off(im, comp) +
+                           size_t(((r0 + mr) * vc + tyb) * 8) * (im.mcux * hc * 8) + ((m0 + mi) * hc + txb) * 8;
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                uint4 q;
+                q.x = (uint32_t(blk[8 * r + 0]) & 0xFFFFu) | (uint32_t(blk[8 * r + 1]) << 16);
+                q.y = (uint32_t(blk[8 * r + 2]) & 0xFFFFu) | (uint32_t(blk[8 * r + 3]) << 16);
+                q.z = (uint32_t(blk[8 * r + 4]) & 0xFFFFu) | (uint32_t(blk[8 * r + 5]) << 16);
+                q.w = (uint32_t(blk[8 * r + 6]) & 0xFFFFu) | (uint32_t(blk[8 * r + 7]) << 16);
+                *reinterpret_cast<uint4*>(dst + size_t(r) * (im.mcux * hc * 8)) = q;
+            }
+        }
+        return;
+    }
     __syncthreads();  // every row read back before the planes overwrite the staging area
 
     // 3. component planes (int16), pitch = plane width + 8 samples
@@ -1522,6 +1549,77 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Fancy upsampling + colour (JD_FLAG_FANCY_UPSAMPLING), lane = 8 consecutive pixels of a row.
+// The triangular filters of libjpeg (jdsample.c h2v1 / h2v2 / h1v2 fancy upsampling) on the
+// reference's un-shifted samples, edges replicated at the component's real sample extent; the
+// same definition as oracle/jdoracle.c fancy_sample().  Other ratios replicate.
+// ------------------------------------------------------------------------------------------
+struct FancyPlane {
+    const int16_t* p;
+    uint32_t pitch, rx, ry, cw, ch;
+    __device__ __forceinline__ int at(uint32_t x, uint32_t y) const { return p[size_t(y) * pitch + x]; }
+};
+
+__device__ __forceinline__ int fancy_px(const FancyPlane& P, uint32_t x, uint32_t y) {
+    if (P.rx == 2 && P.ry == 1) {
+        const uint32_t i = x >> 1;
+        if (x & 1) return i + 1 >= P.cw ? P.at(i, y) : (3 * P.at(i, y) + P.at(i + 1, y) + 2) >> 2;
+        return i == 0 ? P.at(0, y) : (3 * P.at(i, y) + P.at(i - 1, y) + 1) >> 2;
+    }
+    if (P.ry == 2 && (P.rx == 1 || P.rx == 2)) {
+        const uint32_t r = y >> 1;
+        const uint32_t far = (y & 1) ? min(r + 1, P.ch - 1) : (r == 0 ? 0u : r - 1);
+        if (P.rx == 1) return (3 * P.at(x, r) + P.at(x, far) + ((y & 1) ? 2 : 1)) >> 2;
+        const uint32_t i = x >> 1;
+        const int cs = 3 * P.at(i, r) + P.at(i, far);
+        if (x & 1) {
+            if (i + 1 >= P.cw) return (4 * cs + 7) >> 4;
+            return (3 * cs + 3 * P.at(i + 1, r) + P.at(i + 1, far) + 7) >> 4;
+        }
+        if (i == 0) return (4 * cs + 8) >> 4;
+        return (3 * cs + 3 * P.at(i - 1, r) + P.at(i - 1, far) + 8) >> 4;
+    }
+    return P.at(x / P.rx, y / P.ry);
+}
+
+__global__ __launch_bounds__(256) void k_colour_fancy(BatchDev b) {
+    const ImgDesc& im = b.imgs[blockIdx.y];
+    const uint32_t W = im.width, H = im.height, gpr = (W + 7) >> 3;
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= gpr * H) return;
+    const uint32_t y = g / gpr, x0 = (g - y * gpr) << 3;
+    const uint32_t n = min(8u, W - x0);
+    FancyPlane P[3];
+    size_t off = 0;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const uint32_t cc = uint32_t(c) < im.ncomp ? uint32_t(c) : 0u;
+        P[c].pitch = im.mcux * im.h[cc] * 8;
+        P[c].p = reinterpret_cast<const int16_t*>(im.planes) + (uint32_t(c) < im.ncomp ? off : 0);
+        P[c].rx = im.hmax / im.h[cc];
+        P[c].ry = im.vmax / im.v[cc];
+        P[c].cw = (W * im.h[cc] + im.hmax - 1) / im.hmax;
+        P[c].ch = (H * im.v[cc] + im.vmax - 1) / im.vmax;
+        if (uint32_t(c) < im.ncomp) off += size_t(P[c].pitch) * (im.mcuy * im.v[cc] * 8);
+    }
+    uint32_t rgb[8][3];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t x = min(x0 + uint32_t(j), W - 1);
+        const int yv = fancy_px(P[0], x, y);
+        if (im.ncomp == 1) {
+            rgb[j][0] = rgb[j][1] = rgb[j][2] = clamp_u8(yv + 128);
+        } else {
+            const int cb = fancy_px(P[1], x, y), cr = fancy_px(P[2], x, y);
+            colour_px(yv, cb, cr, chroma_terms(cb, cr), rgb[j][0], rgb[j][1], rgb[j][2]);
+        }
+    }
+    uint32_t w[6];
+    pack24(rgb, w);
+    store24(reinterpret_cast<uint8_t*>(im.rgb) + (size_t(y) * W + x0) * 3, w, n);
+}
+
+// ------------------------------------------------------------------------------------------
 // Known-answer hooks
 // ------------------------------------------------------------------------------------------
 __global__ void k_test_idct(const int32_t* in_zz, int32_t* out, int n) {
@@ -1583,6 +1681,9 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
         case 8: hipLaunchKernelGGL(k_dpcm, dim3(b.nseg), dim3(64), 0, s, b); break;
         case 9:
             if (b.max_tiles) hipLaunchKernelGGL(k_idct_color, dim3(b.max_tiles, b.nimg), dim3(kIdctThreads), 0, s, b);
+            break;
+        case 10:
+            if (b.fancy && b.max_fancy_wgs) hipLaunchKernelGGL(k_colour_fancy, dim3(b.max_fancy_wgs, b.nimg), dim3(256), 0, s, b);
             break;
         default: return hipErrorInvalidValue;
     }

@@ -131,7 +131,7 @@ struct jd_ctx {
     size_t lut_dev_count = 0;
 
     // pools
-    DevBuf plan, chunk_brk, blocks, entries, input, output, comp;
+    DevBuf plan, chunk_brk, blocks, entries, input, output, comp, planes;
     PinBuf plan_host, input_host;
 
     hipEvent_t ev[JD_NUM_KERNELS][2] = {};
@@ -559,6 +559,24 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
     if (nimg) {
         HIPCHK(ctx, ensure_dev(ctx->comp, std::max<size_t>(16, P.comp_bytes)));
         for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(ctx->comp.p);
+        const bool fancy = (ctx->flags & JD_FLAG_FANCY_UPSAMPLING) != 0;
+        uint32_t max_fancy_wgs = 0;
+        if (fancy) {  // int16 component planes over the padded MCU grid, 256-B aligned per image
+            std::vector<size_t> poff(P.imgs.size());
+            size_t tot = 0;
+            for (size_t i = 0; i < P.imgs.size(); i++) {
+                const ImgDesc& d = P.imgs[i];
+                size_t n = 0;
+                for (uint32_t c = 0; c < d.ncomp; c++) n += size_t(d.mcux * d.h[c] * 8) * (d.mcuy * d.v[c] * 8) * 2;
+                poff[i] = tot;
+                tot += align_up(n, 256);
+                const uint64_t groups = uint64_t((d.width + 7) / 8) * d.height;
+                max_fancy_wgs = std::max<uint32_t>(max_fancy_wgs, uint32_t((groups + 255) / 256));
+            }
+            HIPCHK(ctx, ensure_dev(ctx->planes, std::max<size_t>(16, tot)));
+            for (size_t i = 0; i < P.imgs.size(); i++)
+                P.imgs[i].planes = reinterpret_cast<uint64_t>(ctx->planes.p) + poff[i];
+        }
         std::vector<uint8_t> blob;
         const size_t nseg = P.seg_img.size();
         const size_t nsub = P.nsub;
@@ -639,6 +657,8 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
         b.max_tiles = P.max_tiles;
+        b.fancy = fancy ? 1u : 0u;
+        b.max_fancy_wgs = max_fancy_wgs;
 
         ctx->last = b;
         ctx->last_blocks = P.total_blocks;
@@ -686,8 +706,11 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
             nsubd * 28,                                        // k_chain: counts in, offsets out
             ecs + blocks * 8 + entries * 4,                    // k_piece_write: ECS in, sparse coefficients out
             blocks * 16,                                       // k_dpcm: BlockInfo read + write
-            blocks * 8 + entries * 4 + P.pixels * 3};          // k_idct_color: coefficients in, RGB out
+            blocks * 8 + entries * 4 + (fancy ? blocks * 128 : P.pixels * 3),  // k_idct_color: coefficients in,
+                                                                                // RGB (fancy: planes) out
+            fancy ? blocks * 128 + P.pixels * 3 : 0.0};        // k_colour_fancy: planes in, RGB out
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
+            if (k == 10 && !fancy) continue;  // k_colour_fancy runs only with the flag
             S.launches[k]++;
             S.bytes[k] += bytes[k];
             if (timing) {
@@ -747,7 +770,7 @@ const char* jd_ctx_last_error(jd_ctx* ctx) { return ctx ? ctx->last_error.c_str(
 
 const char* jd_kernel_name(int k) {
     static const char* names[JD_NUM_KERNELS] = {"k_scan",      "k_index", "k_compact",     "k_subplan", "k_piece_scan",
-                                                "k_rescan",    "k_chain", "k_piece_write", "k_dpcm",    "k_idct_color"};
+                                                "k_rescan",    "k_chain", "k_piece_write", "k_dpcm",    "k_idct_color", "k_colour_fancy"};
     return (k >= 0 && k < JD_NUM_KERNELS) ? names[k] : "?";
 }
 

@@ -17,10 +17,18 @@
 
 namespace jdamd {
 
+// Context flags for the process-wide context (set before the first decode), e.g.
+// JD_FLAG_FANCY_UPSAMPLING for the CLI's --fancy.
+inline unsigned& default_context_flags() {
+    static unsigned flags = 0;
+    return flags;
+}
+
 inline jd_ctx* default_context() {
     static jd_ctx* ctx = [] {
         jd_ctx* c = nullptr;
-        jd_status st = jd_ctx_create(&c, 0, nullptr);
+        jd_opts o{default_context_flags(), 0};
+        jd_status st = jd_ctx_create(&c, 0, &o);
         if (st != JD_OK) throw std::runtime_error(std::string("jd_ctx_create: ") + jd_status_str(st));
         return c;
     }();

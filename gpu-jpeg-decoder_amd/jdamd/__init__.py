@@ -30,10 +30,12 @@ JD_ERR_IO = 8
 JD_FLAG_TIMING = 1
 JD_FLAG_FORCE_SYNC = 2
 JD_FLAG_FORCE_LANES = 4
+JD_FLAG_FANCY_UPSAMPLING = 8
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES}
-JD_NUM_KERNELS = 10
+JD_ABI_VERSION = 2
+JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece_scan", "k_rescan", "k_chain",
-                "k_piece_write", "k_dpcm", "k_idct_color"]
+                "k_piece_write", "k_dpcm", "k_idct_color", "k_colour_fancy"]
 
 
 class JDError(RuntimeError):
@@ -215,10 +217,16 @@ class Decoder:
     """One jd_ctx on one HIP device.  Mirrors the reference's allocate()/decode/clean() lifecycle
     (cuda-decoder/src/parser.cu:324-358, 577-700) as a context object."""
 
-    def __init__(self, device: int = 0, timing: bool = False, parse_threads: int = 0, path: str = "auto"):
+    def __init__(self, device: int = 0, timing: bool = False, parse_threads: int = 0, path: str = "auto",
+                 fancy: bool = False):
+        """fancy=True: libjpeg's triangular chroma upsampling instead of replication
+        (JD_FLAG_FANCY_UPSAMPLING; an option beyond the reference, see include/jd.h)."""
         self.lib = load_library()
+        if self.lib.jd_abi_version() != JD_ABI_VERSION:
+            raise JDError(JD_ERR_INVALID_ARG, f"libjdamd ABI {self.lib.jd_abi_version()} != {JD_ABI_VERSION}: rebuild")
         self.ctx = ctypes.c_void_p()
-        opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path], parse_threads)
+        opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path] | (JD_FLAG_FANCY_UPSAMPLING if fancy else 0),
+                     parse_threads)
         st = self.lib.jd_ctx_create(ctypes.byref(self.ctx), device, ctypes.byref(opts))
         if st != JD_OK:
             raise JDError(st, "jd_ctx_create")

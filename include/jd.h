@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define JD_ABI_VERSION 1
+#define JD_ABI_VERSION 2
 
 typedef enum jd_status {
     JD_OK = 0,
@@ -47,6 +47,10 @@ typedef struct jd_ctx jd_ctx;
  * setting; the flags exist so tests can stress the two extremes of the piece-parallel decode. */
 #define JD_FLAG_FORCE_SYNC 2u  /* 1024-bit pieces: many speculative starts, exercises re-scans */
 #define JD_FLAG_FORCE_LANES 4u /* one piece per restart interval (the whole scan if no DRI) */
+/* Chroma upsampling: replicate (default; the semantics pinned in DESIGN.md §2) or, with this flag,
+ * libjpeg's triangular "fancy" filter for 2x1, 2x2 and 1x2 ratios (closer to libjpeg-turbo /
+ * Pillow output; an option beyond the reference, which has no subsampled chroma at all). */
+#define JD_FLAG_FANCY_UPSAMPLING 8u
 
 typedef struct jd_opts {
     unsigned flags;
@@ -133,7 +137,7 @@ jd_status jd_synchronize(jd_ctx* ctx);
 /* Per-kernel timing (JD_FLAG_TIMING).
  * Kernels: 0 k_scan, 1 k_index, 2 k_compact, 3 k_subplan, 4 k_piece_scan, 5 k_rescan, 6 k_chain,
  * 7 k_piece_write, 8 k_dpcm, 9 k_idct_color. */
-#define JD_NUM_KERNELS 10
+#define JD_NUM_KERNELS 11
 typedef struct jd_stats {
     int launches[JD_NUM_KERNELS];
     double total_ms[JD_NUM_KERNELS]; /* hipEvent time, summed over launches                     */

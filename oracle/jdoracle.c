@@ -491,7 +491,49 @@ int jdo_decode_coefs(const uint8_t* jpeg, size_t len, int32_t* coef) {
     return st;
 }
 
+/* Fancy (triangular) chroma upsampling, an OPTION beyond the reference (which has no chroma
+ * subsampling at all): the published libjpeg / libjpeg-turbo filters (jdsample.c
+ * h2v1_fancy_upsample, h2v2_fancy_upsample, h1v2_fancy_upsample) restated on the reference's
+ * un-shifted samples.  The level shift commutes with the filters exactly (+128 on every input
+ * adds 4 * 128 or 16 * 128 before the >> 2 / >> 4), so this equals libjpeg's filter on shifted
+ * samples minus 128.  Neighbours outside the component's real samples (ceil(W * h / hmax) x
+ * ceil(H * v / vmax)) are replaced by the edge sample, as libjpeg's edge cases and context rows do.
+ * Ratios other than 2x1, 2x2 and 1x2 keep replicate upsampling. */
+static int fancy_sample(const planes_t* pl, const jdo_info* f, int c, int x, int y) {
+    const int rx = f->hmax / f->h[c], ry = f->vmax / f->v[c];
+    const int cw = (f->width * f->h[c] + f->hmax - 1) / f->hmax;
+    const int ch = (f->height * f->v[c] + f->vmax - 1) / f->vmax;
+    const int32_t* P = pl->plane[c];
+    const size_t st = (size_t)pl->stride[c];
+#define S(xx, yy) P[(size_t)(yy) * st + (xx)]
+    if (rx == 2 && ry == 1) {
+        const int i = x >> 1;
+        if (x & 1) return i >= cw - 1 ? S(i, y) : (3 * S(i, y) + S(i + 1, y) + 2) >> 2;
+        return i == 0 ? S(0, y) : (3 * S(i, y) + S(i - 1, y) + 1) >> 2;
+    }
+    if (ry == 2 && (rx == 1 || rx == 2)) {
+        const int r = y >> 1;
+        int far = (y & 1) ? r + 1 : r - 1;
+        far = far < 0 ? 0 : (far > ch - 1 ? ch - 1 : far);
+        if (rx == 1) return (3 * S(x, r) + S(x, far) + ((y & 1) ? 2 : 1)) >> 2;
+        const int i = x >> 1;
+        const int cs = 3 * S(i, r) + S(i, far);
+        if (x & 1) {
+            if (i >= cw - 1) return (4 * cs + 7) >> 4;
+            return (3 * cs + 3 * S(i + 1, r) + S(i + 1, far) + 7) >> 4;
+        }
+        if (i == 0) return (4 * cs + 8) >> 4;
+        return (3 * cs + 3 * S(i - 1, r) + S(i - 1, far) + 8) >> 4;
+    }
+#undef S
+    return P[(size_t)(y * f->v[c] / f->vmax) * st + (size_t)(x * f->h[c] / f->hmax)];
+}
+
 int jdo_decode(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* height) {
+    return jdo_decode_ex(jpeg, len, rgb, width, height, 0);
+}
+
+int jdo_decode_ex(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* height, unsigned flags) {
     img_t* im = (img_t*)malloc(sizeof(img_t));
     if (!im) return JDO_ERR_INVALID_ARG;
     int st = parse(jpeg, len, im);
@@ -522,6 +564,10 @@ int jdo_decode(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* h
             for (int x = 0; x < f->width; x++) {
                 int s[3] = {0, 0, 0};
                 for (int c = 0; c < f->ncomp; c++) {
+                    if (flags & JDO_FANCY_UPSAMPLING) {
+                        s[c] = fancy_sample(&pl, f, c, x, y);
+                        continue;
+                    }
                     int sx = x * f->h[c] / f->hmax, sy = y * f->v[c] / f->vmax;
                     s[c] = pl.plane[c][(size_t)sy * pl.stride[c] + sx];
                 }

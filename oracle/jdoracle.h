@@ -45,6 +45,11 @@ int jdo_parse(const uint8_t* jpeg, size_t len, jdo_info* info);
 /* Full decode to interleaved uint8 RGB (H*W*3).  rgb may be NULL (decode + status only). */
 int jdo_decode(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* height);
 
+/* As jdo_decode; flags: JDO_FANCY_UPSAMPLING = libjpeg's triangular chroma filter for 2x1, 2x2
+ * and 1x2 sampling ratios instead of replication (numerically equal to jd.h's flag). */
+#define JDO_FANCY_UPSAMPLING 8u
+int jdo_decode_ex(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* height, unsigned flags);
+
 /* Entropy-decode only: quantised coefficients of every block, 64 int32 per block in zig-zag order
  * with the DC already un-predicted (absolute).  Blocks are in scan order: mcu * blocks_per_mcu + b.
  * coef must hold mcux*mcuy*blocks_per_mcu*64 ints. */

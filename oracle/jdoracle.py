@@ -37,6 +37,8 @@ def lib() -> ctypes.CDLL:
         L.jdo_parse.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Info)]
         L.jdo_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
                                  ctypes.POINTER(ctypes.c_int)]
+        L.jdo_decode_ex.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                    ctypes.POINTER(ctypes.c_int), ctypes.c_uint]
         L.jdo_decode_coefs.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.jdo_idct_ref.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.jdo_color_ref.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -53,14 +55,19 @@ def info(data: bytes) -> Tuple[int, _Info]:
     return st, i
 
 
-def decode(data: bytes) -> Tuple[int, Optional[np.ndarray]]:
-    """(status, RGB uint8 [H,W,3] or None).  Mirrors JPEGParser extract()+decode()."""
+FANCY_UPSAMPLING = 8  # == JD_FLAG_FANCY_UPSAMPLING
+
+
+def decode(data: bytes, fancy: bool = False) -> Tuple[int, Optional[np.ndarray]]:
+    """(status, RGB uint8 [H,W,3] or None).  Mirrors JPEGParser extract()+decode(); fancy=True
+    selects libjpeg's triangular chroma upsampling (an option beyond the reference)."""
     st, i = info(data)
     if st != 0:
         return st, None
     out = np.empty((i.height, i.width, 3), np.uint8)
     w, h = ctypes.c_int(), ctypes.c_int()
-    st = lib().jdo_decode(data, len(data), out.ctypes.data, ctypes.byref(w), ctypes.byref(h))
+    st = lib().jdo_decode_ex(data, len(data), out.ctypes.data, ctypes.byref(w), ctypes.byref(h),
+                             FANCY_UPSAMPLING if fancy else 0)
     return st, out
 
 

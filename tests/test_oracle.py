@@ -239,3 +239,28 @@ def test_corrupt_and_unsupported_statuses():
     assert jdoracle.decode(b"\xff\xd8\xff\xd9")[0] == 2       # EOI before SOS
     assert jdoracle.decode(b"\x00\x01\x02\x03")[0] == 2       # no SOI
     assert jdoracle.decode(d[:100])[0] == 4                   # ends inside the headers
+
+
+@pytest.mark.parametrize("ss", ["4:2:0", "4:2:2", "4:4:0"])
+def test_fancy_close_to_pillow(ss):
+    """The fancy-upsampling option restates libjpeg's triangular filters: against libjpeg-turbo
+    (Pillow) it differs only by the reference's own IDCT/colour arithmetic, i.e. as little as a
+    4:4:4 decode does (max 4-5 levels), while replicate upsampling is off by tens of levels."""
+    Image = pytest.importorskip("PIL.Image")
+    import jd_synth
+
+    px = jd_synth.synth_pixels(301, 199, 4)
+    data = jd_synth.encode(px, 95, ss)
+    pil = np.asarray(Image.open(io.BytesIO(data)).convert("RGB")).astype(int)
+    st, fancy = jdoracle.decode(data, fancy=True)
+    st2, rep = jdoracle.decode(data)
+    assert st == 0 and st2 == 0
+    assert np.abs(fancy - pil).max() <= 6 and np.abs(fancy - pil).mean() < 1.0
+    assert np.abs(rep - pil).mean() > 2 * np.abs(fancy - pil).mean()
+
+
+def test_fancy_is_identity_without_subsampling():
+    import jd_synth
+
+    data = jd_synth.encode(jd_synth.synth_pixels(77, 33, 2), 90, "4:4:4")
+    assert np.array_equal(jdoracle.decode(data, fancy=True)[1], jdoracle.decode(data)[1])
