@@ -89,23 +89,26 @@ struct alignas(16) ImgDesc {
     uint32_t chunk_base, nchunks;     // 16 KiB scan chunks of this image's ECS
     uint32_t sub_base, sub_cap;       // this image's range in the subsequence list (upper bound)
     uint32_t tile_mcus;               // MCU columns per IDCT/colour tile
-    uint32_t tile_mrows;              // MCU rows per tile (tile_mcus * tile_mrows * bpm <= 64)
+    uint32_t tile_mrows;              // MCU rows per tile: always 1 (a tile is a run of MCUs of one
+                                      // MCU row, tile_mcus * bpm <= 64; the DC prediction relies on it)
     uint32_t tiles_x, tiles_y;        // tiles per image row / column
     uint32_t lg_mw, lg_mh;            // log2 of the MCU width / height in pixels
     uint8_t h[4], v[4];
     uint16_t qslot[4];                // quant table of each component (index into batch Q array)
     uint8_t comp_block0[4];           // first MCU block of each component
     uint8_t shx[4], shy[4];           // log2(hmax / h[c]), log2(vmax / v[c])
-    uint32_t pad[1];
+    uint32_t tile_base;               // first tile of this image in BatchDev::tile_dc
     uint64_t planes;                  // fancy upsampling: device address of the int16 component planes
+    uint32_t qmask;                   // k_idct_color's range test of quantised AC coefficients (bits
+                                      // k..15 and 16+k..31: |c| <= 2^(k-1), 2^(k-1) * max step < 2^16)
+    uint32_t pad[3];
 };
 static_assert(sizeof(ImgDesc) % 16 == 0, "ImgDesc must stay 16-byte aligned");
 
 // Per-block result of the Huffman kernel (sparse coefficient representation):
 //   entry_start = index of the block's first AC entry in the entry array
-//   cnt_dc      = (number of AC entries << 26) | (DC & 0x3FFFFFF): DC quantised, as a 26-bit two's
-//                 complement value — the DC difference until k_dpcm (or the self-synchronising write
-//                 pass) turns it into the predicted DC
+//   cnt_dc      = (number of AC entries << 26) | (DC difference & 0x3FFFFFF): the quantised DC
+//                 difference as a 26-bit two's complement value; k_idct_color predicts the DC
 // AC entry = (int16 value << 16) | zig-zag index (1..63).
 struct BlockInfo {
     uint32_t entry_start;
@@ -162,6 +165,17 @@ constexpr uint32_t kStCorrupt = 1u;     // bad code / overrun / DC range
 constexpr uint32_t kStRstMissing = 2u;  // fewer RST markers than intervals
 constexpr uint32_t kStRstOrder = 4u;    // RSTn numbering wrong
 
+// Per IDCT/colour tile: k_dc_sum's aggregate (sums of the DC differences of components 0..2 after
+// the tile's last interval start, flag = it has one), which k_dc_scan turns into the components'
+// DC predictors at the tile's first block (flag 0).
+struct alignas(16) DcPred {
+    int32_t p0, p1, p2, flag;
+};
+
+struct TileRef {
+    uint32_t img, tile;
+};
+
 struct BatchDev {
     const ImgDesc* imgs;
     uint32_t nimg;
@@ -188,6 +202,7 @@ struct BatchDev {
     uint32_t* piece_nent;         // scan: AC entries in the piece
     uint32_t* piece_mcu0;         // chain: first MCU of the piece within its segment
     uint32_t* piece_ent0;         // chain: first AC-entry slot of the piece
+    uint32_t* seg_fix;            // k_chain: 1 = the interval needs k_chain_fix's serial walk
     CpRec* piece_cp;              // scan: kCpRecords per piece slot (CpRec)
     const uint32_t* chain_seg;    // k_chain: segment of each lane, grouped by table set
     uint32_t nchain;              // multiple of kPieceThreads
@@ -203,8 +218,12 @@ struct BatchDev {
     uint32_t* entries;
     uint64_t entries_cap;         // entry slots allocated
     uint32_t* status;             // per image
-    unsigned long long* counters; // [0] AC entries written
+    unsigned long long* counters; // [0] AC entries written, [1] slow_tiles entries
     uint32_t max_tiles;
+    TileRef* slow_tiles;          // (image, tile) k_idct_color left to k_idct_color_exact; count in counters[1]
+    uint32_t total_tiles;
+    DcPred* tile_dc;              // per tile: k_dc_sum aggregates, then (k_dc_scan) the DC predictors
+                                  // of components 0..2 at the tile's first block
     // fancy upsampling (JD_FLAG_FANCY_UPSAMPLING): k_idct_color writes component planes to HBM
     // (ImgDesc::planes), k_colour_fancy filters and colours them
     uint32_t fancy;

@@ -45,6 +45,19 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
+// The same inclusive scan in six DPP adds (no LDS traffic): Hillis-Steele within each row of 16
+// lanes (row_shr 1, 2, 4, 8), then row_bcast 15 / 31 carry rows into the rows above.  Every lane
+// of the wave must be active.
+__device__ __forceinline__ int wave_scan_dpp(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15, rows 1 and 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31, rows 2 and 3
+    return x;
+}
+
 // Exclusive scan over a 256-thread block; returns the exclusive prefix, *total the block sum.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_wsum, uint32_t* total) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -332,12 +345,14 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 //                  thousand bits), takes the first MCU boundary at/after j*piece_bits as the
 //                  piece start, and counts MCUs and AC entries up to the first MCU boundary
 //                  at/after (j+1)*piece_bits.  Piece 0 starts at bit 0 in the true state.
-//   k_chain        wave per interval: piece j's end must be piece j+1's start; a mismatch (the
-//                  guess had not synchronised) is re-scanned from the verified boundary.  Prefix
-//                  sums give each piece its first MCU and AC-entry slot.
+//   k_rescan       lane per piece whose start is not its predecessor's end: re-scan from that end
+//   k_chain        wave per interval: piece j's end must be piece j+1's start (k_chain_fix walks
+//                  the rare interval where it still is not serially, re-scanning).  Prefix sums
+//                  give each piece its first MCU and AC-entry slot.
 //   k_piece<Write> lane per piece, from its verified MCU boundary: BlockInfo + AC entries, DC as
 //                  differences
-//   k_dpcm         wave per interval: DC differences -> DC values (parser.cpp:106-111)
+//   k_dc_sum/scan  per tile, the DC predictors at its first block (parser.cpp:106-111); the tile's
+//                  own wave in k_idct_color finishes the prediction
 //
 // A lane's bitstream streams through its own LDS row in windows of kWinAdv bytes: a round issues
 // the loads of the NEXT window into registers, decodes every symbol whose refill word lies in the
@@ -945,18 +960,80 @@ __global__ __launch_bounds__(kPieceThreads) void k_rescan(BatchDev b) {
     b.piece_nent[u] = W.ents;
 }
 
-// One lane per interval (workgroups grouped by table set): verify that every piece starts where
-// its predecessor ended; re-scan a piece whose speculative start had not synchronised (the
-// workgroup stages its tables only when some lane needs one); prefix sums give each piece its
-// first MCU and first AC-entry slot.
-__global__ __launch_bounds__(kPieceThreads) void k_chain(BatchDev b) {
+// One wave per interval, all pieces at once: verify that every piece starts where its predecessor
+// ended, and give each piece its first MCU and first AC-entry slot by prefix sums.  The serial
+// rule (piece j's entries start at the running count rounded up to a quad) is the same prefix:
+// align4(align4(e0) + ... ) = align4(e0) + sum of align4(count) over the earlier pieces.  An
+// interval where some speculative start still disagrees after k_rescan (a double failure, rare)
+// is flagged for k_chain_fix, which walks it serially with re-scans.
+__global__ __launch_bounds__(256) void k_chain(BatchDev b) {
+    const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (s >= b.nseg) return;  // wave-uniform
+    SegInfo S;
+    seg_info(b, s, S);
+    const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
+    const uint32_t nmcu_seg = S.nblk / S.bpm;
+    const uint64_t ent_cap_end = uint64_t(S.ent0) + seg_entry_cap(S);
+    bool need = false;
+    for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        if (j < n) need |= b.piece_bit[base + j] != (j ? b.piece_end[base + j - 1] : 0u);
+    }
+    if (__any(need)) {  // wave-uniform
+        if (lane == 0) b.seg_fix[s] = 1u;
+        return;
+    }
+    if (lane == 0) b.seg_fix[s] = 0u;
+    uint32_t mcu_run = 0, ent_run = (S.ent0 + 3u) & ~3u;
+    bool bad = false;
+    for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool in = j < n;
+        uint32_t pm = in ? b.piece_nmcu[base + j] : 0u;
+        const uint32_t pe = in ? b.piece_nent[base + j] : 0u;
+        const bool last = j + 1 == n;
+        // counting from a verified start is exact, so an error there is the stream's; the last
+        // piece's scan runs past the data on purpose (its write lane checks it exactly)
+        bad |= in && !last && (pm >> 31);
+        pm = (in && !last) ? (pm & 0x7FFFFFFFu) : 0u;
+        const uint32_t pe4 = in ? (pe + 3u) & ~3u : 0u;
+        const uint32_t im = uint32_t(wave_scan_dpp(int(pm))), ie = uint32_t(wave_scan_dpp(int(pe4)));
+        const uint32_t m0 = mcu_run + im - pm, e0 = ent_run + ie - pe4;
+        if (last) {  // the last piece takes the interval's remaining MCUs
+            bad |= m0 > nmcu_seg;
+            pm = nmcu_seg >= m0 ? nmcu_seg - m0 : 0u;
+        }
+        // a piece stores at most 63 entries per block: if that cannot fit, the counts are corrupt
+        if (in && uint64_t(e0) + 63ull * pm * S.bpm > ent_cap_end) {
+            bad = true;
+            pm = 0;
+        }
+        if (in) {
+            b.piece_mcu0[base + j] = m0;
+            b.piece_nmcu[base + j] = pm;
+            b.piece_ent0[base + j] = e0;
+        }
+        mcu_run += __shfl(int(im), 63, 64);
+        ent_run += __shfl(int(ie), 63, 64);
+    }
+    if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+}
+
+// One lane per interval flagged by k_chain (workgroups grouped by table set): walk its pieces in
+// order, re-scan every piece whose start disagrees with its predecessor's end (the workgroup
+// stages its tables only when some lane needs them), and prefix the counts serially.
+__global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const uint32_t li = blockIdx.x * kPieceThreads + threadIdx.x;
-    const uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
+    uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
+    if (s != kInvalidImage && !b.seg_fix[s]) s = kInvalidImage;
+    const bool need = s != kInvalidImage;
+    if (!__syncthreads_or(need)) return;  // workgroup-uniform: the common case
     const TableSet& ts = b.tablesets[b.chain_wg_tableset[blockIdx.x]];
-    const bool valid = s != kInvalidImage;
+    const bool valid = need;
     SegInfo S;
     uint32_t base = 0, n = 0;
     if (valid) {
@@ -966,16 +1043,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain(BatchDev b) {
     } else {
         seg_invalid(b, S);
     }
-    // does any piece need a re-scan?  (the first mismatch is enough to know)
-    bool need = false;
     {
-        uint32_t expect = 0;
-        for (uint32_t j = 0; j < n && !need; j++) {
-            need = b.piece_bit[base + j] != expect;
-            expect = b.piece_end[base + j];
-        }
-    }
-    if (__syncthreads_or(need)) {
         stage_luts(b, ts, s_lut, kPieceThreads);
         __syncthreads();
     }
@@ -1029,38 +1097,85 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain(BatchDev b) {
     if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
 }
 
-// One wave per interval: DC differences -> DC values, per component (parser.cpp:106-111: the
-// predictor restarts at 0 at every interval), with the reference's int16 range check.
-__global__ __launch_bounds__(64) void k_dpcm(BatchDev b) {
-    const uint32_t s = blockIdx.x;
-    SegInfo S;
-    seg_info(b, s, S);
-    const uint32_t lane = threadIdx.x;
-    int run0 = 0, run1 = 0, run2 = 0;
-    bool bad = false;
-    uint32_t bb0 = 0;  // MCU position of the chunk's first block
-    for (uint32_t c0 = 0; c0 < S.nblk; c0 += 64) {
-        const uint32_t j = c0 + lane;
-        const bool in = j < S.nblk;
-        const uint32_t bq = (bb0 + lane) % S.bpm;  // MCU block index of block j
-        const uint32_t comp = (S.pattern >> (2 * bq)) & 3u;
-        BlockInfo bi = in ? b.blocks[S.blk0 + j] : BlockInfo{0u, 0u};
-        const int d = int32_t(bi.cnt_dc << 6) >> 6;
-        const int i0 = int(wave_incl_scan(uint32_t(comp == 0 ? d : 0)));
-        const int i1 = int(wave_incl_scan(uint32_t(comp == 1 ? d : 0)));
-        const int i2 = int(wave_incl_scan(uint32_t(comp == 2 ? d : 0)));
-        const int v = comp == 0 ? run0 + i0 : (comp == 1 ? run1 + i1 : run2 + i2);
-        if (in) {
-            bad |= v < -32768 || v > 32767;
-            bi.cnt_dc = (bi.cnt_dc & 0xFC000000u) | (uint32_t(v) & 0x3FFFFFFu);
-            b.blocks[S.blk0 + j] = bi;
+// DC prediction (parser.cpp:106-111: per component, the predictor restarts at 0 at every
+// interval) is a segmented prefix sum of the DC differences the write pass stores.  It is folded
+// into k_idct_color, whose tile is a run of consecutive MCUs of one MCU row (its lanes scan their
+// own blocks); the two kernels below give every tile its predictors at entry.
+//
+// Lane = block of a tile (TR = 1: tile_mcus consecutive MCUs): DC difference, component, and
+// whether the block starts an interval (first block of an MCU whose index is a multiple of DRI).
+struct TileLane {
+    int d;
+    uint32_t comp;
+    bool have, start;
+};
+__device__ __forceinline__ TileLane tile_lane(const BatchDev& b, const ImgDesc& im, uint32_t tile, uint32_t lane) {
+    const uint32_t ty = tile / im.tiles_x, tx = tile - ty * im.tiles_x;
+    const uint32_t m0 = tx * im.tile_mcus, nm = min(im.tile_mcus, im.mcux - m0);
+    const uint32_t m = lane / im.bpm, bb = lane - m * im.bpm;
+    TileLane t;
+    t.have = m < nm;
+    t.comp = (im.block_pattern >> (2 * bb)) & 3u;
+    const uint32_t g = ty * im.mcux + m0 + m;  // raster MCU index
+    t.start = t.have && bb == 0 && (im.restart_interval ? g % im.restart_interval == 0 : g == 0);
+    t.d = 0;
+    if (t.have) t.d = int32_t(b.blocks[im.block_base + uint64_t(g) * im.bpm + bb].cnt_dc << 6) >> 6;
+    return t;
+}
+
+// Wave per tile: the per-component sums of the differences after the tile's last interval start
+// (all of them when it has none) and whether it has one.
+__global__ __launch_bounds__(256) void k_dc_sum(BatchDev b) {
+    const ImgDesc& im = b.imgs[blockIdx.y];
+    const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (tile >= im.tiles_x * im.tiles_y) return;  // wave-uniform
+    const TileLane t = tile_lane(b, im, tile, lane);
+    const uint64_t mask = __ballot(t.start);
+    const uint32_t last = mask ? 63u - uint32_t(__clzll(mask)) : 0u;
+    const bool after = lane >= last;
+    const int s0 = wave_scan_dpp(after && t.comp == 0 ? t.d : 0);
+    const int s1 = wave_scan_dpp(after && t.comp == 1 ? t.d : 0);
+    const int s2 = wave_scan_dpp(after && t.comp == 2 ? t.d : 0);
+    if (lane == 63) b.tile_dc[im.tile_base + tile] = DcPred{s0, s1, s2, mask ? 1 : 0};
+}
+
+// Wave per image: segmented exclusive scan over its tiles in raster order, in place: tile_dc
+// becomes the predictor of each component at the tile's first block.
+__global__ __launch_bounds__(64) void k_dc_scan(BatchDev b) {
+    const ImgDesc& im = b.imgs[blockIdx.x];
+    const uint32_t lane = threadIdx.x, nt = im.tiles_x * im.tiles_y;
+    int c0 = 0, c1 = 0, c2 = 0;
+    for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
+        const uint32_t t = t0 + lane;
+        const DcPred a = t < nt ? b.tile_dc[im.tile_base + t] : DcPred{0, 0, 0, 0};
+        int v0 = a.p0, v1 = a.p1, v2 = a.p2, f = a.flag;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {  // (f, v) o (g, w) = (f | g, g ? w : v + w)
+            const int n0 = __shfl_up(v0, d, 64), n1 = __shfl_up(v1, d, 64), n2 = __shfl_up(v2, d, 64);
+            const int nf = __shfl_up(f, d, 64);
+            if (int(lane) >= d && !f) {
+                v0 += n0;
+                v1 += n1;
+                v2 += n2;
+                f = nf;
+            }
         }
-        run0 += __shfl(i0, 63, 64);
-        run1 += __shfl(i1, 63, 64);
-        run2 += __shfl(i2, 63, 64);
-        bb0 = (bb0 + 64) % S.bpm;
+        if (!f) {  // no interval start in this chunk up to here: continue the carried predictors
+            v0 += c0;
+            v1 += c1;
+            v2 += c2;
+        }
+        int e0 = __shfl_up(v0, 1, 64), e1 = __shfl_up(v1, 1, 64), e2 = __shfl_up(v2, 1, 64);
+        if (lane == 0) {
+            e0 = c0;
+            e1 = c1;
+            e2 = c2;
+        }
+        if (t < nt) b.tile_dc[im.tile_base + t] = DcPred{e0, e1, e2, 0};
+        c0 = __shfl(v0, 63, 64);
+        c1 = __shfl(v1, 63, 64);
+        c2 = __shfl(v2, 63, 64);
     }
-    if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1153,6 +1268,116 @@ __device__ __forceinline__ void idct_col(int* blk) {
     blk[8 * 5] = clip256((x0 - x4) >> 14);
     blk[8 * 6] = clip256((x3 - x2) >> 14);
     blk[8 * 7] = clip256((x7 - x1) >> 14);
+}
+
+// The IDCT the decode path runs (idct.cpp:34-122), in two forms:
+//
+//  * fast: every constant multiply on a single input (C7 (x4 + x5) + (C1 - C7) x4 = C1 x4 + C7 x5
+//    and so on: equal in int32 arithmetic, which is arithmetic mod 2^32), each one full-rate
+//    v_mul/v_mad_i32_i24 instead of a quarter-rate v_mul_lo_u32 on a sum.  Exact when every
+//    multiplied input fits 24 signed bits: with all dequantised coefficients within +-2^16 the
+//    row inputs do and the row outputs stay within +-6.7e6 < 2^23 (interval bound of the row
+//    pass), so the column inputs do too.  Within that range the reference's DC-only shortcuts
+//    (idct.cpp:38-41, 83-86) equal the general formulas (no shift overflows), so the fast form is
+//    branch-free.
+//  * exact: the general formulas plus the shortcuts, selected per row / column exactly as the
+//    reference tests them (including a block[4] << 11 that wraps to 0): any int32 input.
+//
+// k_idct_color takes the fast form when every lane of the wave is in range (wave-uniform), which
+// real images always are; tests/test_gpu.py::test_idct_kat covers both over int32 inputs.
+__device__ __forceinline__ void idct_row_fast(int* blk) {
+    const int x1 = blk[4] << 11, x0 = (blk[0] << 11) + 128;
+    const int b1 = blk[1], b2 = blk[2], b3 = blk[3], b5 = blk[5], b6 = blk[6], b7 = blk[7];
+    int x4 = __mul24(b1, kC1) + __mul24(b7, kC7);
+    int x5 = __mul24(b1, kC7) + __mul24(b7, -kC1);
+    int x6 = __mul24(b5, kC5) + __mul24(b3, kC3);
+    int x7 = __mul24(b5, kC3) + __mul24(b3, -kC5);
+    int x2 = __mul24(b2, kC6) + __mul24(b6, -kC2);
+    int x3 = __mul24(b2, kC2) + __mul24(b6, kC6);
+    int x8 = x0 + x1;
+    int y0 = x0 - x1;
+    const int y1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = y0 + x2;
+    y0 -= x2;
+    x2 = (181 * (x4 + x5) + 128) >> 8;
+    x4 = (181 * (x4 - x5) + 128) >> 8;
+    blk[0] = (x7 + y1) >> 8;
+    blk[1] = (x3 + x2) >> 8;
+    blk[2] = (y0 + x4) >> 8;
+    blk[3] = (x8 + x6) >> 8;
+    blk[4] = (x8 - x6) >> 8;
+    blk[5] = (y0 - x4) >> 8;
+    blk[6] = (x3 - x2) >> 8;
+    blk[7] = (x7 - y1) >> 8;
+}
+
+__device__ __forceinline__ void idct_col_fast(int* blk) {
+    const int x1 = blk[8 * 4] << 8, x0 = (blk[0] << 8) + 8192;
+    const int b1 = blk[8 * 1], b2 = blk[8 * 2], b3 = blk[8 * 3], b5 = blk[8 * 5], b6 = blk[8 * 6], b7 = blk[8 * 7];
+    int x4 = (__mul24(b1, kC1) + __mul24(b7, kC7) + 4) >> 3;
+    int x5 = (__mul24(b1, kC7) + __mul24(b7, -kC1) + 4) >> 3;
+    int x6 = (__mul24(b5, kC5) + __mul24(b3, kC3) + 4) >> 3;
+    int x7 = (__mul24(b5, kC3) + __mul24(b3, -kC5) + 4) >> 3;
+    int x2 = (__mul24(b2, kC6) + __mul24(b6, -kC2) + 4) >> 3;
+    int x3 = (__mul24(b2, kC2) + __mul24(b6, kC6) + 4) >> 3;
+    int x8 = x0 + x1;
+    int y0 = x0 - x1;
+    const int y1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = y0 + x2;
+    y0 -= x2;
+    x2 = (181 * (x4 + x5) + 128) >> 8;
+    x4 = (181 * (x4 - x5) + 128) >> 8;
+    blk[8 * 0] = clip256((x7 + y1) >> 14);
+    blk[8 * 1] = clip256((x3 + x2) >> 14);
+    blk[8 * 2] = clip256((y0 + x4) >> 14);
+    blk[8 * 3] = clip256((x8 + x6) >> 14);
+    blk[8 * 4] = clip256((x8 - x6) >> 14);
+    blk[8 * 5] = clip256((y0 - x4) >> 14);
+    blk[8 * 6] = clip256((x3 - x2) >> 14);
+    blk[8 * 7] = clip256((x7 - y1) >> 14);
+}
+
+__device__ __forceinline__ void idct_row_exact(int* blk) {
+    const bool dc_only = ((blk[4] << 11) | blk[6] | blk[2] | blk[1] | blk[7] | blk[5] | blk[3]) == 0;
+    const int s = blk[0] << 3;
+    idct_row(blk);
+#pragma unroll
+    for (int k = 0; k < 8; k++) blk[k] = dc_only ? s : blk[k];
+}
+
+__device__ __forceinline__ void idct_col_exact(int* blk) {
+    const bool dc_only = ((blk[8 * 4] << 8) | blk[8 * 6] | blk[8 * 2] | blk[8 * 1] | blk[8 * 7] | blk[8 * 5] | blk[8 * 3]) == 0;
+    const int s = clip256((blk[0] + 32) >> 6);
+    idct_col(blk);
+#pragma unroll
+    for (int k = 0; k < 8; k++) blk[8 * k] = dc_only ? s : blk[8 * k];
+}
+
+// Both forms on a block of dequantised coefficients in natural order (blk[0] = DC); fast when
+// the caller knows every coefficient is within +-2^16.  The decode path instantiates them in
+// different kernels (k_idct_color / k_idct_color_exact): together they would make it spill.
+__device__ __forceinline__ void idct_block(int (&blk)[64], bool fast) {
+    if (fast) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) idct_row_fast(blk + 8 * r);
+#pragma unroll
+        for (int c = 0; c < 8; c++) idct_col_fast(blk + c);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 8; r++) idct_row_exact(blk + 8 * r);
+#pragma unroll
+        for (int c = 0; c < 8; c++) idct_col_exact(blk + c);
+    }
 }
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
@@ -1351,13 +1576,17 @@ __device__ __forceinline__ size_t fancy_plane_off(const ImgDesc& im, uint32_t c)
     return off;
 }
 
-__global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
-    // staging (64 rows of 66 int16 = 33 words: odd pitch, conflict-free read-back) and then the
-    // component planes share s_buf; planes need at most 64*64 + 64*2*6 int16 (§ host tile choice)
-    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2464];
-    __shared__ int s_qz[3 * 65];  // quant step per component, zig-zag order (pitch 65: no bank clash)
-    const ImgDesc& im = b.imgs[blockIdx.y];
-    const uint32_t tile = blockIdx.x;
+// staging (64 rows of 66 int16 = 33 words: odd pitch, conflict-free read-back) and then the
+// component planes share s_buf; planes need at most 64*64 + 64*2*6 int16 (§ host tile choice)
+constexpr int kIdctBufWords = 2464;
+constexpr int kQzWords = 3 * 65;  // quant step per component, zig-zag order (pitch 65: no bank clash)
+
+// One tile.  EXACT = false (k_idct_color): a wave with a coefficient beyond the fast IDCT's range
+// (never seen in real images) appends its tile to slow_tiles and leaves; EXACT = true
+// (k_idct_color_exact) decodes those tiles with the exact IDCT form.
+template <bool EXACT>
+__device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint32_t tile, uint32_t* s_buf, int* s_qz) {
+    const ImgDesc& im = b.imgs[img];
     const uint32_t tiles_x = im.tiles_x;
     if (tile >= tiles_x * im.tiles_y) return;
     const uint32_t lane = threadIdx.x;
@@ -1381,13 +1610,37 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     const bool have = mr < nr && mi < nm;
     const uint32_t comp = (im.block_pattern >> (2 * bb)) & 3u;
     int16_t* row = reinterpret_cast<int16_t*>(s_buf + lane * kRow16);
+    const BlockInfo bi =
+        have ? b.blocks[im.block_base + uint64_t((r0 + mr) * im.mcux + m0 + mi) * bpm + bb] : BlockInfo{0u, 0u};
+    int dc_pred;
+    {  // DC prediction: segmented scan of the tile's DC differences onto its entry predictors
+        // (tile_dc, k_dc_scan); a block that starts an interval resets its component's predictor
+        const int d = have ? int32_t(bi.cnt_dc << 6) >> 6 : 0;
+        const uint32_t g = (r0 + mr) * im.mcux + m0 + mi;
+        const bool start = have && bb == 0 && (im.restart_interval ? g % im.restart_interval == 0 : g == 0);
+        const uint64_t smask = __ballot(start);
+        const int p0 = wave_scan_dpp(comp == 0 ? d : 0);
+        const int p1 = wave_scan_dpp(comp == 1 ? d : 0);
+        const int p2 = wave_scan_dpp(comp == 2 ? d : 0);
+        const DcPred cin = b.tile_dc[im.tile_base + tile];
+        int dc = comp == 0 ? p0 : (comp == 1 ? p1 : p2);
+        const uint64_t upto = smask & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+        if (upto == 0) {
+            dc += comp == 0 ? cin.p0 : (comp == 1 ? cin.p1 : cin.p2);
+        }
+        if (smask & ~1ull) {  // wave-uniform: an interval starts inside the tile
+            const int ls = upto ? 63 - int(__clzll(upto)) : 0;  // my segment's first lane
+            const int src = max(ls - 1, 0);
+            const int q0 = __shfl(p0, src, 64), q1 = __shfl(p1, src, 64), q2 = __shfl(p2, src, 64);
+            if (upto && ls > 0) dc -= comp == 0 ? q0 : (comp == 1 ? q1 : q2);
+        }
+        dc_pred = dc;  // exact int, as the reference's int predictor (parser.cpp:106-111): the
+                       // staging below is int16, so DC bypasses it
+    }
     if (have) {
-        const uint64_t gb = im.block_base + uint64_t((r0 + mr) * im.mcux + m0 + mi) * bpm + bb;
-        const BlockInfo bi = b.blocks[gb];
         // a block of a corrupt stream may never have been written: never index past the entries
         int cnt = int(bi.cnt_dc >> 26);
         if (uint64_t(bi.entry_start) + uint64_t(cnt) > b.entries_cap) cnt = 0;
-        row[0] = int16_t(int32_t(bi.cnt_dc << 6) >> 6);  // DC: int16 by k_dpcm's range check
         // entries in 16-byte loads, four in flight at a time (the entry buffer is padded by 64 B)
         const uint32_t lead = bi.entry_start & 3u;
         const uint32_t* ep = b.entries + (bi.entry_start - lead);
@@ -1415,22 +1668,37 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
 
     // 2. dequantise in zig-zag order (24-bit multiplies: |coef| < 2^15, q < 2^16) into natural
     //    positions (a compile-time permutation of registers), then the IDCT in registers
-    int blk[64];
-    {
-        const uint32_t* rw = s_buf + lane * kRow16;
-        const int* qz = s_qz + comp * 65;
+    //    The fast IDCT form needs every dequantised coefficient within +-2^16: an AC coefficient
+    //    c is when |c| <= 2^(k-1) with 2^(k-1) * (largest quant step) < 2^16 (host: im.qmask),
+    //    i.e. when bits k-1..15 of c all equal its sign: c ^ (c << 1) has bits k..15 clear.
+    const uint32_t* rw = s_buf + lane * kRow16;
+    const int* qz = s_qz + comp * 65;
+    const int dq0 = dc_pred * qz[0];
+    if (!EXACT) {  // range test before dequantising: the branch then holds no 64-value block
+        uint32_t acc = 0;
 #pragma unroll
         for (int p = 0; p < 32; p++) {
             const uint32_t w = rw[p];
-            blk[kNatOfZz[2 * p]] = __mul24(int(int16_t(w & 0xFFFFu)), qz[2 * p]);
-            blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, qz[2 * p + 1]);
+            acc |= w ^ (w << 1);
+        }
+        const bool in_range = !have || ((acc & im.qmask) == 0 && uint32_t(dq0 + 65536) <= 131072u);
+        if (!__all(in_range)) {  // wave-uniform
+            if (lane == 0) {
+                const uint32_t k = uint32_t(atomicAdd(&b.counters[1], 1ull));
+                b.slow_tiles[k] = TileRef{img, tile};
+            }
+            return;
         }
     }
+    int blk[64];
+#pragma unroll
+    for (int p = 0; p < 32; p++) {
+        const uint32_t w = rw[p];
+        blk[kNatOfZz[2 * p]] = p == 0 ? dq0 : __mul24(int(int16_t(w & 0xFFFFu)), qz[2 * p]);
+        blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, qz[2 * p + 1]);
+    }
 #if !(JD_ABL & 2)
-#pragma unroll
-    for (int r = 0; r < 8; r++) idct_row(blk + 8 * r);
-#pragma unroll
-    for (int c = 0; c < 8; c++) idct_col(blk + c);
+    idct_block(blk, !EXACT);
 #endif
     if (b.fancy) {  // wave-uniform: component planes to HBM, k_colour_fancy takes it from there
         if (have) {
@@ -1548,6 +1816,23 @@ __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     }
 }
 
+__global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
+    __shared__ int s_qz[kQzWords];
+    idct_tile<false>(b, blockIdx.y, blockIdx.x, s_buf, s_qz);
+}
+
+// The tiles k_idct_color left (grid-stride over the list; empty in practice).
+__global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
+    __shared__ int s_qz[kQzWords];
+    const uint32_t n = uint32_t(min(b.counters[1], (unsigned long long)b.total_tiles));
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const TileRef t = b.slow_tiles[i];
+        idct_tile<true>(b, t.img, t.tile, s_buf, s_qz);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Fancy upsampling + colour (JD_FLAG_FANCY_UPSAMPLING), lane = 8 consecutive pixels of a row.
 // The triangular filters of libjpeg (jdsample.c h2v1 / h2v2 / h1v2 fancy upsampling) on the
@@ -1622,13 +1907,20 @@ __global__ __launch_bounds__(256) void k_colour_fancy(BatchDev b) {
 // ------------------------------------------------------------------------------------------
 // Known-answer hooks
 // ------------------------------------------------------------------------------------------
-__global__ void k_test_idct(const int32_t* in_zz, int32_t* out, int n) {
+// exact_only = 0: the decode path's choice per block (fast form when every input is within
+// +-2^16); 1: the exact form whatever the inputs.
+__global__ void k_test_idct(const int32_t* in_zz, int32_t* out, int n, int exact_only) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int blk[64];
-    for (int z = 0; z < 64; z++) blk[kNatOfZz[z]] = in_zz[size_t(i) * 64 + z];
-    for (int r = 0; r < 8; r++) idct_row(blk + 8 * r);
-    for (int c = 0; c < 8; c++) idct_col(blk + c);
+    bool in_range = !exact_only;
+#pragma unroll
+    for (int z = 0; z < 64; z++) {
+        blk[kNatOfZz[z]] = in_zz[size_t(i) * 64 + z];
+        in_range = in_range && uint32_t(blk[kNatOfZz[z]] + 65536) <= 131072u;
+    }
+    idct_block(blk, in_range);
+#pragma unroll
     for (int z = 0; z < 64; z++) out[size_t(i) * 64 + z] = blk[z];
 }
 
@@ -1673,14 +1965,22 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             if (b.nsub) hipLaunchKernelGGL(k_rescan, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 6:
-            if (b.nchain) hipLaunchKernelGGL(k_chain, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            if (!b.nseg) break;
+            hipLaunchKernelGGL(k_chain, dim3((b.nseg + 3) / 4), dim3(256), 0, s, b);
+            if (b.nchain) hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 7:
             if (b.nsub) hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
-        case 8: hipLaunchKernelGGL(k_dpcm, dim3(b.nseg), dim3(64), 0, s, b); break;
+        case 8:
+            if (!b.max_tiles) break;
+            hipLaunchKernelGGL(k_dc_sum, dim3((b.max_tiles + 3) / 4, b.nimg), dim3(256), 0, s, b);
+            hipLaunchKernelGGL(k_dc_scan, dim3(b.nimg), dim3(64), 0, s, b);
+            break;
         case 9:
-            if (b.max_tiles) hipLaunchKernelGGL(k_idct_color, dim3(b.max_tiles, b.nimg), dim3(kIdctThreads), 0, s, b);
+            if (!b.max_tiles) break;
+            hipLaunchKernelGGL(k_idct_color, dim3(b.max_tiles, b.nimg), dim3(kIdctThreads), 0, s, b);
+            hipLaunchKernelGGL(k_idct_color_exact, dim3(1024), dim3(kIdctThreads), 0, s, b);
             break;
         case 10:
             if (b.fancy && b.max_fancy_wgs) hipLaunchKernelGGL(k_colour_fancy, dim3(b.max_fancy_wgs, b.nimg), dim3(256), 0, s, b);
@@ -1690,8 +1990,8 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_test_idct(const int32_t* in_zz, int32_t* out, int n, hipStream_t s) {
-    hipLaunchKernelGGL(k_test_idct, dim3((n + 63) / 64), dim3(64), 0, s, in_zz, out, n);
+hipError_t launch_test_idct(const int32_t* in_zz, int32_t* out, int n, int exact_only, hipStream_t s) {
+    hipLaunchKernelGGL(k_test_idct, dim3((n + 63) / 64), dim3(64), 0, s, in_zz, out, n, exact_only);
     return hipGetLastError();
 }
 

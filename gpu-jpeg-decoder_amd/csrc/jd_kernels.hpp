@@ -9,12 +9,12 @@ namespace jd {
 
 // The decode pipeline, kernel by kernel (jd_kernel_name(k) names them; DESIGN.md §4 describes
 // each):  0 k_scan, 1 k_index, 2 k_compact (un-stuffing), 3 k_subplan, 4 k_piece_scan,
-// 5 k_rescan, 6 k_chain, 7 k_piece_write (Huffman), 8 k_dpcm, 9 k_idct_color.
+// 5 k_rescan, 6 k_chain, 7 k_piece_write (Huffman), 8 k_dc_pred, 9 k_idct_color.
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s);
 size_t huffman_lds_bytes(uint32_t max_slots);
 
 // Known-answer hooks: run exactly the device arithmetic of stage 3 on caller data.
-hipError_t launch_test_idct(const int32_t* in_zz, int32_t* out, int nblocks, hipStream_t s);
+hipError_t launch_test_idct(const int32_t* in_zz, int32_t* out, int nblocks, int exact_only, hipStream_t s);
 hipError_t launch_test_color(const int32_t* ycc, uint8_t* rgb, int n, hipStream_t s);
 
 }  // namespace jd

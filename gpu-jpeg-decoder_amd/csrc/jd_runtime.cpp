@@ -232,7 +232,7 @@ struct Plan {
     std::vector<uint32_t> seg_img, seg_entry, wg_tableset;
     uint32_t piece_bits = kPieceBits;
     std::vector<uint32_t> chain_seg, chain_wg_tableset;  // k_chain lanes, grouped by table set
-    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, max_slots = 1, nsub = 0;
+    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0;
     uint64_t total_blocks = 0, total_entry_cap = 0, comp_bytes = 0;
     double pixels = 0, ecs_bytes = 0;
 };
@@ -284,6 +284,15 @@ void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uin
         for (int j = 0; j < h.h[c] * h.v[c]; j++, b++) pat |= uint32_t(c) << (2 * b);
         d.qslot[c] = pi.qslot[c];
     }
+    {  // k_idct_color's fast-IDCT range test: |c| <= 2^(k-1) keeps |c * step| < 2^16
+        uint32_t qmax = 1;
+        for (int c = 0; c < h.ncomp; c++)
+            for (int k = 0; k < 64; k++) qmax = std::max<uint32_t>(qmax, pj.q[h.tq[c]][k]);
+        uint32_t k = 1;
+        while (k < 16 && (uint64_t(1) << k) * qmax < 65536) k++;  // largest k: 2^(k-1) * qmax < 2^16
+        const uint32_t lo = (0xFFFFu << k) & 0xFFFFu;
+        d.qmask = lo | (lo << 16);
+    }
     d.block_pattern = pat;
     d.restart_interval = uint32_t(h.restart_interval);
     d.nseg = pi.nseg;
@@ -296,15 +305,9 @@ void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uin
         while ((8u << lh) < 8u * d.vmax) lh++;
         d.lg_mw = 3 + lw;
         d.lg_mh = 3 + lh;
-        uint32_t best = 0;
-        for (uint32_t tr = 1; tr <= 2; tr++) {
-            const uint32_t tm = std::max(1u, uint32_t(kTileMaxBlocks) / (tr * d.bpm));
-            if (tm * tr * d.bpm > best) {
-                best = tm * tr * d.bpm;
-                d.tile_mcus = tm;
-                d.tile_mrows = tr;
-            }
-        }
+        // a run of consecutive MCUs of one MCU row (k_idct_color's DC prediction scans it in order)
+        d.tile_mcus = std::max(1u, uint32_t(kTileMaxBlocks) / d.bpm);
+        d.tile_mrows = 1;
         d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
         d.tiles_y = (d.mcuy + d.tile_mrows - 1) / d.tile_mrows;
         for (int c = 0; c < h.ncomp; c++) {
@@ -461,7 +464,11 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             }
         }
     });
-    for (const ImgDesc& d : P.imgs) P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.tiles_y);
+    for (ImgDesc& d : P.imgs) {
+        d.tile_base = P.total_tiles;
+        P.total_tiles += d.tiles_x * d.tiles_y;
+        P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.tiles_y);
+    }
     const double tb_segs = tbms();
     // 3. piece slots: per image ceil(ECS bits / piece_bits) + nseg (interval lengths are only known
     // on the GPU), grouped by table set so each k_piece workgroup stages one table set
@@ -604,6 +611,9 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         size_t o_piece[6];
         for (int q = 0; q < 6; q++) o_piece[q] = reserve(end, nsub * 4);
         const size_t o_cp = reserve(end, nsub * kCpRecords * sizeof(CpRec));
+        const size_t o_fix = reserve(end, nseg * 4);
+        const size_t o_tdc = reserve(end, size_t(P.total_tiles) * sizeof(DcPred));
+        const size_t o_slow = reserve(end, size_t(P.total_tiles) * 8);
         HIPCHK(ctx, ensure_dev(ctx->plan, end));
         HIPCHK(ctx, ensure_pin(ctx->plan_host, upload));
         memcpy(ctx->plan_host.p, blob.data(), upload);
@@ -645,6 +655,10 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         b.piece_mcu0 = pc[4];
         b.piece_ent0 = pc[5];
         b.piece_cp = reinterpret_cast<CpRec*>(base + o_cp);
+        b.seg_fix = reinterpret_cast<uint32_t*>(base + o_fix);
+        b.tile_dc = reinterpret_cast<DcPred*>(base + o_tdc);
+        b.slow_tiles = reinterpret_cast<TileRef*>(base + o_slow);
+        b.total_tiles = P.total_tiles;
         b.max_slots = P.max_slots;
         b.max_chunks = P.max_chunks;
         b.chunk_nbrk = reinterpret_cast<uint32_t*>(base + o_nbrk);
@@ -705,7 +719,7 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
             nsubd * 8,                                         // k_rescan: start/end check per piece
             nsubd * 28,                                        // k_chain: counts in, offsets out
             ecs + blocks * 8 + entries * 4,                    // k_piece_write: ECS in, sparse coefficients out
-            blocks * 16,                                       // k_dpcm: BlockInfo read + write
+            blocks * 8 + double(P.total_tiles) * 48,           // k_dc_pred: BlockInfo read, tile sums, scan
             blocks * 8 + entries * 4 + (fancy ? blocks * 128 : P.pixels * 3),  // k_idct_color: coefficients in,
                                                                                 // RGB (fancy: planes) out
             fancy ? blocks * 128 + P.pixels * 3 : 0.0};        // k_colour_fancy: planes in, RGB out
@@ -770,7 +784,7 @@ const char* jd_ctx_last_error(jd_ctx* ctx) { return ctx ? ctx->last_error.c_str(
 
 const char* jd_kernel_name(int k) {
     static const char* names[JD_NUM_KERNELS] = {"k_scan",      "k_index", "k_compact",     "k_subplan", "k_piece_scan",
-                                                "k_rescan",    "k_chain", "k_piece_write", "k_dpcm",    "k_idct_color", "k_colour_fancy"};
+                                                "k_rescan",    "k_chain", "k_piece_write", "k_dc_pred", "k_idct_color", "k_colour_fancy"};
     return (k >= 0 && k < JD_NUM_KERNELS) ? names[k] : "?";
 }
 
@@ -979,7 +993,14 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
 
 jd_status jd_test_idct(jd_ctx* ctx, const int32_t* in_dev, int32_t* out_dev, int nblocks) {
     if (!ctx || !in_dev || !out_dev || nblocks < 0) return JD_ERR_INVALID_ARG;
-    HIPCHK(ctx, launch_test_idct(in_dev, out_dev, nblocks, ctx->stream));
+    HIPCHK(ctx, launch_test_idct(in_dev, out_dev, nblocks, 0, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return JD_OK;
+}
+
+jd_status jd_test_idct_exact(jd_ctx* ctx, const int32_t* in_dev, int32_t* out_dev, int nblocks) {
+    if (!ctx || !in_dev || !out_dev || nblocks < 0) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, launch_test_idct(in_dev, out_dev, nblocks, 1, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return JD_OK;
 }

@@ -35,7 +35,7 @@ PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES}
 JD_ABI_VERSION = 2
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece_scan", "k_rescan", "k_chain",
-                "k_piece_write", "k_dpcm", "k_idct_color", "k_colour_fancy"]
+                "k_piece_write", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
 
 
 class JDError(RuntimeError):
@@ -79,7 +79,7 @@ EXPORTED_SYMBOLS = [
     "jd_ctx_create", "jd_ctx_destroy", "jd_parse", "jd_decode", "jd_decode_file", "jd_decode_batch",
     "jd_write_array", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
     "jd_memcpy_h2d", "jd_memcpy_d2h", "jd_synchronize", "jd_get_stats", "jd_reset_stats",
-    "jd_kernel_name", "jd_test_idct", "jd_test_color", "jd_debug_fetch", "jd_ctx_last_error",
+    "jd_kernel_name", "jd_test_idct", "jd_test_idct_exact", "jd_test_color", "jd_debug_fetch", "jd_ctx_last_error",
 ]
 
 _lib = None
@@ -117,6 +117,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         "jd_reset_stats": (c_int, [c_void_p]),
         "jd_kernel_name": (ctypes.c_char_p, [c_int]),
         "jd_test_idct": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+        "jd_test_idct_exact": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
         "jd_test_color": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
         "jd_debug_fetch": (c_int, [c_void_p, c_int, c_void_p, c_size_t, ctypes.POINTER(c_size_t)]),
         "jd_ctx_last_error": (ctypes.c_char_p, [c_void_p]),
@@ -368,12 +369,15 @@ class Decoder:
             raise JDError(st, "jd_debug_fetch " + self.last_error())
         return out.reshape(-1, width) if width > 1 else out
 
-    def test_idct(self, zz_dequant: np.ndarray) -> np.ndarray:
+    def test_idct(self, zz_dequant: np.ndarray, exact_only: bool = False) -> np.ndarray:
+        """The device IDCT on dequantised zig-zag blocks: the decode path's per-block choice of form,
+        or (exact_only) the exact form whatever the inputs."""
         a = np.ascontiguousarray(zz_dequant, dtype=np.int32).reshape(-1, 64)
         n = a.shape[0]
         din, dout = self.alloc(a.nbytes), self.alloc(a.nbytes)
         din.upload(a)
-        st = self.lib.jd_test_idct(self.ctx, din.ptr, dout.ptr, n)
+        fn = self.lib.jd_test_idct_exact if exact_only else self.lib.jd_test_idct
+        st = fn(self.ctx, din.ptr, dout.ptr, n)
         if st != JD_OK:
             raise JDError(st, "jd_test_idct")
         out = dout.download(np.empty((n, 64), np.int32))

@@ -136,7 +136,7 @@ jd_status jd_synchronize(jd_ctx* ctx);
 
 /* Per-kernel timing (JD_FLAG_TIMING).
  * Kernels: 0 k_scan, 1 k_index, 2 k_compact, 3 k_subplan, 4 k_piece_scan, 5 k_rescan, 6 k_chain,
- * 7 k_piece_write, 8 k_dpcm, 9 k_idct_color. */
+ * 7 k_piece_write, 8 k_dc_pred, 9 k_idct_color. */
 #define JD_NUM_KERNELS 11
 typedef struct jd_stats {
     int launches[JD_NUM_KERNELS];

@@ -17,6 +17,10 @@ extern "C" {
 
 /* in: nblocks x 64 dequantised coefficients in zig-zag order; out: nblocks x 64 natural order */
 jd_status jd_test_idct(jd_ctx* ctx, const int32_t* in_dev, int32_t* out_dev, int nblocks);
+/* jd_test_idct runs the decode path's choice per block: the fast 24-bit-multiply form when every
+ * input is within +-2^16, else the exact form (the reference's formulas with its DC-only
+ * shortcuts, any int32 input).  jd_test_idct_exact forces the exact form. */
+jd_status jd_test_idct_exact(jd_ctx* ctx, const int32_t* in_dev, int32_t* out_dev, int nblocks);
 /* ycc: n x (Y, Cb, Cr) IDCT outputs in [-256,255]; rgb: n x 3 bytes */
 jd_status jd_test_color(jd_ctx* ctx, const int32_t* ycc_dev, uint8_t* rgb_dev, int n);
 

@@ -118,6 +118,28 @@ def test_idct_kat(decoder):
     assert np.array_equal(got, want)
 
 
+def test_idct_both_forms_over_int32(decoder):
+    """The fast form (24-bit multiplies, taken when every input is within +-2^16) and the exact form
+    (the reference's formulas and DC-only shortcuts, any int32 input; the oracle wraps like the
+    GPU, -fwrapv) against the oracle, at and beyond the fast form's range."""
+    rng = np.random.default_rng(2)
+    n = 40000
+    edge = rng.integers(-65536, 65537, (n, 64)).astype(np.int32)          # fast form, dense
+    edge[: n // 2][rng.random((n // 2, 64)) < 0.85] = 0
+    edge[:64] = np.where(rng.random((64, 64)) < 0.5, 65536, -65536)      # the range's corners
+    wide = rng.integers(-2**31, 2**31, (n, 64), dtype=np.int64).astype(np.int32)
+    wide[: n // 2][rng.random((n // 2, 64)) < 0.9] = 0                    # exact form, shortcuts
+    dc = np.zeros((4096, 64), np.int32)
+    dc[:, 0] = rng.integers(-2**31, 2**31, 4096, dtype=np.int64)          # DC-only rows and columns
+    wrap = np.zeros((64, 64), np.int32)
+    wrap[:, 14] = (np.arange(64) - 32) * (1 << 21)                         # block[4] << 11 wraps to 0
+    wrap[:, 0] = rng.integers(-5000, 5000, 64)
+    a = np.concatenate([edge, wide, dc, wrap])
+    want = jdoracle.idct(a)
+    assert np.array_equal(decoder.test_idct(a), want)
+    assert np.array_equal(decoder.test_idct(a, exact_only=True), want)
+
+
 def test_color_exhaustive(decoder):
     """All 2^27 (Y, Cb, Cr) in [-256, 255]^3 against utils/color.cpp's double/float formula
     (restated in numpy, float32/float64 exactly as the reference rounds)."""
@@ -165,3 +187,54 @@ def test_cli_array_matches_reference_format(tmp_path, golden):
     got = open(tmp_path / "3_120x120.array", "rb").read()
     want = open(os.path.join(ROOT, "tests", "golden", "ref", "3_120x120.array"), "rb").read()
     assert got == want
+
+
+def _dc_ramp_jpeg(nblocks: int, dri: int) -> bytes:
+    """A grayscale 8 x 8*nblocks baseline JPEG whose every block has DC difference +2047 and no AC
+    (one-symbol DC and AC tables, unit quantisation): the DC leaves int16 after 17 blocks unless
+    restart intervals of `dri` MCUs reset the predictor first."""
+    bits = []
+
+    def put(v, n):
+        bits.extend((v >> (n - 1 - k)) & 1 for k in range(n))
+
+    ecs = bytearray()
+
+    def flush():
+        while len(bits) % 8:
+            bits.append(1)
+        for i in range(0, len(bits), 8):
+            byte = int("".join(map(str, bits[i:i + 8])), 2)
+            ecs.append(byte)
+            if byte == 0xFF:
+                ecs.append(0)
+        bits.clear()
+
+    for k in range(nblocks):
+        if dri and k and k % dri == 0:
+            flush()
+            ecs += bytes([0xFF, 0xD0 + (k // dri - 1) % 8])
+        put(0, 1)          # DC code '0' -> size 11
+        put(2047, 11)      # +2047
+        put(0, 1)          # AC code '0' -> EOB
+    flush()
+    seg = lambda m, body: bytes([0xFF, m]) + (len(body) + 2).to_bytes(2, "big") + body
+    out = b"\xff\xd8" + seg(0xDB, b"\x00" + bytes([1] * 64))
+    out += seg(0xC0, b"\x08" + (8).to_bytes(2, "big") + (8 * nblocks).to_bytes(2, "big") + b"\x01\x01\x11\x00")
+    out += seg(0xC4, b"\x00" + bytes([1] + [0] * 15) + b"\x0b")  # DC table 0: one 1-bit code, symbol 11
+    out += seg(0xC4, b"\x10" + bytes([1] + [0] * 15) + b"\x00")  # AC table 0: one 1-bit code, EOB
+    if dri:
+        out += seg(0xDD, dri.to_bytes(2, "big"))
+    out += seg(0xDA, b"\x01\x01\x00\x00\x3f\x00") + bytes(ecs) + b"\xff\xd9"
+    return out
+
+
+@pytest.mark.parametrize("nblocks,dri", [(20, 0), (16, 0), (20, 8), (150, 5), (150, 16), (150, 17)])
+def test_dc_prediction_beyond_int16_and_resets(decoder, nblocks, dri):
+    """DC predictor values beyond int16 decode with the reference's int arithmetic (its
+    predictor and dequantisation are int, parser.cpp:106-111), and the predictor restarts at
+    every restart interval, including intervals that start inside an IDCT tile."""
+    data = _dc_ramp_jpeg(nblocks, dri)
+    ost, ref = jdoracle.decode(data)
+    assert ost == 0
+    assert np.array_equal(decoder.decode(data), ref)

@@ -6,7 +6,8 @@ some need the chain's re-scan.
   seg_cstart/seg_cend          -> un-stuffed interval lengths
   piece_bit/mcu0/ent0          -> every piece starts on a true MCU boundary, with the right MCU
                                   index and AC-entry offset
-  blocks                       -> per-block AC-entry counts and DC values vs the oracle
+  blocks                       -> per-block AC-entry counts and DC differences vs the oracle
+                                  (the DC predictor itself runs inside k_idct_color)
 """
 import os
 import sys
@@ -14,6 +15,7 @@ import sys
 import numpy as np
 import pytest
 
+import jdamd
 import jdoracle
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -122,6 +124,24 @@ def _s16(x):
     return ((x + 0x8000) & 0xFFFF) - 0x8000
 
 
+def dc_differences(data, dc):
+    """The oracle's absolute DCs (MCU-interleaved block order) as the differences the write pass
+    stores: per component, the predictor restarts at 0 at every restart interval
+    (parser.cpp:106-111)."""
+    h = jdamd.parse(data)
+    comp_of = [c for c in range(h.ncomp) for _ in range(h.h[c] * h.v[c])]
+    out = np.zeros_like(dc)
+    pred = [0, 0, 0, 0]
+    for i in range(dc.shape[0]):
+        mcu, bb = divmod(i, h.blocks_per_mcu)
+        if bb == 0 and h.restart_interval and mcu % h.restart_interval == 0:
+            pred = [0, 0, 0, 0]
+        c = comp_of[bb]
+        out[i] = dc[i] - pred[c]
+        pred[c] = int(dc[i])
+    return out
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_block_coefficients(sync_decoder, name):
     data = _load(name)
@@ -130,6 +150,8 @@ def test_block_coefficients(sync_decoder, name):
     entries = sync_decoder.debug_fetch("entries")
     st, coef = jdoracle.decode_coefs(data)
     assert st == 0
+    coef = coef.copy()
+    coef[:, 0] = dc_differences(data, coef[:, 0].astype(np.int64))
     nb = coef.shape[0]
     bad = []
     for i in range(nb):
