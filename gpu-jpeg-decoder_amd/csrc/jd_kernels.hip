@@ -1104,22 +1104,58 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
 //
 // Lane = block of a tile (TR = 1: tile_mcus consecutive MCUs): DC difference, component, and
 // whether the block starts an interval (first block of an MCU whose index is a multiple of DRI).
+// floor(x / d) for x < 64 and 1 <= d <= 64 with magic = ceil(2^16 / d): one full-rate 24-bit
+// multiply and a shift (the error x (magic - 2^16 / d) / 2^16 < 1/1024 never crosses an integer).
+__device__ __forceinline__ uint32_t magic16(uint32_t d) { return (65536u + d - 1u) / d; }
+__device__ __forceinline__ uint32_t div_small(uint32_t x, uint32_t magic) { return __umul24(x, magic) >> 16; }
+
+// Tile geometry shared by k_dc_sum and k_idct_color (TR = 1: tile_mcus consecutive MCUs of one
+// MCU row).  Interval starts among the tile's MCUs without a per-lane modulo: the first is ms
+// MCUs in (g0 % DRI computed once per wave), the others every DRI MCUs after it.
+struct TileGeo {
+    uint32_t m0, nm, g0;  // first MCU column, MCUs in the tile, raster index of its first MCU
+    uint32_t ri, ms;      // restart interval (0: none) and the first interval start (>= 64: none)
+    uint32_t ri_magic;    // magic16(ri) when 0 < ri < tile_mcus (several starts), else 0
+};
+__device__ __forceinline__ TileGeo tile_geo(const ImgDesc& im, uint32_t tile) {
+    TileGeo G;
+    const uint32_t ty = tile / im.tiles_x, tx = tile - ty * im.tiles_x;
+    G.m0 = tx * im.tile_mcus;
+    G.nm = min(im.tile_mcus, im.mcux - G.m0);
+    G.g0 = ty * im.mcux + G.m0;
+    G.ri = im.restart_interval;
+    if (G.ri) {
+        const uint32_t r = G.g0 % G.ri;
+        G.ms = r ? G.ri - r : 0u;
+    } else {
+        G.ms = G.g0 == 0 ? 0u : 64u;
+    }
+    G.ri_magic = (G.ri && G.ri < im.tile_mcus) ? magic16(G.ri) : 0u;
+    return G;
+}
+// MCU m of the tile (m < 64) starts an interval
+__device__ __forceinline__ bool tile_mcu_starts(const TileGeo& G, uint32_t m) {
+    if (!G.ri_magic) return m == G.ms;  // wave-uniform: at most one start in the tile
+    if (m < G.ms) return false;
+    const uint32_t v = m - G.ms;
+    return v - div_small(v, G.ri_magic) * G.ri == 0;
+}
+
+// Lane = block of a tile: DC difference, component, and whether the block starts an interval
+// (first block of an MCU whose raster index is a multiple of DRI).
 struct TileLane {
     int d;
     uint32_t comp;
     bool have, start;
 };
-__device__ __forceinline__ TileLane tile_lane(const BatchDev& b, const ImgDesc& im, uint32_t tile, uint32_t lane) {
-    const uint32_t ty = tile / im.tiles_x, tx = tile - ty * im.tiles_x;
-    const uint32_t m0 = tx * im.tile_mcus, nm = min(im.tile_mcus, im.mcux - m0);
-    const uint32_t m = lane / im.bpm, bb = lane - m * im.bpm;
+__device__ __forceinline__ TileLane tile_lane(const BatchDev& b, const ImgDesc& im, const TileGeo& G, uint32_t lane) {
+    const uint32_t m = div_small(lane, magic16(im.bpm)), bb = lane - m * im.bpm;
     TileLane t;
-    t.have = m < nm;
+    t.have = m < G.nm;
     t.comp = (im.block_pattern >> (2 * bb)) & 3u;
-    const uint32_t g = ty * im.mcux + m0 + m;  // raster MCU index
-    t.start = t.have && bb == 0 && (im.restart_interval ? g % im.restart_interval == 0 : g == 0);
+    t.start = t.have && bb == 0 && tile_mcu_starts(G, m);
     t.d = 0;
-    if (t.have) t.d = int32_t(b.blocks[im.block_base + uint64_t(g) * im.bpm + bb].cnt_dc << 6) >> 6;
+    if (t.have) t.d = int32_t(b.blocks[im.block_base + uint64_t(G.g0 + m) * im.bpm + bb].cnt_dc << 6) >> 6;
     return t;
 }
 
@@ -1129,7 +1165,7 @@ __global__ __launch_bounds__(256) void k_dc_sum(BatchDev b) {
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
     if (tile >= im.tiles_x * im.tiles_y) return;  // wave-uniform
-    const TileLane t = tile_lane(b, im, tile, lane);
+    const TileLane t = tile_lane(b, im, tile_geo(im, tile), lane);
     const uint64_t mask = __ballot(t.start);
     const uint32_t last = mask ? 63u - uint32_t(__clzll(mask)) : 0u;
     const bool after = lane >= last;
@@ -1319,12 +1355,13 @@ __device__ __forceinline__ void idct_row_fast(int* blk) {
 __device__ __forceinline__ void idct_col_fast(int* blk) {
     const int x1 = blk[8 * 4] << 8, x0 = (blk[0] << 8) + 8192;
     const int b1 = blk[8 * 1], b2 = blk[8 * 2], b3 = blk[8 * 3], b5 = blk[8 * 5], b6 = blk[8 * 6], b7 = blk[8 * 7];
-    int x4 = (__mul24(b1, kC1) + __mul24(b7, kC7) + 4) >> 3;
-    int x5 = (__mul24(b1, kC7) + __mul24(b7, -kC1) + 4) >> 3;
-    int x6 = (__mul24(b5, kC5) + __mul24(b3, kC3) + 4) >> 3;
-    int x7 = (__mul24(b5, kC3) + __mul24(b3, -kC5) + 4) >> 3;
-    int x2 = (__mul24(b2, kC6) + __mul24(b6, -kC2) + 4) >> 3;
-    int x3 = (__mul24(b2, kC2) + __mul24(b6, kC6) + 4) >> 3;
+    // (the rounding 4 rides in the inner multiply-add: two v_mad_i32_i24 per term)
+    int x4 = (__mul24(b1, kC1) + (__mul24(b7, kC7) + 4)) >> 3;
+    int x5 = (__mul24(b1, kC7) + (__mul24(b7, -kC1) + 4)) >> 3;
+    int x6 = (__mul24(b5, kC5) + (__mul24(b3, kC3) + 4)) >> 3;
+    int x7 = (__mul24(b5, kC3) + (__mul24(b3, -kC5) + 4)) >> 3;
+    int x2 = (__mul24(b2, kC6) + (__mul24(b6, -kC2) + 4)) >> 3;
+    int x3 = (__mul24(b2, kC2) + (__mul24(b6, kC6) + 4)) >> 3;
     int x8 = x0 + x1;
     int y0 = x0 - x1;
     const int y1 = x4 + x6;
@@ -1535,6 +1572,66 @@ __device__ __forceinline__ void colour16(const int (&Y0)[8], const int (&Y1)[8],
     pack24(c, w1);
 }
 
+// Packed colour (the common case): two pixels per 32-bit word as int16 halves, exactly the
+// integer terms above: R = clamp(y + t.r), B = clamp(y + t.b), G = clamp(y + t.g) with
+// v_pk_add / v_pk_max / v_pk_min (3 VALU per two pixels and channel), then v_perm byte shuffles
+// into RGB order.  Taken when no chroma sample of the wave's lane-step needs the reference's
+// double-precision G (ChromaTerms::exact, about 2e-4 of the samples).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_clamp_add(uint32_t y, uint32_t t) {
+    s16x2 r = __builtin_bit_cast(s16x2, y) + __builtin_bit_cast(s16x2, t);
+    r = __builtin_elementwise_max(r, (s16x2){0, 0});
+    r = __builtin_elementwise_min(r, (s16x2){255, 255});
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pair16(int lo, int hi) { return (uint32_t(lo) & 0xFFFFu) | (uint32_t(hi) << 16); }
+
+// Terms of the 8 >> SH chroma samples under 8 pixels as per-word pairs (word u = pixels 2u, 2u+1).
+template <int SH>
+__device__ __forceinline__ bool terms_words(const int16_t* s_pl, uint32_t cboff, uint32_t croff, uint32_t (&TR)[4],
+                                            uint32_t (&TG)[4], uint32_t (&TB)[4]) {
+    constexpr int NU = 8 >> SH;
+    int cb[8], cr[8];
+    load_plane<SH>(s_pl, cboff, cb);
+    load_plane<SH>(s_pl, croff, cr);
+    ChromaTerms t[NU];
+    bool ex = false;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        t[u] = chroma_terms(cb[u], cr[u]);
+        ex = ex || t[u].exact;
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int a = SH == 0 ? 2 * w : (SH == 1 ? w : w >> 1);  // sample of the word's pixels
+        const int c = SH == 0 ? 2 * w + 1 : a;
+        TR[w] = pair16(t[a].r, t[c].r);
+        TG[w] = pair16(t[a].g, t[c].g);
+        TB[w] = pair16(t[a].b, t[c].b);
+    }
+    return ex;
+}
+
+// 8 pixels of one row: Y as 4 words of int16 pairs -> 24 RGB bytes in 6 words (pack24's order).
+__device__ __forceinline__ void row_rgb_packed(const uint4& Yq, const uint32_t (&TR)[4], const uint32_t (&TG)[4],
+                                               const uint32_t (&TB)[4], uint32_t (&w)[6]) {
+    const uint32_t Y[4] = {Yq.x, Yq.y, Yq.z, Yq.w};
+    uint32_t RG[4], B[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint32_t r = pk_clamp_add(Y[u], TR[u]), g = pk_clamp_add(Y[u], TG[u]);
+        B[u] = pk_clamp_add(Y[u], TB[u]);
+        RG[u] = __builtin_amdgcn_perm(g, r, 0x06020400u);  // r0 g0 r1 g1
+    }
+    // perm(hi, lo, sel): selector bytes 0-3 take lo's bytes, 4-7 hi's, 0x0c a zero byte
+    w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x02040100u);                                            // r0 g0 b0 r1
+    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0603u), 0x05040100u);  // g1 b1 r2 g2
+    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x06030204u);                                            // b2 r3 g3 b3
+    w[3] = __builtin_amdgcn_perm(B[2], RG[2], 0x02040100u);                                            // r4 g4 b4 r5
+    w[4] = __builtin_amdgcn_perm(RG[3], __builtin_amdgcn_perm(B[2], RG[2], 0x0c0c0603u), 0x05040100u);  // g5 b5 r6 g6
+    w[5] = __builtin_amdgcn_perm(B[3], RG[3], 0x06030204u);                                            // b6 r7 g7 b7
+}
+
 // One wave per tile of tile_mcus x tile_mrows MCUs (host-chosen, <= 64 blocks):
 //  1. lane j owns block j: its LDS row (pitch 65 words) is filled with the block's DC and AC
 //     entries, dequantised in zig-zag order (parser.cpp:111,130) and placed at natural positions
@@ -1579,7 +1676,8 @@ __device__ __forceinline__ size_t fancy_plane_off(const ImgDesc& im, uint32_t c)
 // staging (64 rows of 66 int16 = 33 words: odd pitch, conflict-free read-back) and then the
 // component planes share s_buf; planes need at most 64*64 + 64*2*6 int16 (§ host tile choice)
 constexpr int kIdctBufWords = 2464;
-constexpr int kQzWords = 3 * 65;  // quant step per component, zig-zag order (pitch 65: no bank clash)
+constexpr int kQzWords = 3 * 36;  // quant steps per component, zig-zag order, as u16 pairs (pitch 36
+                                  // words: 16-byte rows; a wave reads at most 3 distinct rows)
 
 // One tile.  EXACT = false (k_idct_color): a wave with a coefficient beyond the fast IDCT's range
 // (never seen in real images) appends its tile to slow_tiles and leaves; EXACT = true
@@ -1587,37 +1685,38 @@ constexpr int kQzWords = 3 * 65;  // quant step per component, zig-zag order (pi
 template <bool EXACT>
 __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint32_t tile, uint32_t* s_buf, int* s_qz) {
     const ImgDesc& im = b.imgs[img];
-    const uint32_t tiles_x = im.tiles_x;
-    if (tile >= tiles_x * im.tiles_y) return;
+    if (tile >= im.tiles_x * im.tiles_y) return;
     const uint32_t lane = threadIdx.x;
-    const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
-    const uint32_t TM = im.tile_mcus, TR = im.tile_mrows, bpm = im.bpm, nc = im.ncomp;
-    const uint32_t m0 = tx * TM, r0 = ty * TR;
-    const uint32_t nm = min(TM, im.mcux - m0), nr = min(TR, im.mcuy - r0);
-    for (uint32_t i = lane; i < nc * 64; i += kIdctThreads) {
-        const uint32_t c = i >> 6, z = i & 63u;
-        s_qz[c * 65 + z] = int(b.qtabs[size_t(im.qslot[c]) * 64 + z]);
+    const TileGeo G = tile_geo(im, tile);
+    const uint32_t TM = im.tile_mcus, bpm = im.bpm, nc = im.ncomp;
+    const uint32_t m0 = G.m0, r0 = G.g0 / im.mcux, nm = G.nm;
+    if (lane < 16 * nc) {  // quant steps: lane = 4 steps of one component (64 steps = 16 lanes)
+        const uint32_t c = lane >> 4, q = lane & 15u;
+        const uint2 v = *reinterpret_cast<const uint2*>(b.qtabs + size_t(im.qslot[c]) * 64 + 4 * q);
+        *reinterpret_cast<uint2*>(s_qz + c * 36 + 2 * q) = v;
     }
     constexpr int kRow16 = 33;  // words per staging row
     uint4* z4 = reinterpret_cast<uint4*>(s_buf);
-    for (uint32_t i = lane; i < (64 * kRow16 + 3) / 4; i += kIdctThreads) z4[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t k = 0; k < (64 * kRow16 + 3) / 4 / kIdctThreads + 1; k++) {
+        const uint32_t i = lane + k * kIdctThreads;
+        if (i < (64 * kRow16 + 3) / 4) z4[i] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
 
     // 1. sparse -> dense (my block): quantised coefficients at their zig-zag positions
     //    (parser.cpp:111,130: the dequantisation happens on read-back, in zig-zag correspondence)
-    const uint32_t m = lane / bpm, bb = lane - m * bpm;
-    const uint32_t mr = m / TM, mi = m - mr * TM;
-    const bool have = mr < nr && mi < nm;
+    const uint32_t m = div_small(lane, magic16(bpm)), bb = lane - m * bpm;
+    const bool have = m < nm;
+    const uint32_t mi = m, mr = 0;
     const uint32_t comp = (im.block_pattern >> (2 * bb)) & 3u;
     int16_t* row = reinterpret_cast<int16_t*>(s_buf + lane * kRow16);
-    const BlockInfo bi =
-        have ? b.blocks[im.block_base + uint64_t((r0 + mr) * im.mcux + m0 + mi) * bpm + bb] : BlockInfo{0u, 0u};
+    const BlockInfo bi = have ? b.blocks[im.block_base + uint64_t(G.g0 + m) * bpm + bb] : BlockInfo{0u, 0u};
     int dc_pred;
     {  // DC prediction: segmented scan of the tile's DC differences onto its entry predictors
         // (tile_dc, k_dc_scan); a block that starts an interval resets its component's predictor
         const int d = have ? int32_t(bi.cnt_dc << 6) >> 6 : 0;
-        const uint32_t g = (r0 + mr) * im.mcux + m0 + mi;
-        const bool start = have && bb == 0 && (im.restart_interval ? g % im.restart_interval == 0 : g == 0);
+        const bool start = have && bb == 0 && tile_mcu_starts(G, m);
         const uint64_t smask = __ballot(start);
         const int p0 = wave_scan_dpp(comp == 0 ? d : 0);
         const int p1 = wave_scan_dpp(comp == 1 ? d : 0);
@@ -1672,8 +1771,8 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
     //    c is when |c| <= 2^(k-1) with 2^(k-1) * (largest quant step) < 2^16 (host: im.qmask),
     //    i.e. when bits k-1..15 of c all equal its sign: c ^ (c << 1) has bits k..15 clear.
     const uint32_t* rw = s_buf + lane * kRow16;
-    const int* qz = s_qz + comp * 65;
-    const int dq0 = dc_pred * qz[0];
+    const uint4* qz4 = reinterpret_cast<const uint4*>(s_qz + comp * 36);
+    const int dq0 = dc_pred * int(reinterpret_cast<const uint16_t*>(s_qz)[comp * 72]);
     if (!EXACT) {  // range test before dequantising: the branch then holds no 64-value block
         uint32_t acc = 0;
 #pragma unroll
@@ -1692,10 +1791,16 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
     }
     int blk[64];
 #pragma unroll
-    for (int p = 0; p < 32; p++) {
-        const uint32_t w = rw[p];
-        blk[kNatOfZz[2 * p]] = p == 0 ? dq0 : __mul24(int(int16_t(w & 0xFFFFu)), qz[2 * p]);
-        blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, qz[2 * p + 1]);
+    for (int p4 = 0; p4 < 8; p4++) {
+        const uint4 qv = qz4[p4];
+        const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p = 4 * p4 + k;
+            const uint32_t w = rw[p];
+            blk[kNatOfZz[2 * p]] = p == 0 ? dq0 : __mul24(int(int16_t(w & 0xFFFFu)), int(qw[k] & 0xFFFFu));
+            blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, int(qw[k] >> 16));
+        }
     }
 #if !(JD_ABL & 2)
     idct_block(blk, !EXACT);
@@ -1704,7 +1809,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
         if (have) {
             const uint32_t hc = im.h[comp], vc = im.v[comp];
             const uint32_t t = bb - im.comp_block0[comp];
-            const uint32_t tyb = t / hc, txb = t - tyb * hc;
+            const uint32_t tyb = t >> __builtin_ctz(hc), txb = t - tyb * hc;  // hc in {1, 2, 4}
             int16_t* dst = reinterpret_cast<int16_t*>(im.planes) + fancy_plane_off(im, comp) +
                            size_t(((r0 + mr) * vc + tyb) * 8) * (im.mcux * hc * 8) + ((m0 + mi) * hc + txb) * 8;
 #pragma unroll
@@ -1731,14 +1836,14 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
             if (uint32_t(c) < nc) {
                 ppitch[c] = TM * im.h[c] * 8 + 8;
                 pbase[c] = off;
-                off += ppitch[c] * TR * im.v[c] * 8;
+                off += ppitch[c] * im.v[c] * 8;  // one MCU row
             }
         }
     }
     if (have) {
         const uint32_t hc = im.h[comp];
         const uint32_t t = bb - im.comp_block0[comp];
-        const uint32_t tyb = t / hc, txb = t - tyb * hc;
+        const uint32_t tyb = t >> __builtin_ctz(hc), txb = t - tyb * hc;  // hc in {1, 2, 4}
         const uint32_t pitch = comp == 0 ? ppitch[0] : (comp == 1 ? ppitch[1] : ppitch[2]);
         const uint32_t base = comp == 0 ? pbase[0] : (comp == 1 ? pbase[1] : pbase[2]);
         int16_t* dst = s_pl + base + ((mr * im.v[comp] + tyb) * 8) * pitch + (mi * hc + txb) * 8;
@@ -1758,7 +1863,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
     //    planes are vertically subsampled (the two rows share their chroma samples and terms)
     const uint32_t lg_mw = im.lg_mw, lg_mh = im.lg_mh;
     const uint32_t gpr = (TM << lg_mw) >> 3;  // 8-pixel groups per tile row
-    const uint32_t th = TR << lg_mh;
+    const uint32_t th = 1u << lg_mh;
     const uint32_t W = im.width, H = im.height;
     const uint32_t x_tile = m0 << lg_mw, y_tile = r0 << lg_mh;
     const uint32_t shx1 = im.shx[1], shy1 = im.shy[1], shx2 = im.shx[2], shy2 = im.shy[2];
@@ -1768,7 +1873,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
     uint8_t* out = reinterpret_cast<uint8_t*>(im.rgb);
     // lane -> (row group gy, column group gc), advanced by 64 groups per iteration
     const uint32_t step_y = kIdctThreads / gpr, step_c = kIdctThreads - step_y * gpr;
-    uint32_t gy = lane / gpr, gc = lane - gy * gpr;
+    uint32_t gy = gpr <= 64u ? div_small(lane, magic16(gpr)) : 0u, gc = lane - gy * gpr;
 #if JD_ABL & 1
     if (lane < 1000) return;
 #endif
@@ -1776,12 +1881,29 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
         const uint32_t py = gy * rows, gx = gc << 3;
         const uint32_t y = y_tile + py, x = x_tile + gx;
         if (y >= H || x >= W) continue;
-        int Y0[8], Y1[8];
-        load_plane<0>(s_pl, pbase[0] + py * ppitch[0] + gx, Y0);
-        if (pair) load_plane<0>(s_pl, pbase[0] + (py + 1) * ppitch[0] + gx, Y1);
+        const uint32_t yoff = pbase[0] + py * ppitch[0] + gx;
         const uint32_t cboff = pbase[1] + (py >> shy1) * ppitch[1] + (gx >> shx1);
         const uint32_t croff = pbase[2] + (py >> shy2) * ppitch[2] + (gx >> shx2);
         uint32_t w0[6], w1[6];
+        bool slow = true;
+        if (cmode <= 2u) {  // wave-uniform
+            uint32_t TR[4], TG[4], TB[4];
+            bool ex;
+            switch (cmode) {
+                case 0: ex = terms_words<0>(s_pl, cboff, croff, TR, TG, TB); break;
+                case 1: ex = terms_words<1>(s_pl, cboff, croff, TR, TG, TB); break;
+                default: ex = terms_words<2>(s_pl, cboff, croff, TR, TG, TB); break;
+            }
+            if (!__any(ex)) {  // uniform over the lanes in this step
+                row_rgb_packed(*reinterpret_cast<const uint4*>(s_pl + yoff), TR, TG, TB, w0);
+                if (pair) row_rgb_packed(*reinterpret_cast<const uint4*>(s_pl + yoff + ppitch[0]), TR, TG, TB, w1);
+                slow = false;
+            }
+        }
+        if (slow) {
+        int Y0[8], Y1[8];
+        load_plane<0>(s_pl, yoff, Y0);
+        if (pair) load_plane<0>(s_pl, yoff + ppitch[0], Y1);
         if (pair) {
             switch (cmode) {  // wave-uniform
                 case 0: colour16<0>(Y0, Y1, s_pl, cboff, croff, w0, w1); break;
@@ -1806,6 +1928,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
             }
             pack24(rgb, w0);
         }
+        }
 #if JD_ABL & 32
         if (w0[0] == 0x12345678u && w1[3] == 0x9abcdef0u)
 #endif
@@ -1818,14 +1941,14 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
 
 __global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
-    __shared__ int s_qz[kQzWords];
+    __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
     idct_tile<false>(b, blockIdx.y, blockIdx.x, s_buf, s_qz);
 }
 
 // The tiles k_idct_color left (grid-stride over the list; empty in practice).
 __global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
-    __shared__ int s_qz[kQzWords];
+    __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
     const uint32_t n = uint32_t(min(b.counters[1], (unsigned long long)b.total_tiles));
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const TileRef t = b.slow_tiles[i];
