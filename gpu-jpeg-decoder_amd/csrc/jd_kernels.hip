@@ -340,11 +340,12 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 // start on MCU boundaries and nothing runs serially:
 //   k_subplan      per image: pieces of every interval (interval lengths are only known on the
 //                  GPU, after k_index)
-//   k_piece<Scan>  lane per piece j: starts piece_overlap bits before j*piece_bits with a guessed
-//                  state (Huffman codes self-synchronise; so does the MCU phase given a few
-//                  thousand bits), takes the first MCU boundary at/after j*piece_bits as the
-//                  piece start, and counts MCUs and AC entries up to the first MCU boundary
-//                  at/after (j+1)*piece_bits.  Piece 0 starts at bit 0 in the true state.
+//   k_piece<Scan>  lane per piece j of n = ceil(bits / piece_bits) equal shares L = ceil(bits / n):
+//                  starts piece_overlap bits before j*L with a guessed state (Huffman codes
+//                  self-synchronise; so does the MCU phase given a few thousand bits), takes the
+//                  first MCU boundary at/after j*L as the piece start, and counts MCUs and AC
+//                  entries up to the first MCU boundary at/after (j+1)*L.  Piece 0 starts at
+//                  bit 0 in the true state.
 //   k_rescan       lane per piece whose start is not its predecessor's end: re-scan from that end
 //   k_chain        wave per interval: piece j's end must be piece j+1's start (k_chain_fix walks
 //                  the rare interval where it still is not serially, re-scanning).  Prefix sums
@@ -428,6 +429,10 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
     S.pattern = im.block_pattern;
     S.bpm = im.bpm;
 }
+
+// Nominal piece length of an interval cut into npc pieces: equal shares of its bits (at most
+// piece_bits), so the lanes of a wave walk about the same number of bits.
+__device__ __forceinline__ uint32_t piece_len(const SegInfo& S, uint32_t npc) { return (S.bits + npc - 1u) / npc; }
 
 // AC-entry slots of an interval: 63 per block (a block stores at most 63) plus 3 per MCU for
 // aligning every piece's first entry to a 16-byte quad (at most one pad per non-empty piece).
@@ -864,10 +869,11 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     if (MODE == kWalkScan) {
         // piece 0 counts from bit 0 in the true state; piece j > 0 synchronises from
         // piece_overlap bits before its nominal start (from bit 0, exactly, when that is closer)
-        const uint64_t pstart = uint64_t(j) * b.piece_bits;
+        const uint32_t plen = piece_len(S, npc);
+        const uint64_t pstart = uint64_t(j) * plen;
         W.warm_to = (j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
         W.start = (pstart <= b.piece_overlap) ? 0u : min(uint32_t(pstart - b.piece_overlap), W.warm_to);
-        W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(pstart + b.piece_bits, 0xFFFFFFFEu));
+        W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(pstart + plen, 0xFFFFFFFEu));
     } else {
         W.start = valid ? b.piece_bit[u] : 0u;
         W.warm_to = W.start;
@@ -891,7 +897,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     if (MODE == kWalkScan)
         walk_scan<kScanSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
-                             valid, W, cp, b.piece_bits / kCpMax);
+                             valid, W, cp, max(1u, piece_len(S, npc) / kCpMax));
     else
         walk_write(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
     if (!valid) return;
@@ -948,11 +954,11 @@ __global__ __launch_bounds__(kPieceThreads) void k_rescan(BatchDev b) {
     table_slots(ts, S, dcp, acp);
     Walk W;
     W.start = W.warm_to = expect;
-    W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
+    W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * piece_len(S, npc), 0xFFFFFFFEu));
     W.nmcu = W.ent0 = 0;
     W.blk0 = 0;
     walk_scan<kScanJoin>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, need, W,
-                         b.piece_cp + size_t(u) * kCpRecords, b.piece_bits / kCpMax);
+                         b.piece_cp + size_t(u) * kCpRecords, max(1u, piece_len(S, npc) / kCpMax));
     if (!need) return;
     b.piece_bit[u] = W.start;
     b.piece_end[u] = W.m_end;
@@ -1061,11 +1067,11 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
         if (pbit != expect) {  // the speculative start had not synchronised: re-scan from the truth
             Walk W;
             W.start = W.warm_to = expect;
-            W.stop_at = (j + 1 == n) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * b.piece_bits, 0xFFFFFFFEu));
+            W.stop_at = (j + 1 == n) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * piece_len(S, n), 0xFFFFFFFEu));
             W.nmcu = W.ent0 = 0;
             W.blk0 = 0;
             walk_scan<kScanJoin>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
-                                 true, W, b.piece_cp + size_t(u) * kCpRecords, b.piece_bits / kCpMax);
+                                 true, W, b.piece_cp + size_t(u) * kCpRecords, max(1u, piece_len(S, n) / kCpMax));
             pbit = expect;
             pend = W.m_end;
             pm = W.mcus;

@@ -4,8 +4,9 @@ Per image i: each channel = 128 + A*sin(x*fx + y*fy + phi) + N(0, 3), with (A, f
 from a generator seeded by i; encoded as baseline JPEG with the standard Huffman tables
 (optimize=False) at the requested quality / subsampling / restart interval.
 
-Encoding uses Pillow (libjpeg-turbo), present in this image.  Generation is parallel (processes)
-because a 1024-image 1080p batch takes ~15 s serially.
+Encoding uses the in-repo baseline encoder tools/jdenc.c by default (JD_ENCODER=pillow selects
+Pillow / libjpeg-turbo; optimized-table fixtures always use Pillow).  Generation is parallel
+(processes) because a 1024-image 1080p batch takes several seconds serially.
 """
 from __future__ import annotations
 

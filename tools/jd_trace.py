@@ -303,20 +303,21 @@ def emulate(d: bytes, piece_bits: int = 8192, overlap: int = 4096):
         val = int.from_bytes(data + b"\xff" * 16, "big")
         total = (len(data) + 16) * 8
         n = max(1, -(-bits // piece_bits))
+        plen = -(-bits // n)  # equal shares (jd_kernels.hip piece_len)
         big = 1 << 40
         pcs = []
         for j in range(n):  # scan
-            pstart = j * piece_bits
+            pstart = j * plen
             warm_to = 0 if j == 0 else min(pstart, bits)
             start = 0 if pstart <= overlap else min(pstart - overlap, warm_to)
-            stop_at = big if j == n - 1 else pstart + piece_bits
+            stop_at = big if j == n - 1 else pstart + plen
             ms, me, mc, en = _walk_scan(t, pattern, val, total, bits, start, warm_to, stop_at)
             pcs.append([0 if j == 0 else ms, me, mc, en])
         for j in range(1, n):  # chain: verify, re-scan from the verified boundary
             if pcs[j][0] != pcs[j - 1][1]:
                 rescans += 1
                 st = pcs[j - 1][1]
-                stop_at = big if j == n - 1 else (j + 1) * piece_bits
+                stop_at = big if j == n - 1 else (j + 1) * plen
                 ms, me, mc, en = _walk_scan(t, pattern, val, total, bits, st, st, stop_at)
                 pcs[j] = [st, me, mc, en]
         blocks = []
