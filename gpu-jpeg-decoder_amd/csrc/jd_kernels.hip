@@ -97,6 +97,16 @@ __device__ __forceinline__ void load64(uintptr_t t0, uintptr_t fend, uint32_t (&
 //   FF FF      -> fill byte (part of the break that follows)
 //   FF other   -> terminating marker (EOI ...): the ECS ends
 // ------------------------------------------------------------------------------------------
+// Per-byte masks of a word (high bit of each byte lane): returns byte == 0x00; ff: byte == 0xFF;
+// nz: neither 00 nor FF.
+__device__ __forceinline__ uint32_t scan_masks(uint32_t x, uint32_t& ff, uint32_t& nz) {
+    const uint32_t t = ~x;
+    ff = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    const uint32_t zero = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    nz = ~(zero | ff) & 0x80808080u;
+    return zero;
+}
+
 __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     __shared__ uint32_t s_wsum[2][kScanThreads / 64];
     const ImgDesc& im = b.imgs[blockIdx.y];
@@ -111,26 +121,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     const uint32_t nextb = (t0 + 64 < fend) ? uint32_t(*reinterpret_cast<gu8*>(t0 + 64)) : 0u;
 
     uint32_t ndrop = 0, nbrk = 0;
-    if (t0 >= lo && t0 + 64 < fend) {
+    const bool interior = t0 >= lo && t0 + 64 < fend;
+    if (interior) {
         // interior thread: exact per-byte masks (high bit of each byte lane), one word at a time
         // with the neighbours' masks carried (few live registers: this pass is latency-bound)
-        //   ff   : byte == 0xFF            zero: byte == 0x00
         //   drop : 00 preceded by FF       brk : FF followed by neither 00 nor FF
-        auto masks = [](uint32_t x, uint32_t& ff, uint32_t& nz) {
-            const uint32_t t = ~x;
-            ff = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
-            const uint32_t zero = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-            nz = ~(zero | ff) & 0x80808080u;  // neither 00 nor FF
-            return zero;
-        };
         uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;  // only its top byte is used
         uint32_t ff_cur, nz_cur;
-        uint32_t zero_cur = masks(w[0], ff_cur, nz_cur);
+        uint32_t zero_cur = scan_masks(w[0], ff_cur, nz_cur);
         const uint32_t nznext = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;  // byte after it
 #pragma unroll
         for (int q = 0; q < 16; q++) {
             uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = 0;
-            if (q < 15) zero_nx = masks(w[q + 1], ff_nx, nz_nx);
+            if (q < 15) zero_nx = scan_masks(w[q + 1], ff_nx, nz_nx);
             const uint32_t pf = (ff_cur << 8) | (ff_prev >> 24);
             const uint32_t nn = (nz_cur >> 8) | (nz_nx << 24);
             ndrop += __builtin_popcount(zero_cur & pf);
@@ -155,7 +158,39 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     uint32_t tot_drop, tot_brk;
     const uint32_t drop_before = block_excl_scan(ndrop, s_wsum[0], &tot_drop);
     uint32_t off = block_excl_scan(nbrk, s_wsum[1], &tot_brk);
-    if (nbrk) {
+    if (nbrk && interior) {
+        // walk the break bits only (a wave with a break used to run a 64-byte loop): per word the
+        // same masks as the count above, then one iteration per break in it
+        Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
+        uint32_t d = drop_before;
+        uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;
+        uint32_t ff_cur, nz_cur;
+        uint32_t zero_cur = scan_masks(w[0], ff_cur, nz_cur);
+        const uint32_t nznext = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = 0;
+            if (q < 15) zero_nx = scan_masks(w[q + 1], ff_nx, nz_nx);
+            const uint32_t pf = (ff_cur << 8) | (ff_prev >> 24);
+            const uint32_t nn = (nz_cur >> 8) | (nz_nx << 24);
+            const uint32_t dm = zero_cur & pf;
+            uint32_t bm = ff_cur & nn;
+            while (bm) {
+                const uint32_t bit = __builtin_ctz(bm);  // 7, 15, 23 or 31: byte k = bit >> 3
+                const uint32_t k = bit >> 3;
+                const uint32_t nbv = k < 3u ? (w[q] >> (8u * (k + 1u))) & 0xFFu : (q < 15 ? w[q < 15 ? q + 1 : q] & 0xFFu : nextb);
+                const uint32_t dd = d + __builtin_popcount(dm & ((1u << bit) - 1u));
+                const uint32_t is_term = (nbv & 0xF8u) == 0xD0u ? 0u : 1u;
+                out[off++] = Break{uint32_t(t0 + 4u * q + k - file), (dd << 1) | is_term};
+                bm &= bm - 1u;
+            }
+            d += __builtin_popcount(dm);
+            ff_prev = ff_cur;
+            ff_cur = ff_nx;
+            nz_cur = nz_nx;
+            zero_cur = zero_nx;
+        }
+    } else if (nbrk) {  // edge threads: byte by byte
         Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
         uint32_t d = drop_before;
 #pragma unroll 1
@@ -275,6 +310,24 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
 // the image's un-stuffed stream with byte stores at the unaligned head/tail and dword stores in
 // between, so neighbouring chunks (other workgroups) never share a stored word.
 // ------------------------------------------------------------------------------------------
+// Bytes [0, n) of c (a thread's kept bytes, contiguous in the run), n >= 60, to LDS bytes
+// [off, off + n): aligned dword stores for every word wholly inside the run, byte stores at its
+// two ends (the neighbouring threads own the other bytes of those two words).
+__device__ __forceinline__ void store_run(uint32_t* s_out, uint32_t off, const uint32_t (&c)[16], uint32_t n) {
+    uint8_t* so = reinterpret_cast<uint8_t*>(s_out);
+    const uint32_t a = (4u - (off & 3u)) & 3u;  // bytes before the first aligned word
+    const uint32_t wb = (off + a) >> 2, nf = (n - a) >> 2, t = a + 4u * nf;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+        if (uint32_t(j) < a) so[off + j] = uint8_t(c[0] >> (8 * j));
+#pragma unroll
+    for (int k = 0; k < 16; k++)  // run bytes [a + 4k, a + 4k + 4)
+        if (uint32_t(k) < nf) s_out[wb + k] = __builtin_amdgcn_alignbyte(k < 15 ? c[k < 15 ? k + 1 : k] : 0u, c[k], a);
+#pragma unroll
+    for (int j = 56; j < 64; j++)  // the tail: at most 3 bytes, all at j >= n - 3 >= 57
+        if (uint32_t(j) >= t && uint32_t(j) < n) so[off + j] = uint8_t(c[j >> 2] >> (8 * (j & 3)));
+}
+
 __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
     __shared__ uint32_t s_out[kScanChunk / 4 + 4];
     __shared__ uint32_t s_wsum[kScanThreads / 64];
@@ -287,32 +340,64 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
     uint32_t w[16];
     load64(t0, fend, w);
     const uint32_t prevb = (t0 > lo && t0 - 1 < fend) ? uint32_t(*reinterpret_cast<gu8*>(t0 - 1)) : 0u;
+    // interior threads (all 64 bytes in the ECS): stuffed zeros from the SWAR masks of k_scan,
+    // their positions kept (the two highest); others: a per-byte keep mask
+    const bool interior = t0 >= lo && t0 + 64 <= fend;
     uint64_t keep = 0;
+    uint32_t nd = 0, p0 = 0, p1 = 0;
+    if (interior) {
+        uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;
 #pragma unroll
-    for (int i = 0; i < 64; i++) {
-        const uint32_t by = byte_of(w, i);
-        const uint32_t pb = i ? byte_of(w, i - 1) : prevb;
-        const uintptr_t a = t0 + i;
-        const bool inr = a >= lo && a < fend;
-        const bool drop = a > lo && by == 0x00u && pb == 0xFFu;
-        if (inr && !drop) keep |= 1ull << i;
-    }
-    uint32_t total;
-    uint32_t off = block_excl_scan(uint32_t(__builtin_popcountll(keep)), s_wsum, &total);
-    uint8_t* so = reinterpret_cast<uint8_t*>(s_out);
-    if (keep == ~0ull) {  // common case: whole thread kept
-        const uint32_t sh = off & 3u, wb = off >> 2;
-        if (sh == 0u) {
-#pragma unroll
-            for (int q = 0; q < 16; q++) s_out[wb + q] = w[q];
-        } else {
-            // words wb+1..wb+15 whole (funnel shifts of neighbouring words); the 4 - sh bytes
-            // before them and the sh after them share words with the neighbouring threads
-            for (uint32_t j = 0; j < 4u - sh; j++) so[off + j] = uint8_t(w[0] >> (8 * j));
-#pragma unroll
-            for (int k = 1; k < 16; k++) s_out[wb + k] = __builtin_amdgcn_alignbyte(w[k], w[k - 1], 4u - sh);
-            for (uint32_t j = 0; j < sh; j++) so[off + 64 - sh + j] = uint8_t(w[15] >> (8 * (4 - sh + j)));
+        for (int q = 0; q < 16; q++) {
+            uint32_t ff, nz;
+            const uint32_t zero = scan_masks(w[q], ff, nz);
+            uint32_t dm = zero & ((ff << 8) | (ff_prev >> 24));
+            if (q == 0 && t0 == lo) dm &= ~0x80u;  // the ECS's first byte is never dropped
+            ff_prev = ff;
+            while (dm) {
+                p1 = p0;
+                p0 = 4u * q + (uint32_t(__builtin_ctz(dm)) >> 3);
+                nd++;
+                dm &= dm - 1u;
+            }
         }
+    }
+    if (!interior || nd > 2u) {
+#pragma unroll
+        for (int i = 0; i < 64; i++) {
+            const uint32_t by = byte_of(w, i);
+            const uint32_t pb = i ? byte_of(w, i - 1) : prevb;
+            const uintptr_t a = t0 + i;
+            const bool inr = a >= lo && a < fend;
+            const bool drop = a > lo && by == 0x00u && pb == 0xFFu;
+            if (inr && !drop) keep |= 1ull << i;
+        }
+    }
+    const uint32_t nkeep = (interior && nd <= 2u) ? 64u - nd : uint32_t(__builtin_popcountll(keep));
+    uint32_t total;
+    uint32_t off = block_excl_scan(nkeep, s_wsum, &total);
+    uint8_t* so = reinterpret_cast<uint8_t*>(s_out);
+    if (interior && nd <= 2u) {
+        // common case: at most two stuffed zeros (a wave with one used to run a 64-byte loop):
+        // remove them, highest first, by shifting the later bytes down one (a funnel shift and a
+        // bit-field insert per word), then store the run
+        uint32_t cw[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) cw[q] = w[q];
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            if (uint32_t(r) < nd) {
+                const uint32_t p = r == 0 ? p0 : p1;
+                const uint32_t qp = p >> 2, lowm = (1u << (8u * (p & 3u))) - 1u;
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    const uint32_t sh = __builtin_amdgcn_alignbyte(q < 15 ? cw[q < 15 ? q + 1 : q] : 0u, cw[q], 1u);
+                    const uint32_t m = uint32_t(q) < qp ? 0xFFFFFFFFu : (uint32_t(q) == qp ? lowm : 0u);
+                    cw[q] = (cw[q] & m) | (sh & ~m);
+                }
+            }
+        }
+        store_run(s_out, off, cw, 64u - nd);
     } else {
 #pragma unroll
         for (int i = 0; i < 64; i++)
@@ -502,9 +587,11 @@ static_assert(kRowWords % 2 == 1, "row pitch must be odd");
 constexpr int kWalkScan = 0, kWalkWrite = 1;
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 
+constexpr int kRingWords = 8;  // write walk: per-lane ring of two entry quads (16-byte aligned)
 size_t piece_lds_bytes(uint32_t max_slots) {
     return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * kRowWords * 4;
 }
+static_assert((kPieceThreads * kRowWords * 4) % 16 == 0, "rings must start 16-byte aligned");
 
 // One walk over an interval's bits from `start`.
 //   scan : (true MCU-start state at `start` when warm_to == start, else speculative) until the
@@ -579,13 +666,13 @@ __device__ __forceinline__ uint32_t lut_fast(uint32_t tab, uint32_t peek) {
 }
 //
 // The write walk: nmcu MCUs from the MCU boundary `start`: BlockInfo (DC difference) + AC entries.
-// AC entries shift through a 4-entry register queue and leave as one 16-byte store per aligned
-// quad [ent - 4, ent): a wave's 64 lanes store to 64 unrelated places, so store instructions, not
+// AC entries collect in a per-lane LDS ring and leave as one 16-byte store per aligned quad
+// [4 fq, 4 fq + 4): a wave's 64 lanes store to 64 unrelated places, so store instructions, not
 // bytes, bound this pass.  Pieces start on a quad (k_chain aligns them); the last, partial quad
 // is stored dword by dword.  The walk stops after its last block; running past the interval's
 // data is checked once per window round (writes stay inside the piece's slots either way).
 __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp,
-                                           uint32_t acp, uint32_t* row, bool active_in, Walk& W) {
+                                           uint32_t acp, uint32_t* row, uint32_t* ring, bool active_in, Walk& W) {
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
@@ -604,17 +691,22 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
     uint32_t z = 0, b3 = 0, tab = tab_dc0;
     uint32_t ent = W.ent0, ent_blk = W.ent0, blk = 0;
     int dcd = 0;
-    uint32_t wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;
     // Stores are deferred and issued every few loop iterations, so that one store instruction
     // carries many lanes (a wave's store instructions, not its bytes, bound this pass): a lane
     // completes at most one quad per 4 iterations (one entry per symbol) and one block per 2
     // (a DC and at least one AC symbol), so one pending quad and one pending block suffice.
-    uint32_t pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0, pent = 0, pbi0 = 0, pbi1 = 0, pblk = 0;
-    bool pend_q = false, pend_b = false;
-#define JD_FLUSH_Q()                                                                              \
-    do {                                                                                          \
-        if (pend_q) *reinterpret_cast<uint4*>(eout + pent - 4u) = make_uint4(pq0, pq1, pq2, pq3); \
-        pend_q = false;                                                                           \
+    // Entries go to the lane's LDS ring of two quads (slot ent & 7; a symbol that emits nothing
+    // writes the next free slot without advancing, so its word is overwritten); a flush stores
+    // the completed quad fq straight from the ring.
+    uint32_t fq = W.ent0 >> 2;  // quads stored so far (pieces start on a quad)
+    uint32_t pbi0 = 0, pbi1 = 0, pblk = 0;
+    bool pend_b = false;
+#define JD_FLUSH_Q()                                                                                         \
+    do {                                                                                                     \
+        if (fq < (ent >> 2)) {                                                                               \
+            *reinterpret_cast<uint4*>(eout + 4u * fq) = *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)); \
+            fq++;                                                                                            \
+        }                                                                                                    \
     } while (0)
 #define JD_FLUSH_B()                                       \
     do {                                                   \
@@ -642,19 +734,8 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
             const bool fin = zn >= 63u;
             const bool emit = (e & ~zn & kEntEmit) != 0;  // zn < 64 (bit 6 of zn clear)
             dcd = (e & kEntDc) ? val : dcd;
-            const uint32_t ev = (uint32_t(val) << 16) | zn;
-            wq0 = emit ? wq1 : wq0;
-            wq1 = emit ? wq2 : wq1;
-            wq2 = emit ? wq3 : wq2;
-            wq3 = emit ? ev : wq3;
+            ring[ent & 7u] = (uint32_t(val) << 16) | zn;
             ent += emit ? 1u : 0u;
-            const bool qdone = emit && (ent & 3u) == 0u;
-            pq0 = qdone ? wq0 : pq0;
-            pq1 = qdone ? wq1 : pq1;
-            pq2 = qdone ? wq2 : pq2;
-            pq3 = qdone ? wq3 : pq3;
-            pent = qdone ? ent : pent;
-            pend_q = pend_q || qdone;
             pbi0 = fin ? ent_blk : pbi0;
             pbi1 = fin ? pack_cnt_dc(ent - ent_blk, dcd) : pbi1;
             pblk = fin ? blk : pblk;
@@ -686,11 +767,12 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
     }
 #undef JD_FLUSH_Q
 #undef JD_FLUSH_B
-    if (ent & 3u) {  // the last, partial quad: its r entries are the newest, wq[4-r..3]
+    if (ent & 3u) {  // the last, partial quad (every complete one is stored)
         const uint32_t r = ent & 3u, qb = ent - r;
-        eout[qb] = r == 3u ? wq1 : r == 2u ? wq2 : wq3;
-        if (r >= 2u) eout[qb + 1u] = r == 3u ? wq2 : wq3;
-        if (r == 3u) eout[qb + 2u] = wq3;
+        const uint4 q = *reinterpret_cast<const uint4*>(ring + 4u * ((qb >> 2) & 1u));
+        eout[qb] = q.x;
+        if (r >= 2u) eout[qb + 1u] = q.y;
+        if (r == 3u) eout[qb + 2u] = q.z;
     }
     W.end = R.bit();
     W.bad = (errs & kEntBad) != 0 || (nblk > 0 && blk != nblk) || W.end > S.bits;
@@ -899,7 +981,12 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
         walk_scan<kScanSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
                              valid, W, cp, max(1u, piece_len(S, npc) / kCpMax));
     else
-        walk_write(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, valid, W);
+        walk_write(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
+                   s_rows + kPieceThreads * kRowWords + threadIdx.x * kRingWords, valid, W);
+    if (MODE == kWalkWrite) {  // the walks end wave-uniformly: one counter atomic per wave, not per lane
+        const int tot = wave_scan_dpp(valid ? int(W.ents) : 0);
+        if ((threadIdx.x & 63u) == 63u && tot) atomicAdd(&b.counters[0], (unsigned long long)uint32_t(tot));
+    }
     if (!valid) return;
     if (MODE == kWalkScan) {
         // piece 0 starts at bit 0 whatever its walk found (it is the true state)
@@ -919,7 +1006,6 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
             if (s + 1 < im.seg_base + im.nseg && (S.bits >> 3) > ((end + 7) >> 3)) bad = true;
         }
         if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
-        atomicAdd(&b.counters[0], (unsigned long long)W.ents);
     }
 }
 
@@ -2099,7 +2185,9 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             if (b.nchain) hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 7:
-            if (b.nsub) hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            if (b.nsub)
+                hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads),
+                                   lds + size_t(kPieceThreads) * kRingWords * 4, s, b);
             break;
         case 8:
             if (!b.max_tiles) break;
