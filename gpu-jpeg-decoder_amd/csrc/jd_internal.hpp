@@ -101,12 +101,13 @@ struct alignas(16) ImgDesc {
     uint64_t planes;                  // fancy upsampling: device address of the int16 component planes
     uint32_t qmask;                   // k_idct_color's range test of quantised AC coefficients (bits
                                       // k..15 and 16+k..31: |c| <= 2^(k-1), 2^(k-1) * max step < 2^16)
-    uint32_t pad[3];
+    uint32_t entry_cap;               // AC-entry slots of this image (entry indices are image-relative)
+    uint64_t entry_base;              // first AC-entry slot of this image in BatchDev::entries
 };
 static_assert(sizeof(ImgDesc) % 16 == 0, "ImgDesc must stay 16-byte aligned");
 
 // Per-block result of the Huffman kernel (sparse coefficient representation):
-//   entry_start = index of the block's first AC entry in the entry array
+//   entry_start = index of the block's first AC entry, relative to its image's ImgDesc::entry_base
 //   cnt_dc      = (number of AC entries << 26) | (DC difference & 0x3FFFFFF): the quantised DC
 //                 difference as a 26-bit two's complement value; k_idct_color predicts the DC
 // AC entry = (int16 value << 16) | zig-zag index (1..63).
@@ -186,7 +187,7 @@ struct BatchDev {
     const uint32_t* seg_img;      // image of each segment
     uint32_t* seg_cstart;         // first un-stuffed byte of each segment (image-relative)
     uint32_t* seg_cend;           // end of each segment's data (image-relative, un-stuffed)
-    const uint32_t* seg_entry;    // first AC-entry slot of each segment
+    const uint32_t* seg_entry;    // first AC-entry slot of each segment (image-relative)
     uint32_t* seg_sub_base;       // first piece slot of each segment
     uint32_t* seg_nsub;           // pieces of each segment
     uint32_t nseg;

@@ -492,8 +492,9 @@ struct SegInfo {
     uint32_t bits;     // un-stuffed data bits of the interval
     uintptr_t data;    // address of the interval's first un-stuffed byte
     uintptr_t last;    // last mapped 16-byte chunk of the image's un-stuffed region
-    uint32_t ent0;     // first AC-entry slot of the interval
+    uint32_t ent0;     // first AC-entry slot of the interval (image-relative)
     uint32_t pattern, bpm;
+    uint32_t* eimg;    // the image's AC entries (BatchDev::entries + ImgDesc::entry_base)
 };
 
 __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo& S) {
@@ -511,6 +512,7 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
     S.data = uintptr_t(im.comp) + cstart;
     S.last = (uintptr_t(im.comp) + (im.len - im.ecs_off) + 63) & ~uintptr_t(15);
     S.ent0 = b.seg_entry[s];
+    S.eimg = b.entries + im.entry_base;
     S.pattern = im.block_pattern;
     S.bpm = im.bpm;
 }
@@ -529,6 +531,7 @@ __device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
     S.nblk = 0;
     S.blk0 = 0;
     S.ent0 = 0;
+    S.eimg = b.entries;
     S.pattern = 0;
     S.bpm = 1;
 }
@@ -683,7 +686,7 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
     BitRow R;
     R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
     BlockInfo* const bout = b.blocks + W.blk0;
-    uint32_t* const eout = b.entries;
+    uint32_t* const eout = S.eimg;
     const uint32_t nblk = W.nmcu * S.bpm;
     const uint32_t bpm3 = 3u * S.bpm;
     const uint32_t lbase = lds_addr(s_lutw);
@@ -1831,10 +1834,10 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
     if (have) {
         // a block of a corrupt stream may never have been written: never index past the entries
         int cnt = int(bi.cnt_dc >> 26);
-        if (uint64_t(bi.entry_start) + uint64_t(cnt) > b.entries_cap) cnt = 0;
+        if (uint64_t(bi.entry_start) + uint64_t(cnt) > im.entry_cap) cnt = 0;
         // entries in 16-byte loads, four in flight at a time (the entry buffer is padded by 64 B)
         const uint32_t lead = bi.entry_start & 3u;
-        const uint32_t* ep = b.entries + (bi.entry_start - lead);
+        const uint32_t* ep = b.entries + im.entry_base + (bi.entry_start - lead);
         const int n4 = cnt > 0 ? int(lead + uint32_t(cnt) + 3u) >> 2 : 0;  // cnt == 0: touch nothing
 #if JD_ABL & 4
         if (lane == 1000)

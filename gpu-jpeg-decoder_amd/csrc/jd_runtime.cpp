@@ -237,7 +237,9 @@ struct Plan {
     double pixels = 0, ecs_bytes = 0;
 };
 
-// Largest item prefix [lo, hi) whose sparse-coefficient capacity fits 32-bit entry indices.
+// Largest item prefix [lo, hi) whose sparse-coefficient slots stay within kMaxBatchEntries
+// (entry indices are image-relative; this only bounds the pool, 4 B per slot).
+constexpr uint64_t kMaxBatchEntries = 8ull << 30;
 int batch_split(jd_ctx* ctx, int lo, int n) {
     uint64_t cap = 0;
     int hi = lo;
@@ -245,7 +247,7 @@ int batch_split(jd_ctx* ctx, int lo, int n) {
         if (ctx->pst[hi] != JD_OK) continue;
         const jd_header& h = ctx->parsed[hi].hdr;
         const uint64_t blocks = uint64_t(h.mcux) * h.mcuy * h.blocks_per_mcu;
-        if (hi > lo && cap + blocks * 64 > 0xF0000000ull) break;
+        if (hi > lo && cap + blocks * 64 > kMaxBatchEntries) break;
         cap += blocks * 64;
     }
     return hi;
@@ -346,6 +348,10 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         if (ctx->pst[it] != JD_OK) continue;
         const ParsedJpeg& pj = ctx->parsed[it];
         const jd_header& h = pj.hdr;
+        if (uint64_t(h.mcux) * h.mcuy * entry_slots_per_mcu(uint32_t(h.blocks_per_mcu)) > 0xFFFFFF00ull) {
+            ctx->pst[it] = JD_ERR_CAPACITY;  // image-relative entry indices are 32-bit
+            continue;
+        }
         bool same_tables = prev && prev->hdr.ncomp == h.ncomp;
         for (int c = 0; same_tables && c < h.ncomp; c++) {
             const HuffSpec &d0 = pj.dc[pj.td[c]], &d1 = prev->dc[prev->td[c]];
@@ -454,13 +460,15 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             const ParsedJpeg& pj = ctx->parsed[pi.item];
             ImgDesc& d = P.imgs[i];
             fill_desc(pj, items[pi.item], dev_addr[pi.item], out_addr[pi.item], pi, d);
+            d.entry_base = pi.entry_base;
+            d.entry_cap = uint32_t(uint64_t(d.mcux) * d.mcuy * entry_slots_per_mcu(d.bpm));
             P.item_of_img[i] = pi.item;
             const uint32_t nmcu = d.mcux * d.mcuy;
             const uint64_t per = entry_slots_per_mcu(d.bpm);
             for (uint32_t k = 0; k < d.nseg; k++) {
                 const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
                 P.seg_img[d.seg_base + k] = uint32_t(i);
-                P.seg_entry[d.seg_base + k] = uint32_t(pi.entry_base + uint64_t(std::min(m0, nmcu)) * per);
+                P.seg_entry[d.seg_base + k] = uint32_t(uint64_t(std::min(m0, nmcu)) * per);  // image-relative
             }
         }
     });
@@ -495,7 +503,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     if (ctx->host_timing) std::fprintf(stderr, "plan imgs %.3f descs %.3f pieces %.3f ms\n", tb_imgs, tb_segs - tb_imgs, tbms() - tb_segs);
     if (sub > 0x7FFFFFFFull) return JD_ERR_CAPACITY;
     P.nsub = uint32_t(sub);
-    if (entry_cursor > 0xFFFFFFFFull) return JD_ERR_CAPACITY;
+
     P.total_entry_cap = entry_cursor;
     return JD_OK;
 }
