@@ -100,6 +100,9 @@ def main():
     ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact vs the oracle")
     ap.add_argument("--path", default="auto", choices=["auto", "sync", "lanes"],
                     help="entropy-decode path (auto: lanes for images with restart intervals)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one blocking jd_decode_batch per step instead of jd_decode_batch_async (which "
+                         "parses and plans step k+1 on the host while the GPU decodes step k)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -153,8 +156,10 @@ def main():
     ecs = float(sum(len(d) - h.ecs_offset for d, h in zip(datas, hdrs)))
     jpeg_bytes = float(sum(len(d) for d in datas))
 
+    pipelined = not args.no_pipeline
     for _ in range(args.warmup):
-        dec.decode_prepared(prepared)
+        dec.decode_prepared(prepared, pipelined=pipelined)
+    dec.wait()
     status = [r.status for r in prepared[1]]
     if any(status):
         raise SystemExit(f"decode failed: statuses {sorted(set(status))}")
@@ -178,7 +183,8 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        dec.decode_prepared(prepared)
+        dec.decode_prepared(prepared, pipelined=pipelined)
+    dec.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -218,7 +224,7 @@ def main():
             "config": {"workload": desc, "config": args.config, "images_per_rank": batch,
                        "global_batch": batch * world, "width": W, "height": H, "subsampling": ss,
                        "restart_rows": rrows, "parallelism": f"dp{world} (image sharding)",
-                       "entropy_path": args.path},
+                       "entropy_path": args.path, "host_pipelined": pipelined},
             "images_per_s": tot_img / t_max,
             "jpeg_MB_per_s": tot_bytes / t_max / 1e6,
             "ecs_MB_per_s": tot_ecs / t_max / 1e6,

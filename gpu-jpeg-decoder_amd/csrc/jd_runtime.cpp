@@ -114,6 +114,28 @@ class Pool {
 
 }  // namespace
 
+// One launched batch whose results are not collected yet (jd_decode_batch_async keeps two in
+// flight: the host plans batch k+1 while the GPU decodes batch k).
+struct Pending {
+    bool active = false;
+    jd_result* results = nullptr;
+    int lo = 0, hi = 0;
+    std::vector<jd_status> pst;                 // per item lo..hi: host-side status
+    std::vector<int> w, h;                      // per item
+    std::vector<int> item_of_img;
+    std::vector<std::array<uint64_t, 3>> host_copies;  // {host dst, device src, bytes} (host output)
+    uint32_t nimg = 0;
+    void* host = nullptr;                       // pinned: u64 counters[2], then u32 status[nimg]
+    size_t host_cap = 0;
+    void* plan_host = nullptr;                  // pinned staging of this slot's plan blob
+    size_t plan_cap = 0;
+    hipEvent_t done = nullptr;
+    hipEvent_t ev[JD_NUM_KERNELS][2] = {};
+    bool timing = false, fancy = false;
+    double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0;
+    double t_plan = 0, t_upload = 0;
+};
+
 struct jd_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -132,9 +154,10 @@ struct jd_ctx {
 
     // pools
     DevBuf plan, chunk_brk, blocks, entries, input, output, comp, planes;
-    PinBuf plan_host, input_host;
+    PinBuf input_host;
 
-    hipEvent_t ev[JD_NUM_KERNELS][2] = {};
+    Pending pend[2];
+    int slot = 0;  // the slot the next launch uses
     jd_stats stats{};
 
     std::vector<ParsedJpeg> parsed;
@@ -161,7 +184,10 @@ jd_status hip_fail(jd_ctx* ctx, hipError_t e, const char* what) {
 hipError_t ensure_dev(DevBuf& b, size_t bytes) {
     if (bytes <= b.cap) return hipSuccess;
     const size_t n = std::max(bytes, b.cap + b.cap / 2);
-    if (b.p) (void)hipFree(b.p);
+    if (b.p) {
+        (void)hipDeviceSynchronize();  // a launched batch may still use it (jd_decode_batch_async)
+        (void)hipFree(b.p);
+    }
     b.p = nullptr;
     b.cap = 0;
     hipError_t e = hipMalloc(&b.p, n);
@@ -322,7 +348,7 @@ void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uin
     }
     d.nchunks = pi.nchunks;  // scan chunks over [align16(file + ecs_off), file + len)
     d.chunk_base = pi.chunk_base;
-    d.comp = pi.comp;  // offset for now; rebased onto the pool in run_batch
+    d.comp = pi.comp;  // offset for now; rebased onto the pool in launch_batch
 }
 
 // Entry slots per MCU: 63 per block (a block stores at most 63) plus 3 for aligning piece starts
@@ -523,8 +549,30 @@ size_t reserve(size_t& end, size_t bytes) {
     return off;
 }
 
-jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result* results, int rgb_on_device,
-                    hipStream_t s) {
+jd_status finish_batch(jd_ctx* ctx, Pending& pd);
+
+// Grow-only pinned buffer of a pending slot (the slot is idle when this is called).
+hipError_t ensure_pinned(void*& p, size_t& cap, size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    const size_t n = std::max(bytes, cap + cap / 2);
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+// Parses nothing (parse_all did), plans items [lo, hi), uploads the plan and launches every kernel
+// on stream s into the context's current pending slot, which it leaves active; finish_batch
+// collects it.
+jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result* results, int rgb_on_device,
+                       hipStream_t s) {
+    Pending& pd = ctx->pend[ctx->slot];
+    if (pd.active) {
+        const jd_status fst = finish_batch(ctx, pd);
+        if (fst != JD_OK) return fst;
+    }
     // 1. inputs and outputs on the device
     std::vector<uint64_t> dev_addr(size_t(hi), 0), out_addr(size_t(hi), 0);
     size_t in_bytes = 0, out_bytes = 0;
@@ -623,9 +671,9 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         const size_t o_tdc = reserve(end, size_t(P.total_tiles) * sizeof(DcPred));
         const size_t o_slow = reserve(end, size_t(P.total_tiles) * 8);
         HIPCHK(ctx, ensure_dev(ctx->plan, end));
-        HIPCHK(ctx, ensure_pin(ctx->plan_host, upload));
-        memcpy(ctx->plan_host.p, blob.data(), upload);
-        HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, ctx->plan_host.p, upload, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, ensure_pinned(pd.plan_host, pd.plan_cap, upload));
+        memcpy(pd.plan_host, blob.data(), upload);
+        HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, pd.plan_host, upload, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, ensure_dev(ctx->chunk_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
         HIPCHK(ctx, ensure_dev(ctx->blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
         HIPCHK(ctx, ensure_dev(ctx->entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
@@ -689,9 +737,9 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
         const double t_upload = tms();
         double t_k[JD_NUM_KERNELS];
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
-            if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][0], s));
+            if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][0], s));
             HIPCHK(ctx, launch_kernel(k, b, s));
-            if (timing) HIPCHK(ctx, hipEventRecord(ctx->ev[k][1], s));
+            if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][1], s));
             t_k[k] = tms();
         }
         if (ctx->host_timing) {
@@ -699,68 +747,119 @@ jd_status run_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result
             for (int k = 0; k < JD_NUM_KERNELS; k++) std::fprintf(stderr, " %.3f", t_k[k]);
             std::fprintf(stderr, "\n");
         }
-        std::vector<uint32_t> status(nimg);
-        unsigned long long ctr[2] = {0, 0};
-        HIPCHK(ctx, hipMemcpyAsync(status.data(), b.status, nimg * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(ctx, hipMemcpyAsync(ctr, b.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
-        const double t_launch = tms();
-        HIPCHK(ctx, hipStreamSynchronize(s));
-        if (ctx->host_timing)
-            std::fprintf(stderr, "host plan %.3f upload %.3f launch %.3f sync %.3f ms\n", t_plan, t_upload - t_plan,
-                         t_launch - t_upload, tms() - t_launch);
+        HIPCHK(ctx, ensure_pinned(pd.host, pd.host_cap, 16 + size_t(nimg) * 4));
+        HIPCHK(ctx, hipMemcpyAsync(pd.host, b.counters, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(pd.host) + 16, b.status, nimg * 4, hipMemcpyDeviceToHost, s));
+        pd.timing = timing;
+        pd.fancy = fancy;
+        pd.blocks = double(P.total_blocks);
+        pd.pixels = P.pixels;
+        pd.ecs = P.ecs_bytes;
+        pd.nsub = double(nsub);
+        pd.nseg = double(nseg);
+        pd.chunks = double(P.total_chunks);
+        pd.tiles = double(P.total_tiles);
+        pd.piece_bits = double(P.piece_bits);
+        pd.t_plan = t_plan;
+        pd.t_upload = t_upload - t_plan;
+    }
+    pd.nimg = nimg;
+    pd.item_of_img = P.item_of_img;
+    pd.results = results;
+    pd.lo = lo;
+    pd.hi = hi;
+    pd.pst.assign(ctx->pst.begin() + lo, ctx->pst.begin() + hi);
+    pd.w.resize(size_t(hi - lo));
+    pd.h.resize(size_t(hi - lo));
+    pd.host_copies.clear();
+    for (int i = lo; i < hi; i++) {
+        pd.w[i - lo] = ctx->parsed[i].hdr.width;
+        pd.h[i - lo] = ctx->parsed[i].hdr.height;
+        if (!rgb_on_device && out_addr[i] && items[i].rgb && ctx->pst[i] == JD_OK)
+            pd.host_copies.push_back({reinterpret_cast<uint64_t>(items[i].rgb), out_addr[i],
+                                      uint64_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3});
+    }
+    HIPCHK(ctx, hipEventRecord(pd.done, s));
+    pd.active = true;
+    ctx->slot ^= 1;
+    return JD_OK;
+}
+
+// Waits for a launched batch and collects it: per-image status (a kernel's corrupt flag
+// overrides OK), results, host copies of RGB, statistics.
+jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
+    if (!pd.active) return JD_OK;
+    pd.active = false;
+    const auto tw0 = std::chrono::steady_clock::now();
+    HIPCHK(ctx, hipEventSynchronize(pd.done));
+    const uint32_t nimg = pd.nimg;
+    if (nimg) {
+        const unsigned long long* ctr = static_cast<const unsigned long long*>(pd.host);
+        const uint32_t* status = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pd.host) + 16);
         for (uint32_t i = 0; i < nimg; i++)
-            if (status[i]) ctx->pst[P.item_of_img[i]] = JD_ERR_CORRUPT;
+            if (status[i]) pd.pst[size_t(pd.item_of_img[i] - pd.lo)] = JD_ERR_CORRUPT;
+        if (ctx->host_timing)
+            std::fprintf(stderr, "host plan %.3f upload %.3f wait %.3f ms\n", pd.t_plan, pd.t_upload,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count());
 
         // algorithmic bytes per kernel
         jd_stats& S = ctx->stats;
         const double entries = double(ctr[0]);
-        const double blocks = double(P.total_blocks);
-        const double ecs = P.ecs_bytes;
-        const double nsubd = double(nsub), nsegd = double(nseg);
-        const double overlap_factor = (double(P.piece_bits) + kPieceOverlap) / double(P.piece_bits);
+        const double blocks = pd.blocks, ecs = pd.ecs, nsubd = pd.nsub, nsegd = pd.nseg;
+        const bool fancy = pd.fancy;
+        const double overlap_factor = (pd.piece_bits + kPieceOverlap) / pd.piece_bits;
         const double bytes[JD_NUM_KERNELS] = {
             ecs,                                               // k_scan: read the ECS once
-            double(P.total_chunks) * 12 + nsegd * 8,           // k_index: per-chunk counters, boundaries
+            pd.chunks * 12 + nsegd * 8,                        // k_index: per-chunk counters, boundaries
             2 * ecs,                                           // k_compact: read + write the ECS
             nsubd * 4 + nsegd * 16,                            // k_subplan: piece map
             ecs * std::min(overlap_factor, 2.0) + nsubd * 16,  // k_piece_scan: bits incl. overlap, counts out
             nsubd * 8,                                         // k_rescan: start/end check per piece
             nsubd * 28,                                        // k_chain: counts in, offsets out
             ecs + blocks * 8 + entries * 4,                    // k_piece_write: ECS in, sparse coefficients out
-            blocks * 8 + double(P.total_tiles) * 48,           // k_dc_pred: BlockInfo read, tile sums, scan
-            blocks * 8 + entries * 4 + (fancy ? blocks * 128 : P.pixels * 3),  // k_idct_color: coefficients in,
-                                                                                // RGB (fancy: planes) out
-            fancy ? blocks * 128 + P.pixels * 3 : 0.0};        // k_colour_fancy: planes in, RGB out
+            blocks * 8 + pd.tiles * 48,                        // k_dc_pred: BlockInfo read, tile sums, scan
+            blocks * 8 + entries * 4 + (fancy ? blocks * 128 : pd.pixels * 3),  // k_idct_color: coefficients
+                                                                                 // in, RGB (fancy: planes) out
+            fancy ? blocks * 128 + pd.pixels * 3 : 0.0};       // k_colour_fancy: planes in, RGB out
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
             if (k == 10 && !fancy) continue;  // k_colour_fancy runs only with the flag
             S.launches[k]++;
             S.bytes[k] += bytes[k];
-            if (timing) {
+            if (pd.timing) {
                 float ms = 0;
-                HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev[k][0], ctx->ev[k][1]));
+                HIPCHK(ctx, hipEventElapsedTime(&ms, pd.ev[k][0], pd.ev[k][1]));
                 S.total_ms[k] += ms;
             }
         }
         S.batches += 1;
         S.images += nimg;
-        S.pixels += P.pixels;
-        S.ecs_bytes += P.ecs_bytes;
+        S.pixels += pd.pixels;
+        S.ecs_bytes += pd.ecs;
         S.blocks += blocks;
-        S.segments += double(nseg);
-        S.subsequences += double(nsub);
+        S.segments += nsegd;
+        S.subsequences += nsubd;
     }
+    for (int i = pd.lo; i < pd.hi; i++) {
+        const jd_status st = pd.pst[size_t(i - pd.lo)];
+        pd.results[i].status = st;
+        const bool dims = st == JD_OK || st == JD_ERR_CORRUPT;
+        pd.results[i].width = dims ? pd.w[size_t(i - pd.lo)] : 0;
+        pd.results[i].height = dims ? pd.h[size_t(i - pd.lo)] : 0;
+    }
+    if (!pd.host_copies.empty()) {
+        for (const auto& c : pd.host_copies)
+            HIPCHK(ctx, hipMemcpy(reinterpret_cast<void*>(c[0]), reinterpret_cast<const void*>(c[1]), c[2],
+                                  hipMemcpyDeviceToHost));
+    }
+    return JD_OK;
+}
 
-    // 3. results (and host copies when the caller asked for host output)
-    for (int i = lo; i < hi; i++) {
-        results[i].status = ctx->pst[i];
-        results[i].width = ctx->pst[i] == JD_OK || ctx->pst[i] == JD_ERR_CORRUPT ? ctx->parsed[i].hdr.width : 0;
-        results[i].height = ctx->pst[i] == JD_OK || ctx->pst[i] == JD_ERR_CORRUPT ? ctx->parsed[i].hdr.height : 0;
-        if (!rgb_on_device && out_addr[i] && items[i].rgb) {
-            const size_t n = size_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3;
-            HIPCHK(ctx, hipMemcpyAsync(items[i].rgb, reinterpret_cast<void*>(out_addr[i]), n, hipMemcpyDeviceToHost, s));
-        }
+// Collects every launched batch, oldest first.
+jd_status finish_all(jd_ctx* ctx) {
+    for (int k = 0; k < 2; k++) {
+        const jd_status st = finish_batch(ctx, ctx->pend[(ctx->slot + k) & 1]);
+        if (st != JD_OK) return st;
     }
-    if (!rgb_on_device) HIPCHK(ctx, hipStreamSynchronize(s));
     return JD_OK;
 }
 
@@ -813,12 +912,15 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
         delete ctx;
         return JD_ERR_HIP;
     }
-    for (int k = 0; k < JD_NUM_KERNELS; k++)
-        for (int j = 0; j < 2; j++)
-            if (hipEventCreate(&ctx->ev[k][j]) != hipSuccess) {
-                delete ctx;
-                return JD_ERR_HIP;
-            }
+    for (Pending& pd : ctx->pend) {
+        bool ok = hipEventCreateWithFlags(&pd.done, hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; k < JD_NUM_KERNELS; k++)
+            for (int j = 0; j < 2; j++) ok = ok && hipEventCreate(&pd.ev[k][j]) == hipSuccess;
+        if (!ok) {
+            jd_ctx_destroy(ctx);
+            return JD_ERR_HIP;
+        }
+    }
     *out = ctx;
     return JD_OK;
 }
@@ -829,11 +931,15 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_brk, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output, &ctx->comp})
         if (b->p) (void)hipFree(b->p);
-    for (PinBuf* b : {&ctx->plan_host, &ctx->input_host})
-        if (b->p) (void)hipHostFree(b->p);
-    for (int k = 0; k < JD_NUM_KERNELS; k++)
-        for (int j = 0; j < 2; j++)
-            if (ctx->ev[k][j]) (void)hipEventDestroy(ctx->ev[k][j]);
+    if (ctx->input_host.p) (void)hipHostFree(ctx->input_host.p);
+    for (Pending& pd : ctx->pend) {
+        if (pd.host) (void)hipHostFree(pd.host);
+        if (pd.plan_host) (void)hipHostFree(pd.plan_host);
+        if (pd.done) (void)hipEventDestroy(pd.done);
+        for (int k = 0; k < JD_NUM_KERNELS; k++)
+            for (int j = 0; j < 2; j++)
+                if (pd.ev[k][j]) (void)hipEventDestroy(pd.ev[k][j]);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return JD_OK;
@@ -848,13 +954,24 @@ jd_status jd_parse(const uint8_t* jpeg, size_t len, jd_header* hdr) {
     return st;
 }
 
-jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results, int rgb_on_device,
-                          void* hip_stream) {
+namespace {
+// Parse on the host, then plan + launch every sub-batch; async leaves the last one launched
+// (each launch first collects the batch two launches back, whose slot it reuses).
+jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results, int rgb_on_device,
+                       void* hip_stream, bool async) {
     if (!ctx || n < 0 || (n > 0 && (!items || !results))) return JD_ERR_INVALID_ARG;
     for (int i = 0; i < n; i++)
         if (!items[i].jpeg || items[i].len > 0xFFFFFFF0ull) return JD_ERR_INVALID_ARG;
     if (hipSetDevice(ctx->device) != hipSuccess) return JD_ERR_HIP;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    // the host input staging buffer is reused per launch: with host inputs, collect first
+    bool host_inputs = false;
+    for (int i = 0; i < n && !host_inputs; i++) host_inputs = !items[i].jpeg_dev;
+    if (host_inputs || !rgb_on_device) {
+        const jd_status st = finish_all(ctx);
+        if (st != JD_OK) return st;
+        async = false;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     parse_all(ctx, items, n);
     if (ctx->host_timing)
@@ -862,11 +979,31 @@ jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* r
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     for (int lo = 0; lo < n;) {
         const int hi = batch_split(ctx, lo, n);
-        jd_status st = run_batch(ctx, items, lo, hi, results, rgb_on_device, s);
+        jd_status st = launch_batch(ctx, items, lo, hi, results, rgb_on_device, s);
         if (st != JD_OK) return st;
+        if (async) {  // collect the previous launch (its slot is the current one now)
+            st = finish_batch(ctx, ctx->pend[ctx->slot]);
+            if (st != JD_OK) return st;
+        }
         lo = hi;
     }
-    return JD_OK;
+    return async ? JD_OK : finish_all(ctx);
+}
+}  // namespace
+
+jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results, int rgb_on_device,
+                          void* hip_stream) {
+    return decode_batch(ctx, items, n, results, rgb_on_device, hip_stream, false);
+}
+
+jd_status jd_decode_batch_async(jd_ctx* ctx, const jd_item* items, int n, jd_result* results, void* hip_stream) {
+    return decode_batch(ctx, items, n, results, 1, hip_stream, true);
+}
+
+jd_status jd_decode_wait(jd_ctx* ctx) {
+    if (!ctx) return JD_ERR_INVALID_ARG;
+    if (hipSetDevice(ctx->device) != hipSuccess) return JD_ERR_HIP;
+    return finish_all(ctx);
 }
 
 jd_status jd_decode(jd_ctx* ctx, const uint8_t* jpeg, size_t len, uint8_t* rgb, int rgb_on_device, int* width,
@@ -952,6 +1089,8 @@ jd_status jd_memcpy_d2h(jd_ctx* ctx, void* dst, const void* src, size_t n) {
 
 jd_status jd_synchronize(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
+    const jd_status st = finish_all(ctx);
+    if (st != JD_OK) return st;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return JD_OK;
 }

@@ -32,7 +32,7 @@ JD_FLAG_FORCE_SYNC = 2
 JD_FLAG_FORCE_LANES = 4
 JD_FLAG_FANCY_UPSAMPLING = 8
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES}
-JD_ABI_VERSION = 2
+JD_ABI_VERSION = 3
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece_scan", "k_rescan", "k_chain",
                 "k_piece_write", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
@@ -77,7 +77,7 @@ class _Stats(ctypes.Structure):
 # Every symbol include/jd.h and include/jd_test.h declare (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = [
     "jd_ctx_create", "jd_ctx_destroy", "jd_parse", "jd_decode", "jd_decode_file", "jd_decode_batch",
-    "jd_write_array", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
+    "jd_decode_batch_async", "jd_decode_wait", "jd_write_array", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
     "jd_memcpy_h2d", "jd_memcpy_d2h", "jd_synchronize", "jd_get_stats", "jd_reset_stats",
     "jd_kernel_name", "jd_test_idct", "jd_test_idct_exact", "jd_test_color", "jd_debug_fetch", "jd_ctx_last_error",
 ]
@@ -105,6 +105,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
                                    ctypes.POINTER(c_int)]),
         "jd_decode_batch": (c_int, [c_void_p, ctypes.POINTER(_Item), c_int, ctypes.POINTER(_Result), c_int,
                                     c_void_p]),
+        "jd_decode_batch_async": (c_int, [c_void_p, ctypes.POINTER(_Item), c_int, ctypes.POINTER(_Result), c_void_p]),
+        "jd_decode_wait": (c_int, [c_void_p]),
         "jd_write_array": (c_int, [ctypes.c_char_p, c_void_p, c_int, c_int]),
         "jd_status_str": (ctypes.c_char_p, [c_int]),
         "jd_abi_version": (c_int, []),
@@ -318,11 +320,22 @@ class Decoder:
             items[i] = _Item(_addr_of(host_datas[i]), dev_ptrs[i], len(host_datas[i]), rgb_ptrs[i])
         return items, (_Result * n)()
 
-    def decode_prepared(self, batch, stream: Optional[int] = None) -> None:
+    def decode_prepared(self, batch, stream: Optional[int] = None, pipelined: bool = False) -> None:
+        """Decode a make_batch() batch.  pipelined=True: jd_decode_batch_async (returns once the
+        batch is launched and the previous one collected; call wait() after the last)."""
         items, results = batch
-        st = self.lib.jd_decode_batch(self.ctx, items, len(items), results, 1, stream)
+        if pipelined:
+            st = self.lib.jd_decode_batch_async(self.ctx, items, len(items), results, stream)
+        else:
+            st = self.lib.jd_decode_batch(self.ctx, items, len(items), results, 1, stream)
         if st != JD_OK:
             raise JDError(st, "jd_decode_batch " + (self.last_error() if st == JD_ERR_HIP else ""))
+
+    def wait(self) -> None:
+        """Collect every pipelined batch (jd_decode_wait)."""
+        st = self.lib.jd_decode_wait(self.ctx)
+        if st != JD_OK:
+            raise JDError(st, "jd_decode_wait " + (self.last_error() if st == JD_ERR_HIP else ""))
 
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define JD_ABI_VERSION 2
+#define JD_ABI_VERSION 3
 
 typedef enum jd_status {
     JD_OK = 0,
@@ -116,6 +116,17 @@ jd_status jd_decode_file(jd_ctx* ctx, const char* path, uint8_t* rgb, size_t rgb
  * returns after the batch completes; per-image status in results[i]. */
 jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
                           int rgb_on_device, void* hip_stream);
+
+/* Pipelined form of jd_decode_batch for inputs and outputs already in device memory (jpeg_dev
+ * and rgb device pointers; other items make it behave as jd_decode_batch): returns once the
+ * batch is launched, after collecting the batch launched before it, so the host parses and plans
+ * batch k+1 while the GPU decodes batch k.  results[] (and the caller's buffers) must stay valid
+ * until the batch is collected: by the next jd_decode_batch_async / jd_decode_batch call on the
+ * context, or by jd_decode_wait. */
+jd_status jd_decode_batch_async(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
+                                void* hip_stream);
+/* Collects every launched batch (fills their results). */
+jd_status jd_decode_wait(jd_ctx* ctx);
 
 /* `.array` text writer: "H W\n", then R, G, B planes as space-terminated decimal ints, one plane
  * per line, no trailing newline.  Replaces JPEGParser::write() (cpp-decoder/src/parser.cpp:197-209)

@@ -74,6 +74,39 @@ def test_device_resident_batch(decoder, golden):
         assert sha(img) == e["sha256"], e["file"]
 
 
+def test_pipelined_batches(decoder, golden):
+    """jd_decode_batch_async: three device-resident batches launched back to back (each call
+    collects the one before), then jd_decode_wait; every result and pixel as the blocking call."""
+    ok = [e for e in golden if e["status"] == 0]
+    groups = [ok[0::3], ok[1::3], ok[2::3]]
+    bufs, batches = [], []
+    for g in groups:
+        hosts = [np.frombuffer(e["data"], np.uint8).copy() for e in g]
+        offs, total = [], 0
+        for h in hosts:
+            offs.append(total)
+            total += (h.nbytes + 255) // 256 * 256
+        din = decoder.alloc(total)
+        for h, o in zip(hosts, offs):
+            din.upload(h, o)
+        sizes = [e["width"] * e["height"] * 3 for e in g]
+        ooffs, ototal = [], 0
+        for sz in sizes:
+            ooffs.append(ototal)
+            ototal += (sz + 255) // 256 * 256
+        dout = decoder.alloc(ototal)
+        bufs.append((din, dout, ooffs, sizes, hosts))
+        batches.append(decoder.make_batch(hosts, [din.ptr + o for o in offs], [dout.ptr + o for o in ooffs]))
+    for bt in batches:
+        decoder.decode_prepared(bt, pipelined=True)
+    decoder.wait()
+    for g, bt, (din, dout, ooffs, sizes, hosts) in zip(groups, batches, bufs):
+        assert [r.status for r in bt[1]] == [0] * len(g)
+        assert [(r.width, r.height) for r in bt[1]] == [(e["width"], e["height"]) for e in g]
+        for e, o, sz in zip(g, ooffs, sizes):
+            assert sha(dout.download(np.empty(sz, np.uint8), o)) == e["sha256"], e["file"]
+
+
 @pytest.mark.parametrize("w,h,ss,rows,blocks,q", [
     (1920, 1080, "4:2:0", 1, 0, 90),   # BASELINE config 2 shape
     (1920, 1080, "4:2:0", 0, 0, 90),   # no DRI: single segment
