@@ -139,6 +139,8 @@ constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
 #endif
 constexpr uint32_t kPieceBits = JD_PIECE_BITS;
 constexpr uint32_t kPieceOverlap = JD_PIECE_OVERLAP;
+constexpr uint32_t kMinPieceBits = 512;      // adaptive floor (small batches)
+constexpr uint64_t kPieceTarget = 65536;    // pieces wanted per batch before shrinking stops
 constexpr int kPieceThreads = 256;  // one workgroup shares one copy of its table set in LDS
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.

@@ -132,7 +132,7 @@ struct Pending {
     hipEvent_t done = nullptr;
     hipEvent_t ev[JD_NUM_KERNELS][2] = {};
     bool timing = false, fancy = false;
-    double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0;
+    double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0, piece_overlap = 0;
     double t_plan = 0, t_upload = 0;
 };
 
@@ -256,7 +256,7 @@ struct Plan {
     std::vector<TableSet> tablesets;
     std::vector<uint16_t> qtabs;
     std::vector<uint32_t> seg_img, seg_entry, wg_tableset;
-    uint32_t piece_bits = kPieceBits;
+    uint32_t piece_bits = kPieceBits, piece_overlap = kPieceOverlap;
     std::vector<uint32_t> chain_seg, chain_wg_tableset;  // k_chain lanes, grouped by table set
     uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0;
     uint64_t total_blocks = 0, total_entry_cap = 0, comp_bytes = 0;
@@ -509,7 +509,18 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     std::vector<uint32_t> order(nimg);
     for (size_t i = 0; i < order.size(); i++) order[i] = uint32_t(i);
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return pim[a].ts < pim[b].ts; });
-    P.piece_bits = (ctx->flags & JD_FLAG_FORCE_SYNC) ? 1024u : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u : kPieceBits;
+    // Piece size: kPieceBits for full batches; a small batch (one image, a few) gets shorter pieces
+    // so it still spreads over ~kPieceTarget lanes — a lane walks piece_bits + overlap bits, so
+    // single-image latency falls with the piece size while the overlap (sync distance) is fixed.
+    uint64_t ecs_bits = 0;
+    for (const ImgDesc& d : P.imgs) ecs_bits += uint64_t(d.len - d.ecs_off) * 8;
+    uint32_t adaptive = kPieceBits;
+    while (adaptive > kMinPieceBits && ecs_bits / adaptive < kPieceTarget) adaptive >>= 1;
+    P.piece_bits = (ctx->flags & JD_FLAG_FORCE_SYNC) ? 1024u : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u : adaptive;
+    // shorter pieces also get a shorter warm-up: a lane that has not synchronised by then is
+    // re-scanned (k_rescan / k_chain), which costs less than every lane walking 4096 extra bits
+    P.piece_overlap = (ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES)) ? kPieceOverlap
+                                                                             : std::min(kPieceOverlap, 2 * adaptive);
     uint64_t sub = 0;
     P.chain_seg.reserve(seg_cursor + kPieceThreads * P.tablesets.size());
     for (size_t oi = 0; oi < order.size();) {
@@ -700,7 +711,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.nchain = uint32_t(P.chain_seg.size());
         b.chain_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_chts);
         b.piece_bits = P.piece_bits;
-        b.piece_overlap = kPieceOverlap;
+        b.piece_overlap = P.piece_overlap;
         uint32_t* const pc[6] = {reinterpret_cast<uint32_t*>(base + o_piece[0]), reinterpret_cast<uint32_t*>(base + o_piece[1]),
                                  reinterpret_cast<uint32_t*>(base + o_piece[2]), reinterpret_cast<uint32_t*>(base + o_piece[3]),
                                  reinterpret_cast<uint32_t*>(base + o_piece[4]), reinterpret_cast<uint32_t*>(base + o_piece[5])};
@@ -760,6 +771,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         pd.chunks = double(P.total_chunks);
         pd.tiles = double(P.total_tiles);
         pd.piece_bits = double(P.piece_bits);
+        pd.piece_overlap = double(P.piece_overlap);
         pd.t_plan = t_plan;
         pd.t_upload = t_upload - t_plan;
     }
@@ -807,7 +819,7 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
         const double entries = double(ctr[0]);
         const double blocks = pd.blocks, ecs = pd.ecs, nsubd = pd.nsub, nsegd = pd.nseg;
         const bool fancy = pd.fancy;
-        const double overlap_factor = (pd.piece_bits + kPieceOverlap) / pd.piece_bits;
+        const double overlap_factor = (pd.piece_bits + pd.piece_overlap) / pd.piece_bits;
         const double bytes[JD_NUM_KERNELS] = {
             ecs,                                               // k_scan: read the ECS once
             pd.chunks * 12 + nsegd * 8,                        // k_index: per-chunk counters, boundaries
