@@ -189,6 +189,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if any(r.status for r in prepared[1]):  # the last timed batch's per-image statuses
+        raise SystemExit("decode failed inside the timed region")
     st = dec.stats()
 
     # one all-gather of per-rank counters (RCCL over xGMI when N > 1)
