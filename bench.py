@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--quality", type=int, default=90)
     ap.add_argument("--cpu-sample", type=int, default=-1, help="images for the CPU baseline (-1 auto, 0 off)")
     ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact vs the oracle")
-    ap.add_argument("--path", default="auto", choices=["auto", "sync", "lanes"],
+    ap.add_argument("--path", default="auto", choices=["auto", "sync", "lanes", "full"],
                     help="entropy-decode path (auto: lanes for images with restart intervals)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one blocking jd_decode_batch per step instead of jd_decode_batch_async (which "

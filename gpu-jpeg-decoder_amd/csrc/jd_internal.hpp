@@ -34,6 +34,11 @@ constexpr int kLutSize = 1 << kLutBits;
 //     bit  15     dc   DC symbol
 //     bits 16..20 sz   magnitude bits (DC: symbol, AC: symbol & 15)
 //     bit  21     bad  corrupt code (slow path only)
+//   AC tables also describe the FOLLOWING symbol when the first is not EOB and both fit in the
+//   kLutBits (the scan walk takes two symbols per lookup then; the write walk ignores these bits):
+//     bits 22..25 L2   bits of the second symbol (0: no pair)
+//     bits 26..31 adv2 its advance of z (EOB: 63, which ends any block after an AC symbol)
+//     bit  5      emit2
 //   The coefficient is always EXTEND(the last sz of the L bits), so a decode step is one lookup
 //   plus bit-field extracts.  Codes longer than kLutBits take the canonical slow path:
 //   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not
@@ -49,6 +54,7 @@ struct alignas(16) HuffLut {
 static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
 constexpr int kLutWords = int(sizeof(HuffLut) / 4);
 constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 21;
+constexpr uint32_t kEntEmit2 = 1u << 5;
 
 // Entry of a code of length l for symbol sym; 0 when it cannot be represented (l + sz > 31 or a
 // DC size beyond 16 bits: corrupt for 8-bit baseline, whose DC sizes are <= 11).

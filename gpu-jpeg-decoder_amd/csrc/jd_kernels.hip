@@ -707,6 +707,7 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
 #define JD_FLUSH_Q()                                                                                         \
     do {                                                                                                     \
         if (fq < (ent >> 2)) {                                                                               \
+            if (!(JD_ABL & 8) || ent == 0x7FFFFFFFu)                                                         \
             *reinterpret_cast<uint4*>(eout + 4u * fq) = *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)); \
             fq++;                                                                                            \
         }                                                                                                    \
@@ -840,11 +841,19 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
             uint32_t e = lut_fast(tab, peek);
             if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
             errs |= e;
-            R.skip(e & 31u, row);
             // EOB / ZRL / run-size (parser.cpp:114-134)
-            const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
-            const bool fin = zn >= 63u;
+            uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+            uint32_t L = e & 31u;
             ents += __builtin_amdgcn_ubfe(e & ~zn, 6u, 1u);  // emit flag, unless past index 63
+            const uint32_t L2 = __builtin_amdgcn_ubfe(e, 22u, 4u);
+            if (L2 != 0u && zn < 63u) {  // a pair entry, and the first symbol left the block open
+                const uint32_t z2 = zn + (e >> 26);
+                ents += __builtin_amdgcn_ubfe(e & ~(z2 >> 1), 5u, 1u);  // emit2 unless z2 > 63
+                zn = z2;
+                L += L2;
+            }
+            R.skip(L, row);
+            const bool fin = zn >= 63u;
             z = fin ? 0u : zn;
             b3 += fin ? 3u : 0u;
             tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;

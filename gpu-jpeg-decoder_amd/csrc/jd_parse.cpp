@@ -182,6 +182,18 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
         const int first = codes[i] << shift, last = ((codes[i] + 1) << shift) - 1;
         for (int idx = first; idx <= last; idx++) lut->fast[idx] = e;
     }
+    if (!is_dc) {  // pair entries: the second symbol decoded from the bits left after the first
+        uint32_t one[kLutSize];
+        memcpy(one, lut->fast, sizeof(one));
+        for (uint32_t idx = 0; idx < kLutSize; idx++) {
+            const uint32_t e1 = one[idx], L1 = e1 & 31u;
+            if (e1 == 0 || ((e1 >> 8) & 127u) == 64u || L1 >= uint32_t(kLutBits)) continue;
+            const uint32_t e2 = one[(idx << L1) & (kLutSize - 1)], L2 = e2 & 31u;
+            if (e2 == 0 || L2 > uint32_t(kLutBits) - L1) continue;  // needs bits beyond the index
+            const uint32_t adv2 = ((e2 >> 8) & 127u) == 64u ? 63u : (e2 >> 8) & 127u;
+            lut->fast[idx] = e1 | (L2 << 22) | (adv2 << 26) | ((e2 & kEntEmit) ? kEntEmit2 : 0u);
+        }
+    }
     return true;
 }
 

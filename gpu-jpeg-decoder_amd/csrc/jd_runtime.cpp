@@ -515,7 +515,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     uint64_t ecs_bits = 0;
     for (const ImgDesc& d : P.imgs) ecs_bits += uint64_t(d.len - d.ecs_off) * 8;
     uint32_t adaptive = kPieceBits;
-    while (adaptive > kMinPieceBits && ecs_bits / adaptive < kPieceTarget) adaptive >>= 1;
+    while (!(ctx->flags & JD_FLAG_FULL_PIECES) && adaptive > kMinPieceBits && ecs_bits / adaptive < kPieceTarget) adaptive >>= 1;
     P.piece_bits = (ctx->flags & JD_FLAG_FORCE_SYNC) ? 1024u : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u : adaptive;
     // shorter pieces also get a shorter warm-up: a lane that has not synchronised by then is
     // re-scanned (k_rescan / k_chain), which costs less than every lane walking 4096 extra bits

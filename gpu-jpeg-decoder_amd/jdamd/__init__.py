@@ -31,7 +31,8 @@ JD_FLAG_TIMING = 1
 JD_FLAG_FORCE_SYNC = 2
 JD_FLAG_FORCE_LANES = 4
 JD_FLAG_FANCY_UPSAMPLING = 8
-PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES}
+JD_FLAG_FULL_PIECES = 16
+PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES, "full": JD_FLAG_FULL_PIECES}
 JD_ABI_VERSION = 3
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece_scan", "k_rescan", "k_chain",

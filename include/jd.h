@@ -47,6 +47,9 @@ typedef struct jd_ctx jd_ctx;
  * setting; the flags exist so tests can stress the two extremes of the piece-parallel decode. */
 #define JD_FLAG_FORCE_SYNC 2u  /* 1024-bit pieces: many speculative starts, exercises re-scans */
 #define JD_FLAG_FORCE_LANES 4u /* one piece per restart interval (the whole scan if no DRI) */
+/* Small batches (under ~64 K pieces of 8192 bits) use shorter pieces by default, down to 512 bits
+ * with a 2x-piece warm-up; this flag keeps 8192-bit pieces / 4096-bit warm-up for every batch. */
+#define JD_FLAG_FULL_PIECES 16u
 /* Chroma upsampling: replicate (default; the semantics pinned in DESIGN.md §2) or, with this flag,
  * libjpeg's triangular "fancy" filter for 2x1, 2x2 and 1x2 ratios (closer to libjpeg-turbo /
  * Pillow output; an option beyond the reference, which has no subsampled chroma at all). */

@@ -27,10 +27,11 @@ def golden():
     return entries
 
 
-@pytest.fixture(scope="session", params=["auto", "sync", "lanes"])
+@pytest.fixture(scope="session", params=["auto", "sync", "lanes", "full"])
 def decoder(request):
-    """A decoder per entropy-decode path: default selection, every image through the
-    self-synchronising passes, every image one lane per restart interval."""
+    """A decoder per entropy-decode path: default selection (small batches: short pieces), every
+    image through 1024-bit pieces, every image one lane per restart interval, and the full-batch
+    geometry (8192-bit pieces, 4096-bit warm-up) whatever the batch size."""
     import jdamd
 
     dec = jdamd.Decoder(0, timing=True, path=request.param)
