@@ -29,8 +29,15 @@ constexpr uint8_t kNatOfZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25
                                      38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 typedef __attribute__((address_space(1))) const uint8_t gu8;
+// Output pointers as global (not flat) addresses: a flat store also counts on lgkmcnt, so every
+// LDS wait after it would wait for the store too.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
 
 // ------------------------------------------------------------------------------------------
 // wave / block helpers (wave64)
@@ -1636,19 +1643,20 @@ __device__ __forceinline__ void store24(uint8_t* dst, const uint32_t (&w)[6], ui
     const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
     if (n == 8 && (ad & 3) == 0) {
         if ((ad & 7) == 0) {
-            uint2* d2 = reinterpret_cast<uint2*>(dst);
-            d2[0] = make_uint2(w[0], w[1]);
-            d2[1] = make_uint2(w[2], w[3]);
-            d2[2] = make_uint2(w[4], w[5]);
+            auto d2 = gptr(reinterpret_cast<u32x2*>(dst));
+            d2[0] = u32x2{w[0], w[1]};
+            d2[1] = u32x2{w[2], w[3]};
+            d2[2] = u32x2{w[4], w[5]};
         } else {
-            uint32_t* d1 = reinterpret_cast<uint32_t*>(dst);
+            auto d1 = gptr(reinterpret_cast<uint32_t*>(dst));
 #pragma unroll
             for (int q = 0; q < 6; q++) d1[q] = w[q];
         }
     } else {
+        auto d = gptr(dst);
 #pragma unroll
         for (int k = 0; k < 24; k++)
-            if (uint32_t(k) < 3 * n) dst[k] = uint8_t(w[k / 4] >> (8 * (k % 4)));
+            if (uint32_t(k) < 3 * n) d[k] = uint8_t(w[k / 4] >> (8 * (k % 4)));
     }
 }
 
@@ -1923,7 +1931,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
                 q.y = (uint32_t(blk[8 * r + 2]) & 0xFFFFu) | (uint32_t(blk[8 * r + 3]) << 16);
                 q.z = (uint32_t(blk[8 * r + 4]) & 0xFFFFu) | (uint32_t(blk[8 * r + 5]) << 16);
                 q.w = (uint32_t(blk[8 * r + 6]) & 0xFFFFu) | (uint32_t(blk[8 * r + 7]) << 16);
-                *reinterpret_cast<uint4*>(dst + size_t(r) * (im.mcux * hc * 8)) = q;
+                *gptr(reinterpret_cast<u32x4*>(dst + size_t(r) * (im.mcux * hc * 8))) = u32x4{q.x, q.y, q.z, q.w};
             }
         }
         return;
