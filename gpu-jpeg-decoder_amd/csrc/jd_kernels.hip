@@ -2077,7 +2077,7 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
 struct FancyPlane {
     const int16_t* p;
     uint32_t pitch, rx, ry, cw, ch;
-    __device__ __forceinline__ int at(uint32_t x, uint32_t y) const { return p[size_t(y) * pitch + x]; }
+    __device__ __forceinline__ int at(uint32_t x, uint32_t y) const { return gptr(p)[size_t(y) * pitch + x]; }
 };
 
 __device__ __forceinline__ int fancy_px(const FancyPlane& P, uint32_t x, uint32_t y) {
