@@ -113,11 +113,23 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # one process per GPU; JD_DIST_BACKEND=gloo with more ranks than GPUs rehearses the
+    # multi-rank path on a one-GPU box (ranks then share devices round-robin)
+    backend = os.environ.get("JD_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" or ndev == 0:
+        device_index = local_rank
+    else:
+        device_index = local_rank % ndev
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(device_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", device_index)
+    local_rank = device_index
 
     import jd_synth
     import jdamd
@@ -195,7 +207,8 @@ def main():
 
     # one all-gather of per-rank counters (RCCL over xGMI when N > 1)
     local = torch.tensor([elapsed, pixels * args.steps, batch * args.steps, ecs * args.steps,
-                          jpeg_bytes * args.steps], dtype=torch.float64, device=dev)
+                          jpeg_bytes * args.steps], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
     t_max, (tot_px, tot_img, tot_ecs, tot_bytes) = gather_counters(local, world)
 
     if rank == 0:
@@ -207,7 +220,7 @@ def main():
         per_launch_bytes = kd["bytes"] / max(1, kd["launches"])
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         cpu = None
-        if args.cpu_sample:
+        if args.cpu_sample and world == 1:  # the CPU baseline is an N=1 figure
             cpu = cpu_baseline(hosts, hdrs, args.cpu_sample)
         res = {
             "metric": "MPixels/s decoded (and images/s) at 1/2/4/8 MI355X; % HBM roofline",
