@@ -32,13 +32,17 @@ constexpr int kLutSize = 1 << kLutBits;
 //                      a coefficient lands at z + adv unless that is past 63 (parser.cpp:120-131:
 //                      its magnitude bits are consumed, the value dropped, the block ends)
 //     bit  15     dc   DC symbol
-//     bits 16..20 sz   magnitude bits (DC: symbol, AC: symbol & 15)
-//     bit  21     bad  corrupt code (slow path only)
+//     bits 16..19 sz   magnitude bits (DC: symbol, AC: symbol & 15; a DC size above 15 is corrupt)
+//     bit  7      bad  corrupt code (slow path only)
 //   AC tables also describe the FOLLOWING symbol when the first is not EOB and both fit in the
-//   kLutBits (the scan walk takes two symbols per lookup then; the write walk ignores these bits):
+//   kLutBits; each AC table is built twice, in the format of the walk that reads it:
+//   scan  (k_piece<Scan>, k_rescan, k_chain_fix; HuffLut slot 2 id):
 //     bits 22..25 L2   bits of the second symbol (0: no pair)
 //     bits 26..31 adv2 its advance of z (EOB: 63, which ends any block after an AC symbol)
 //     bit  5      emit2
+//   write (k_piece<Write>; slot 2 id + 1):
+//     bits 20..23 L2   bits of the second symbol (0: no pair)
+//     bits 24..31 sym2 its run/size byte
 //   The coefficient is always EXTEND(the last sz of the L bits), so a decode step is one lookup
 //   plus bit-field extracts.  Codes longer than kLutBits take the canonical slow path:
 //   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not
@@ -53,14 +57,14 @@ struct alignas(16) HuffLut {
 };
 static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
 constexpr int kLutWords = int(sizeof(HuffLut) / 4);
-constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 21;
+constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 7;
 constexpr uint32_t kEntEmit2 = 1u << 5;
 
 // Entry of a code of length l for symbol sym; 0 when it cannot be represented (l + sz > 31 or a
-// DC size beyond 16 bits: corrupt for 8-bit baseline, whose DC sizes are <= 11).
+// DC size beyond 15 bits: corrupt for 8-bit baseline, whose DC sizes are <= 11).
 JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
     const uint32_t sz = is_dc ? sym : (sym & 15u);
-    if (sz > 16u || l + sz > 31u || l == 0u) return 0u;
+    if (sz > 15u || l + sz > 31u || l == 0u) return 0u;
     if (is_dc) return (l + sz) | kEntDc | (sz << 16);
     const uint32_t adv = sym == 0u ? 64u : (sym >> 4) + 1u;
     return (l + sz) | (sz ? kEntEmit : 0u) | (adv << 8) | (sz << 16);

@@ -482,7 +482,7 @@ __device__ __forceinline__ uint32_t huff_slow(const uint32_t* lutw, uint32_t pee
 
 // EXTEND (utils/stream.cpp:44-52) of the last sz bits of the L bits at the top of peek.
 __device__ __forceinline__ int huff_value(uint32_t peek, uint32_t e) {
-    const uint32_t L = e & 31u, sz = __builtin_amdgcn_ubfe(e, 16u, 5u);
+    const uint32_t L = e & 31u, sz = __builtin_amdgcn_ubfe(e, 16u, 4u);
     const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - L, sz);  // width 0 -> 0
     const uint32_t half = (1u << sz) >> 1;
     return int(mag) - (mag < half ? int(2 * half - 1) : 0);
@@ -543,9 +543,11 @@ __device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
     S.bpm = 1;
 }
 
-__device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads) {
+// write: the write walk's table format (jd_internal.hpp), else the scan walks'
+__device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads,
+                                           bool write = false) {
     for (int slot = 0; slot < ts.nslots; slot++) {
-        const uint4* src = reinterpret_cast<const uint4*>(b.luts + ts.lut[slot]);
+        const uint4* src = reinterpret_cast<const uint4*>(b.luts + 2 * ts.lut[slot] + (write ? 1 : 0));
         uint4* dst = reinterpret_cast<uint4*>(s_lut + slot);
         for (int i = threadIdx.x; i < int(sizeof(HuffLut) / 16); i += nthreads) dst[i] = src[i];
     }
@@ -739,20 +741,34 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
             if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
             errs |= e;
             const int val = huff_value(peek, e);
-            R.skip(e & 31u, row);
             // EOB / ZRL / run-size (parser.cpp:114-134)
-            const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
-            const bool fin = zn >= 63u;
+            uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+            uint32_t L = e & 31u;
             const bool emit = (e & ~zn & kEntEmit) != 0;  // zn < 64 (bit 6 of zn clear)
             dcd = (e & kEntDc) ? val : dcd;
             ring[ent & 7u] = (uint32_t(val) << 16) | zn;
             ent += emit ? 1u : 0u;
+            const uint32_t L2 = __builtin_amdgcn_ubfe(e, 20u, 4u);
+            if (L2 != 0u && zn < 63u) {  // a pair entry, and the first symbol left the block open
+                const uint32_t s2 = e >> 24, sz2 = s2 & 15u;
+                const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - (L + L2), sz2);
+                const uint32_t half = (1u << sz2) >> 1;
+                const int v2 = int(mag) - (mag < half ? int(2 * half - 1) : 0);
+                zn += s2 ? (s2 >> 4) + 1u : 64u;
+                ring[ent & 7u] = (uint32_t(v2) << 16) | zn;
+                ent += (sz2 != 0u && zn < 64u) ? 1u : 0u;
+                L += L2;
+            }
+            R.skip(L, row);
+            const bool fin = zn >= 63u;
             pbi0 = fin ? ent_blk : pbi0;
             pbi1 = fin ? pack_cnt_dc(ent - ent_blk, dcd) : pbi1;
             pblk = fin ? blk : pblk;
             pend_b = pend_b || fin;
-            if ((it & 3u) == 0u) JD_FLUSH_Q();
-            if ((it & 1u) == 0u) JD_FLUSH_B();
+            if ((it & 1u) == 0u) {
+                JD_FLUSH_Q();
+                JD_FLUSH_B();
+            }
             if (fin) {
                 blk++;
                 ent_blk = ent;
@@ -945,7 +961,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
-    stage_luts(b, ts, s_lut, kPieceThreads);
+    stage_luts(b, ts, s_lut, kPieceThreads, MODE == kWalkWrite);
     __syncthreads();
 
     const uint32_t u = blockIdx.x * kPieceThreads + threadIdx.x;

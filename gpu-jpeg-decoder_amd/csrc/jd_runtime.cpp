@@ -214,10 +214,11 @@ int lut_id(jd_ctx* ctx, const HuffSpec& s, bool is_dc, uint64_t h) {
             !memcmp(c.spec.vals, s.vals, size_t(s.nvals)))
             return it->second;
     }
-    HuffLut lut;
-    if (!build_lut(s, is_dc, &lut)) return -1;
-    const int id = int(ctx->lut_host.size());
+    HuffLut lut, lut_w;  // slots 2 id (scan format) and 2 id + 1 (write format)
+    if (!build_lut(s, is_dc, &lut, false) || !build_lut(s, is_dc, &lut_w, true)) return -1;
+    const int id = int(ctx->lut_host.size() / 2);
     ctx->lut_host.push_back(lut);
+    ctx->lut_host.push_back(lut_w);
     ctx->lut_specs.push_back(CachedLut{s, is_dc});
     ctx->lut_by_hash.emplace(h, id);
     return id;
