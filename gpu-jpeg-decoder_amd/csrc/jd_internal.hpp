@@ -159,7 +159,10 @@ constexpr int kScanBytesPerThread = 64;
 constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
 constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cannot hold more
 
-constexpr int kCpMax = 8;          // checkpoints per piece (k_rescan / k_chain shortcuts)
+#ifndef JD_CP_MAX
+#define JD_CP_MAX 8
+#endif
+constexpr int kCpMax = JD_CP_MAX;  // checkpoints per piece (k_rescan / k_chain shortcuts)
 constexpr int kCpRecords = kCpMax + 1;
 
 // Speculative-scan checkpoints, kCpRecords per piece slot: kCpMax checkpoints, then the totals.
