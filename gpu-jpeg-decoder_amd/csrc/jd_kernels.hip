@@ -504,6 +504,12 @@ struct SegInfo {
     uint32_t* eimg;    // the image's AC entries (BatchDev::entries + ImgDesc::entry_base)
 };
 
+// The image's last interval: it ends at EOI, not at an RSTn.
+__device__ __forceinline__ bool seg_is_final(const BatchDev& b, uint32_t s) {
+    const ImgDesc& im = b.imgs[b.seg_img[s]];
+    return s + 1 == im.seg_base + im.nseg;
+}
+
 __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo& S) {
     const ImgDesc& im = b.imgs[b.seg_img[s]];
     const uint32_t k_seg = s - im.seg_base;
@@ -1102,10 +1108,28 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const uint64_t ent_cap_end = uint64_t(S.ent0) + seg_entry_cap(S);
+    // The scan's last interval ends at EOI, and what follows its last MCU is ignored (the oracle
+    // stops after the frame's MCUs): the piece whose MCUs reach the interval's count is the last
+    // one that matters, and the pieces after it (decoding trailing bytes) are dropped.
+    uint32_t jl = n - 1;
+    if (seg_is_final(b, s)) {
+        uint32_t run = 0;
+        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            const uint32_t pm = j < n ? (b.piece_nmcu[base + j] & 0x7FFFFFFFu) : 0u;
+            const uint32_t inc = run + uint32_t(wave_scan_dpp(int(pm)));
+            const uint64_t hit = __ballot(j < n && inc >= nmcu_seg);
+            if (hit) {  // wave-uniform
+                jl = j0 + uint32_t(__builtin_ctzll(hit));
+                break;
+            }
+            run = __shfl(inc, 63, 64);
+        }
+    }
     bool need = false;
-    for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+    for (uint32_t j0 = 0; j0 <= jl; j0 += 64) {
         const uint32_t j = j0 + lane;
-        if (j < n) need |= b.piece_bit[base + j] != (j ? b.piece_end[base + j - 1] : 0u);
+        if (j <= jl) need |= b.piece_bit[base + j] != (j ? b.piece_end[base + j - 1] : 0u);
     }
     if (__any(need)) {  // wave-uniform
         if (lane == 0) b.seg_fix[s] = 1u;
@@ -1116,10 +1140,10 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     bool bad = false;
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
         const uint32_t j = j0 + lane;
-        const bool in = j < n;
+        const bool in = j <= jl;  // pieces past jl: no MCUs, no entries
         uint32_t pm = in ? b.piece_nmcu[base + j] : 0u;
         const uint32_t pe = in ? b.piece_nent[base + j] : 0u;
-        const bool last = j + 1 == n;
+        const bool last = j == jl;
         // counting from a verified start is exact, so an error there is the stream's; the last
         // piece's scan runs past the data on purpose (its write lane checks it exactly)
         bad |= in && !last && (pm >> 31);
@@ -1136,7 +1160,7 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
             bad = true;
             pm = 0;
         }
-        if (in) {
+        if (j < n) {
             b.piece_mcu0[base + j] = m0;
             b.piece_nmcu[base + j] = pm;
             b.piece_ent0[base + j] = e0;
@@ -1178,10 +1202,17 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
     const uint32_t nmcu_seg = S.nblk / S.bpm;
-    bool bad = false;
+    const bool final_seg = seg_is_final(b, s);  // trailing bytes after its last MCU are ignored
+    bool bad = false, done = false;
     uint32_t expect = 0, mcu_run = 0, ent_run = S.ent0;
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t u = base + j;
+        if (done) {  // past the piece that completed the final interval: nothing to decode
+            b.piece_mcu0[u] = nmcu_seg;
+            b.piece_nmcu[u] = 0u;
+            b.piece_ent0[u] = (ent_run + 3u) & ~3u;
+            continue;
+        }
         uint32_t pbit = b.piece_bit[u], pend = b.piece_end[u], pm = b.piece_nmcu[u], pe = b.piece_nent[u];
         bool pbad = (pm >> 31) != 0;  // the piece's scan hit an error while counting
         pm &= 0x7FFFFFFFu;
@@ -1202,11 +1233,12 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
         }
         // counting from a verified start is exact, so an error there is the stream's; the last
         // piece's scan runs past the data on purpose (its write lane checks it exactly)
-        if (j + 1 < n) {
+        if (j + 1 < n && !(final_seg && mcu_run + pm >= nmcu_seg)) {
             bad |= pbad;
         } else {  // the last piece takes the interval's remaining MCUs
             if (mcu_run > nmcu_seg) bad = true;
             pm = nmcu_seg >= mcu_run ? nmcu_seg - mcu_run : 0u;
+            done = true;
         }
         ent_run = (ent_run + 3u) & ~3u;  // pieces start on a 16-byte quad of entries
         // a piece stores at most 63 entries per block: if that cannot fit, the counts are corrupt

@@ -271,3 +271,69 @@ def test_dc_prediction_beyond_int16_and_resets(decoder, nblocks, dri):
     ost, ref = jdoracle.decode(data)
     assert ost == 0
     assert np.array_equal(decoder.decode(data), ref)
+
+
+def _cut_interval(jpeg, seg, nmcu):
+    """seg cut right after its first nmcu MCUs (tools/jd_trace.py decodes the symbols), the last
+    byte padded with 1-bits (and a stuffed zero after an FF); seg itself when it ends earlier."""
+    import jd_trace
+
+    t = jd_trace.parse(jpeg)
+    pattern, _ = jd_trace._layout(t)
+    val, total = int.from_bytes(seg, "big"), len(seg) * 8
+    p, k = 0, 0
+    for _ in range(nmcu):
+        for bi in range(len(pattern)):
+            while True:
+                r = jd_trace._symbol(t, pattern, val, total, p, bi, k)
+                if r is None or p + r[0] > total:
+                    return seg
+                p += r[0]
+                k, fin, _ = jd_trace._step(k, r[1])
+                if fin:
+                    break
+    nb = (p + 7) // 8
+    out = bytearray(seg[:nb])
+    if p % 8:
+        out[-1] |= (1 << (8 - p % 8)) - 1
+    if out and out[-1] == 0xFF:
+        out.append(0)
+    return bytes(out)
+
+
+@pytest.mark.parametrize("w,h,ss,q,rst", [(8, 8, "gray", 90, 0), (16, 16, "4:2:0", 50, 0), (24, 16, "4:4:4", 95, 0),
+                                          (64, 48, "4:2:2", 75, 0), (32, 32, "4:2:0", 90, 1), (40, 16, "4:4:4", 75, 2)])
+def test_random_entropy_data_vs_oracle(decoder, w, h, ss, q, rst):
+    """Random entropy-coded bytes behind valid headers: every symbol the tables allow, in any
+    order (runs past index 63, ZRL, codes longer than the LUT, magnitudes whose dequantised values
+    need the exact IDCT form, paired and unpaired lookups).  Status (decoded or not) and pixels
+    must match the oracle, image by image, in one batch.  rst > 0: restart intervals of rst MCUs,
+    each its own random bytes followed by the expected RSTn (trailing bytes before an RSTn are
+    corrupt, trailing bytes before EOI are not)."""
+    rng = np.random.default_rng(w * 10007 + h * 101 + q + rst)
+    hdr = jd_synth.encode(jd_synth.synth_pixels(w, h, 1, ss == "gray"), q, "4:4:4" if ss == "gray" else ss,
+                          restart_blocks=rst)
+    hd = jdamd.parse(hdr)
+    head = hdr[:hd.ecs_offset]
+    nseg = -(-hd.mcux * hd.mcuy // rst) if rst else 1
+    files = []
+    for i in range(96):
+        segs = []
+        for k in range(nseg):
+            n = (w * h // 64) * 2 * int(rng.integers(8, 40)) // nseg  # about 16-80 bytes per block
+            ecs = rng.integers(0, 256, max(n, 1), dtype=np.uint8)
+            ecs[ecs == 0xFF] = 0xFE  # no markers inside an interval
+            seg = ecs.tobytes()
+            if k + 1 < nseg and i % 4:  # 3 of 4: cut the interval where its MCUs end, 1-padded
+                seg = _cut_interval(hdr, seg, rst)
+            segs.append(seg + (bytes([0xFF, 0xD0 + k % 8]) if k + 1 < nseg else b""))
+        files.append(head + b"".join(segs) + b"\xff\xd9")
+    outs, status = decoder.decode_batch(files)
+    decoded = 0
+    for i, data in enumerate(files):
+        ost, ref = jdoracle.decode(data)
+        assert (ost == 0) == (status[i] == 0), i
+        if ost == 0:
+            assert np.array_equal(outs[i], ref), i
+            decoded += 1
+    assert decoded > 0
