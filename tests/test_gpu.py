@@ -302,7 +302,8 @@ def _cut_interval(jpeg, seg, nmcu):
 
 
 @pytest.mark.parametrize("w,h,ss,q,rst", [(8, 8, "gray", 90, 0), (16, 16, "4:2:0", 50, 0), (24, 16, "4:4:4", 95, 0),
-                                          (64, 48, "4:2:2", 75, 0), (32, 32, "4:2:0", 90, 1), (40, 16, "4:4:4", 75, 2)])
+                                          (64, 48, "4:2:2", 75, 0), (32, 32, "4:2:0", 90, 1), (40, 16, "4:4:4", 75, 2),
+                                          (256, 256, "gray", 90, 0), (128, 128, "4:2:0", 75, 0)])
 def test_random_entropy_data_vs_oracle(decoder, w, h, ss, q, rst):
     """Random entropy-coded bytes behind valid headers: every symbol the tables allow, in any
     order (runs past index 63, ZRL, codes longer than the LUT, magnitudes whose dequantised values
