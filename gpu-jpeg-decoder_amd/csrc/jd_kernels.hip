@@ -1320,18 +1320,27 @@ __device__ __forceinline__ TileLane tile_lane(const BatchDev& b, const ImgDesc& 
 
 // Wave per tile: the per-component sums of the differences after the tile's last interval start
 // (all of them when it has none) and whether it has one.
+constexpr uint32_t kDcTilesPerWave = 4;  // k_dc_sum: the tiles' BlockInfo loads are in flight together
 __global__ __launch_bounds__(256) void k_dc_sum(BatchDev b) {
     const ImgDesc& im = b.imgs[blockIdx.y];
-    const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    if (tile >= im.tiles_x * im.tiles_y) return;  // wave-uniform
-    const TileLane t = tile_lane(b, im, tile_geo(im, tile), lane);
-    const uint64_t mask = __ballot(t.start);
-    const uint32_t last = mask ? 63u - uint32_t(__clzll(mask)) : 0u;
-    const bool after = lane >= last;
-    const int s0 = wave_scan_dpp(after && t.comp == 0 ? t.d : 0);
-    const int s1 = wave_scan_dpp(after && t.comp == 1 ? t.d : 0);
-    const int s2 = wave_scan_dpp(after && t.comp == 2 ? t.d : 0);
-    if (lane == 63) b.tile_dc[im.tile_base + tile] = DcPred{s0, s1, s2, mask ? 1 : 0};
+    const uint32_t nt = im.tiles_x * im.tiles_y, lane = threadIdx.x & 63u;
+    const uint32_t tile0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kDcTilesPerWave;
+    if (tile0 >= nt) return;  // wave-uniform
+    TileLane t[kDcTilesPerWave];
+#pragma unroll
+    for (uint32_t k = 0; k < kDcTilesPerWave; k++)
+        t[k] = tile0 + k < nt ? tile_lane(b, im, tile_geo(im, tile0 + k), lane) : TileLane{0, 0u, false, false};
+#pragma unroll
+    for (uint32_t k = 0; k < kDcTilesPerWave; k++) {
+        if (tile0 + k >= nt) break;  // wave-uniform
+        const uint64_t mask = __ballot(t[k].start);
+        const uint32_t last = mask ? 63u - uint32_t(__clzll(mask)) : 0u;
+        const bool after = lane >= last;
+        const int s0 = wave_scan_dpp(after && t[k].comp == 0 ? t[k].d : 0);
+        const int s1 = wave_scan_dpp(after && t[k].comp == 1 ? t[k].d : 0);
+        const int s2 = wave_scan_dpp(after && t[k].comp == 2 ? t[k].d : 0);
+        if (lane == 63) b.tile_dc[im.tile_base + tile0 + k] = DcPred{s0, s1, s2, mask ? 1 : 0};
+    }
 }
 
 // Wave per image: segmented exclusive scan over its tiles in raster order, in place: tile_dc
@@ -2259,7 +2268,8 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             break;
         case 8:
             if (!b.max_tiles) break;
-            hipLaunchKernelGGL(k_dc_sum, dim3((b.max_tiles + 3) / 4, b.nimg), dim3(256), 0, s, b);
+            hipLaunchKernelGGL(k_dc_sum, dim3((b.max_tiles + 4 * kDcTilesPerWave - 1) / (4 * kDcTilesPerWave), b.nimg),
+                               dim3(256), 0, s, b);
             hipLaunchKernelGGL(k_dc_scan, dim3(b.nimg), dim3(64), 0, s, b);
             break;
         case 9:
