@@ -710,12 +710,13 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
     uint32_t ent = W.ent0, ent_blk = W.ent0, blk = 0;
     int dcd = 0;
     // Stores are deferred and issued every few loop iterations, so that one store instruction
-    // carries many lanes (a wave's store instructions, not its bytes, bound this pass): a lane
-    // completes at most one quad per 4 iterations (one entry per symbol) and one block per 2
-    // (a DC and at least one AC symbol), so one pending quad and one pending block suffice.
-    // Entries go to the lane's LDS ring of two quads (slot ent & 7; a symbol that emits nothing
-    // writes the next free slot without advancing, so its word is overwritten); a flush stores
-    // the completed quad fq straight from the ring.
+    // carries many lanes (a wave's store instructions, not its bytes, bound this pass).  An
+    // iteration emits at most two entries (a pair entry: two AC symbols), and a block takes at
+    // least two iterations (its DC symbol never pairs), so flushing one quad and one block every
+    // two iterations keeps at most 7 entries pending: one ring of two quads and one pending
+    // block suffice.  Entries go to the ring at slot ent & 7 (a symbol that emits nothing writes
+    // the next free slot without advancing, so its word is overwritten); a flush stores the
+    // completed quad fq straight from the ring.
     uint32_t fq = W.ent0 >> 2;  // quads stored so far (pieces start on a quad)
     uint32_t pbi0 = 0, pbi1 = 0, pblk = 0;
     bool pend_b = false;
