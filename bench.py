@@ -5,18 +5,29 @@
 
 One step = one pass of the decode path (host header parse + plan, RST scan, Huffman, IDCT/colour)
 over one batch of synthetic JPEGs whose bytes are already resident in HBM; RGB stays in HBM.
-N>1: one process per GPU (torch.distributed.run), images sharded by rank (weak scaling: each rank
-decodes its own batch of B images, BASELINE config 4 = 8 x config 2), no collective on the data
-path; one all-gather of per-rank counters at the end (RCCL over xGMI).
+N>1: one process per GPU (torch.distributed.run; `--gpus N` without a launcher starts one itself),
+images sharded by rank (weak scaling: each rank decodes its own batch of B images, BASELINE
+config 4 = 8 x config 2; mixed batches are balanced by estimated entropy-coded bytes), no
+collective on the data path; one all-gather of per-rank counters at the end (RCCL over xGMI).
 
-Rank 0 prints one JSON line (contract in the task statement); "roofline" reports the dominant
-kernel's algorithmic bytes / its hipEvent-measured average launch time against the 8 TB/s HBM
-peak, and "cpu_baseline" the oracle (CPU restatement of the reference decoder) on a bounded sample.
+Rank 0 prints one JSON line (contract in the task statement) with, besides the contract keys:
+  roofline      the dominant kernel's algorithmic bytes / its hipEvent-measured average launch time
+                against the 8 TB/s HBM peak, the same against an in-run copy-kernel peak, its HBM
+                traffic and VALU issue fraction from the committed PMC profiles (profiles/)
+  e2e_h2d       the same batch with the JPEG bytes handed over in host memory (PCIe-inclusive)
+  cpu_baseline  the reference's own CPU decoder (oracle/_ref/ref_bench, built from its sources) on
+                the BASELINE config-1 image, and the oracle (the CPU restatement, which also decodes
+                4:2:0 / RST) on a bounded sample of this workload, 1 core and all cores, with the
+                port/reference calibration ratio (reference time: cpp-decoder/benchmark/benchmark.cc:29-35)
 """
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -31,20 +42,65 @@ CONFIGS = {
     "c5": (1920, 1080, "mixed", 0, 1024, "1024 x 1080p mixed 4:4:4/4:2:2/4:2:0, q in {50,75,90,95}, no RST "
                                          "(BASELINE config 5)"),
 }
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SIMDS = 1024               # 256 CUs x 4 SIMD-32
+VALU_CYCLES_PER_INST = 2   # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+BOX_CPU_SHARE = 16         # CPUs a one-GPU share of the box gets (task environment)
 
 
-def measured_traffic(config: str, kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC profile of this config
-    (profiles/<round>_traffic.json, written by tools/profile_summary.py), or None."""
-    import glob
+# ---------------------------------------------------------------------------------------------
+# launch, ranks, shards
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
-        with open(f) as fh:
-            t = json.load(fh)
-        if t.get("config") == config and kernel in t.get("kernels", {}):
-            return t["kernels"][kernel]["hbm_bytes"], os.path.relpath(f, ROOT)
+
+def maybe_launch(args):
+    """`--gpus N` without a launcher: start torch.distributed.run with N ranks as a child process
+    (nothing has touched the GPU yet) and return its exit code; None when this process is a rank."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        if args.gpus <= 1:
+            return None
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+        cmd += sys.argv[1:]
+        return subprocess.call(cmd)
+    if int(world_env) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks")
     return None
+
+
+def dist_setup():
+    """Rank / device selection and process-group init (one process per GPU).  JD_DIST_BACKEND=gloo
+    with more ranks than GPUs rehearses the multi-rank path on a one-GPU box (ranks then share
+    devices round-robin).  Returns a dict; 'world_seen' is the process group's own size."""
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    backend = os.environ.get("JD_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    device_index = local_rank if (backend == "nccl" or ndev == 0) else local_rank % ndev
+    world_seen = 1
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if ndev:
+            torch.cuda.set_device(device_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
+        else:
+            dist.init_process_group(backend)
+        world_seen = dist.get_world_size()
+        if world_seen != world:
+            raise SystemExit(f"process group has {world_seen} ranks, WORLD_SIZE={world}")
+    return {"rank": rank, "world": world, "local_rank": local_rank, "local_world": local_world,
+            "backend": backend if world > 1 else "none", "device_index": device_index, "world_seen": world_seen}
 
 
 def rank_seed(rank: int, batch: int) -> int:
@@ -52,42 +108,251 @@ def rank_seed(rank: int, batch: int) -> int:
     return rank * batch
 
 
-def gather_counters(local, world: int):
-    """One all-gather of the per-rank [elapsed, pixels, images, ecs bytes, file bytes] counters
-    (RCCL over xGMI on the GPU box, gloo in tests/test_dist.py).  Returns (max elapsed, sums)."""
+def shard_seeds(config: str, batch: int, rank: int, world: int):
+    """The global image seeds rank `rank` decodes.  Uniform configs: a contiguous range of `batch`
+    seeds per rank.  Mixed batches (C5) vary 5x in size per image, so the world * batch images are
+    assigned greedily, largest estimated entropy-coded size first, to the least-loaded rank
+    (SURVEY.md §8e); sizes come from jd_synth's per-(subsampling, quality) model, so every rank
+    computes the same assignment without encoding the others' images."""
+    import jd_synth
+
+    W, H, ss, _, _, _ = CONFIGS[config]
+    if ss != "mixed" or world == 1:
+        s0 = rank_seed(rank, batch)
+        return list(range(s0, s0 + batch))
+    est = [(jd_synth.estimated_bytes(W, H, *jd_synth.mixed_params(g)), g) for g in range(world * batch)]
+    est.sort(key=lambda t: (-t[0], t[1]))
+    load = [0.0] * world
+    count = [0] * world
+    mine = []
+    for b, g in est:
+        r = min((k for k in range(world) if count[k] < batch), key=lambda k: (load[k], k))
+        load[r] += b
+        count[r] += 1
+        if r == rank:
+            mine.append(g)
+    return sorted(mine)
+
+
+def numa_cpus(device_index: int):
+    """Host CPUs of the GPU's NUMA node that this process may run on (None if unknown)."""
+    try:
+        import torch
+
+        pr = torch.cuda.get_device_properties(device_index)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        if node < 0:
+            return None
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        mine = cpus & os.sched_getaffinity(0)
+        return sorted(mine) or None
+    except Exception:
+        return None
+
+
+def host_threads(d):
+    """Parse/plan workers for this rank: a slice of the CPUs of its GPU's NUMA node (or of all it
+    may use), one slice per local rank on that node, at most the box's one-GPU share; with several
+    ranks the process is pinned to its slice so the ranks' workers do not compete."""
+    allowed = sorted(os.sched_getaffinity(0))
+    lw = max(1, d["local_world"])
+    node = numa_cpus(d["device_index"]) if d["world"] > 1 else None
+    if node:  # the local ranks whose GPUs sit on this node share its CPUs (GPUs spread evenly)
+        share = max(1, min(lw, round(lw * len(node) / len(allowed))))
+        per = max(1, len(node) // share)
+        k = d["local_rank"] % share
+        mine = node[k * per:(k + 1) * per]
+    else:
+        per = max(1, len(allowed) // lw)
+        k = d["local_rank"] % lw
+        mine = allowed[k * per:(k + 1) * per] or allowed
+    threads = max(1, min(BOX_CPU_SHARE, len(mine)))
+    if d["world"] > 1:
+        try:
+            os.sched_setaffinity(0, mine)
+        except OSError:
+            pass
+    return threads, {"cpus_allowed": len(allowed), "numa_node_cpus": len(node) if node else None,
+                     "rank_cpus": len(mine), "parse_threads": threads}
+
+
+def gather_matrix(local, world: int):
+    """One all-gather of the per-rank counter vector (RCCL over xGMI on the GPU box, gloo in
+    tests/test_dist.py); returns a [world, k] numpy array."""
     import torch
     import torch.distributed as dist
 
     if world > 1:
         allc = [torch.zeros_like(local) for _ in range(world)]
         dist.all_gather(allc, local)
-        allc = torch.stack(allc).cpu().numpy()
-    else:
-        allc = local.cpu().numpy()[None]
+        return torch.stack(allc).cpu().numpy()
+    return local.cpu().numpy()[None]
+
+
+def gather_counters(local, world: int):
+    """(max over ranks of counter 0 = elapsed, sums of the other counters)."""
+    allc = gather_matrix(local, world)
     return float(allc[:, 0].max()), tuple(float(allc[:, k].sum()) for k in range(1, allc.shape[1]))
 
 
-def cpu_baseline(hosts, hdrs, n_req: int, target_s: float = 12.0):
-    """The oracle (CPU restatement of the reference decoder, full decode to RGB) on one core over a
-    bounded sample of the same workload: n_req images, or (n_req < 0) as many as take ~target_s."""
+# ---------------------------------------------------------------------------------------------
+# measurement helpers
+# ---------------------------------------------------------------------------------------------
+def newest_profile(pattern: str, config: str, kernel: str):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), reverse=True):
+        with open(f) as fh:
+            t = json.load(fh)
+        if t.get("config") == config and kernel in t.get("kernels", {}):
+            return t["kernels"][kernel], os.path.relpath(f, ROOT)
+    return None, None
+
+
+def measured_traffic(config: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC traffic profile of this
+    config (profiles/<round>_traffic.json, tools/profile_summary.py), or None."""
+    k, src = newest_profile("*_traffic.json", config, kernel)
+    return (k["hbm_bytes"], src) if k else None
+
+
+def valu_issue(config: str, kernel: str, avg_ms: float):
+    """VALU issue fraction of `kernel` from the newest committed SQ profile of this config
+    (profiles/<round>_sq_<config>.json): VALU wave-instructions per launch x 2 cycles over the
+    SIMD-cycles of the launch at the clock the profiled run held (GRBM_GUI_ACTIVE / 8 XCDs / time)."""
+    k, src = newest_profile("*_sq_*.json", config, kernel)
+    if not k or avg_ms <= 0:
+        return None
+    clk = k.get("clock_ghz") or 2.4
+    frac = k["valu_insts"] * VALU_CYCLES_PER_INST / (SIMDS * clk * 1e9 * avg_ms * 1e-3)
+    return {"valu_insts_per_launch": k["valu_insts"], "clock_ghz": clk, "issue_frac": frac, "source": src}
+
+
+def copy_peak_gbs(dev, gib: float = 4.0, reps: int = 5):
+    """In-run HBM peak: a device-to-device copy of `gib` GiB (read + write bytes / time)."""
+    import torch
+
+    n = int(gib * (1 << 30))
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2.0 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def ref_bench(paths, procs: int, reps: int):
+    """The reference decoder (oracle/_ref/ref_bench: cpp-decoder's JPEGParser compiled from its own
+    sources; extract()+decode() timed like cpp-decoder/benchmark/benchmark.cc:29-35) in `procs`
+    parallel processes.  Returns (aggregate images/s, per-process seconds)."""
     import jdoracle
 
+    if not os.path.exists(jdoracle.REF_BENCH):
+        return None
+    ps = [subprocess.Popen([jdoracle.REF_BENCH, str(reps)] + list(paths), stdout=subprocess.PIPE, text=True)
+          for _ in range(procs)]
+    rate, secs = 0.0, []
+    for p in ps:
+        out, _ = p.communicate(timeout=300)
+        if p.returncode != 0:
+            return None
+        r = json.loads(out.strip().splitlines()[-1])
+        rate += r["images"] / r["seconds"]
+        secs.append(r["seconds"])
+    return rate, secs
+
+
+def cpu_baseline(hosts, hdrs, target_s: float = 5.0):
+    """CPU decoders on this host, 1 core and all cores (the box's one-GPU CPU share):
+      reference : the reference's JPEGParser (oracle/_ref/ref_bench) on the BASELINE config-1 image
+                  (512x512 4:4:4 q90, no RST) — the only shape it decodes correctly
+      port      : the oracle (CPU restatement; bit-serial Huffman, reference IDCT + colour) on the
+                  first images of this workload, and on the config-1 image for the calibration
+    value = the port on this workload at all cores (kind "port"); `reference_equivalent` scales it
+    by the calibration ratio."""
+    import numpy as np
+
+    import jd_synth
+    import jdoracle
+
+    cores = max(1, min(BOX_CPU_SHARE, len(os.sched_getaffinity(0))))
+    res = {"unit": "MPixels/s", "kind": "port", "cores": cores, "nproc": os.cpu_count(),
+           "cpus_allowed": len(os.sched_getaffinity(0)), "cpu_model": cpu_model()}
+
+    def port(sample, threads):
+        secs, st, _ = jdoracle.decode_many(sample, threads=threads, want_rgb=True)
+        if any(st):
+            raise SystemExit(f"oracle failed on the CPU sample: {sorted(set(st))}")
+        return secs
+
     n = len(hosts)
-    if n_req < 0:
-        probe = min(n, 4)
-        secs, _, _ = jdoracle.decode_many(hosts[:probe], threads=1, want_rgb=True)
-        n_req = int(max(probe, min(n, target_s / max(secs / probe, 1e-6))))
-    n_req = min(n_req, n)
-    secs, st, _ = jdoracle.decode_many(hosts[:n_req], threads=1, want_rgb=True)
-    if any(st):
-        raise SystemExit(f"oracle failed on the CPU sample: {sorted(set(st))}")
-    cpx = float(sum(h.width * h.height for h in hdrs[:n_req]))
-    return {"value": cpx / secs / 1e6, "unit": "MPixels/s", "cores": 1, "kind": "port",
-            "sample": f"first {n_req} of the workload's images decoded to RGB by oracle/liboracle.so "
-                      f"(bit-serial Huffman, reference IDCT + colour), 1 thread, {secs:.2f} s",
-            "images_per_s": n_req / secs}
+    probe = min(n, 2)
+    per = port(hosts[:probe], 1) / probe
+    n1 = int(max(1, min(n, target_s / max(per, 1e-6))))
+    s1 = port(hosts[:n1], 1)
+    px1 = float(sum(h.width * h.height for h in hdrs[:n1]))
+    nall = int(max(cores, min(n, cores * target_s / max(per, 1e-6))))
+    sample = [hosts[i % n] for i in range(nall)]
+    sall = port(sample, cores)
+    pxall = float(sum(hdrs[i % n].width * hdrs[i % n].height for i in range(nall)))
+    res["port_1core"] = {"MPix_s": px1 / s1 / 1e6, "images": n1, "seconds": s1}
+    res["port_all_cores"] = {"MPix_s": pxall / sall / 1e6, "images": nall, "seconds": sall, "threads": cores}
+    res["value"] = res["port_all_cores"]["MPix_s"]
+
+    c1 = jd_synth.encode(jd_synth.synth_pixels(512, 512, 0), 90, "4:4:4", 0, 0)
+    c1a = np.frombuffer(c1, np.uint8).copy()
+    pc1 = port([c1a] * 20, 1) / 20
+    res["port_c1_1core_MPix_s"] = 512 * 512 / pc1 / 1e6
+    sample_desc = (f"port: first {n1} workload images on 1 thread ({s1:.1f} s), {nall} on {cores} threads "
+                   f"({sall:.1f} s)")
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "c1_512x512_444_q90.jpg")
+        with open(path, "wb") as f:
+            f.write(c1)
+        one = ref_bench([path], 1, 4)
+        if one:
+            per_ref = one[1][0] / 4
+            reps = int(max(4, target_s / max(per_ref, 1e-6)))
+            r1 = ref_bench([path], 1, reps)
+            rall = ref_bench([path], cores, max(2, reps // 2))
+            res["reference_c1"] = {"MPix_s_1core": r1[0] * 512 * 512 / 1e6,
+                                   "MPix_s_all_cores": rall[0] * 512 * 512 / 1e6, "processes": cores,
+                                   "binary": "oracle/_ref/ref_bench (cpp-decoder sources, g++ -O2)",
+                                   "decodes_1core": reps}
+            cal = res["port_c1_1core_MPix_s"] / res["reference_c1"]["MPix_s_1core"]
+            res["calibration_port_over_reference"] = cal
+            res["reference_equivalent"] = {"MPix_s_1core": px1 / s1 / 1e6 / cal,
+                                           "MPix_s_all_cores": res["value"] / cal}
+            sample_desc += f"; reference: config-1 image x{reps} on 1 process, x{max(2, reps // 2)} on {cores}"
+        else:
+            res["reference_c1"] = None
+            sample_desc += "; reference binary oracle/_ref/ref_bench not built on this box"
+    res["sample"] = sample_desc
+    return res
 
 
+# ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,40 +361,27 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override images per rank")
     ap.add_argument("--quality", type=int, default=90)
-    ap.add_argument("--cpu-sample", type=int, default=-1, help="images for the CPU baseline (-1 auto, 0 off)")
-    ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact vs the oracle")
+    ap.add_argument("--cpu-sample", type=int, default=1, help="1: time the CPU baselines, 0: skip")
+    ap.add_argument("--verify", type=int, default=1, help="check images {0, n/2, n-1} bit-exact vs the oracle")
+    ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the H2D-inclusive run (0: skip)")
+    ap.add_argument("--copy-peak", type=int, default=1, help="measure an in-run HBM copy peak")
     ap.add_argument("--path", default="auto", choices=["auto", "sync", "lanes", "full"],
                     help="entropy-decode path (auto: lanes for images with restart intervals)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one blocking jd_decode_batch per step instead of jd_decode_batch_async (which "
                          "parses and plans step k+1 on the host while the GPU decodes step k)")
     args = ap.parse_args()
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    rc = maybe_launch(args)
+    if rc is not None:
+        sys.exit(rc)
 
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    # one process per GPU; JD_DIST_BACKEND=gloo with more ranks than GPUs rehearses the
-    # multi-rank path on a one-GPU box (ranks then share devices round-robin)
-    backend = os.environ.get("JD_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    if backend == "nccl" or ndev == 0:
-        device_index = local_rank
-    else:
-        device_index = local_rank % ndev
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(device_index)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device("cuda", device_index)
-    local_rank = device_index
+    d = dist_setup()
+    rank, world = d["rank"], d["world"]
+    dev = torch.device("cuda", d["device_index"])
 
     import jd_synth
     import jdamd
@@ -137,13 +389,15 @@ def main():
     W, H, ss, rrows, batch, desc = CONFIGS[args.config]
     if args.batch:
         batch = args.batch
-    seed0 = rank_seed(rank, batch)  # disjoint images per rank: shard by image
+    seeds = shard_seeds(args.config, batch, rank, world)  # disjoint images per rank: shard by image
     t_gen = time.time()
-    datas = jd_synth.make_batch(batch, W, H, args.quality, "4:2:0" if ss == "mixed" else ss, rrows, 0, seed0,
-                                mixed=(ss == "mixed"))
+    jobs = jd_synth.make_jobs(seeds, W, H, args.quality, "4:2:0" if ss == "mixed" else ss, rrows, 0,
+                              mixed=(ss == "mixed"))
+    datas = jd_synth.make_images(jobs)
     t_gen = time.time() - t_gen
-    hosts = [np.frombuffer(d, np.uint8).copy() for d in datas]
-    hdrs = [jdamd.parse(d) for d in datas]
+    n = len(datas)
+    hosts = [np.frombuffer(x, np.uint8).copy() for x in datas]
+    hdrs = [jdamd.parse(x) for x in datas]
     in_offs, tot = [], 0
     for h in hosts:
         in_offs.append(tot)
@@ -161,12 +415,13 @@ def main():
     jpeg_dev.copy_(torch.from_numpy(flat))
     torch.cuda.synchronize(dev)
 
-    dec = jdamd.Decoder(local_rank, timing=True, path=args.path)
+    threads, thread_info = host_threads(d)
+    dec = jdamd.Decoder(d["device_index"], timing=True, path=args.path, parse_threads=threads)
     prepared = dec.make_batch(hosts, [jpeg_dev.data_ptr() + o for o in in_offs],
                               [rgb_dev.data_ptr() + o for o in out_offs])
     pixels = float(sum(h.width * h.height for h in hdrs))
-    ecs = float(sum(len(d) - h.ecs_offset for d, h in zip(datas, hdrs)))
-    jpeg_bytes = float(sum(len(d) for d in datas))
+    ecs = float(sum(len(x) - h.ecs_offset for x, h in zip(datas, hdrs)))
+    jpeg_bytes = float(sum(len(x) for x in datas))
 
     pipelined = not args.no_pipeline
     for _ in range(args.warmup):
@@ -176,18 +431,18 @@ def main():
     if any(status):
         raise SystemExit(f"decode failed: statuses {sorted(set(status))}")
 
-    # correctness spot check against the oracle (outside the timed region)
-    verified = 0
+    # correctness spot check against the oracle (outside the timed region): head, middle, tail
+    verified = []
     if args.verify:
         import jdoracle
 
-        for i in range(min(args.verify, batch)):
+        for i in sorted({0, n // 2, n - 1}):
             h = hdrs[i]
             got = rgb_dev[out_offs[i]:out_offs[i] + h.width * h.height * 3].cpu().numpy().reshape(h.height, h.width, 3)
             st, ref = jdoracle.decode(datas[i])
             if st != 0 or not np.array_equal(got, ref):
                 raise SystemExit(f"bit-exactness check failed on image {i}")
-            verified += 1
+            verified.append(i)
 
     dec.reset_stats()
     if world > 1:
@@ -205,23 +460,42 @@ def main():
         raise SystemExit("decode failed inside the timed region")
     st = dec.stats()
 
+    # PCIe-inclusive rate (not `value`): the JPEG bytes handed over in host memory, RGB to HBM
+    e2e = None
+    if args.e2e_steps:
+        host_batch = dec.make_batch(hosts, [None] * n, [rgb_dev.data_ptr() + o for o in out_offs])
+        dec.decode_prepared(host_batch)
+        torch.cuda.synchronize(dev)
+        te = time.perf_counter()
+        for _ in range(args.e2e_steps):
+            dec.decode_prepared(host_batch)
+        torch.cuda.synchronize(dev)
+        te = time.perf_counter() - te
+        if any(r.status for r in host_batch[1]):
+            raise SystemExit("decode failed in the H2D-inclusive run")
+        e2e = {"MPix_s": pixels * args.e2e_steps / te / 1e6, "ms_per_step": te / args.e2e_steps * 1e3,
+               "steps": args.e2e_steps, "note": "per rank; JPEG bytes from pageable host memory through the "
+               "library's pinned staging + H2D copy, RGB left in HBM"}
+
     # one all-gather of per-rank counters (RCCL over xGMI when N > 1)
-    local = torch.tensor([elapsed, pixels * args.steps, batch * args.steps, ecs * args.steps,
-                          jpeg_bytes * args.steps], dtype=torch.float64,
-                         device=dev if backend == "nccl" else "cpu")
-    t_max, (tot_px, tot_img, tot_ecs, tot_bytes) = gather_counters(local, world)
+    local = torch.tensor([elapsed, pixels * args.steps, n * args.steps, ecs * args.steps,
+                          jpeg_bytes * args.steps, ecs, n], dtype=torch.float64,
+                         device=dev if d["backend"] == "nccl" else "cpu")
+    allc = gather_matrix(local, world)
+    t_max = float(allc[:, 0].max())
+    tot_px, tot_img, tot_ecs, tot_bytes = (float(allc[:, k].sum()) for k in range(1, 5))
 
     if rank == 0:
         kern = st["kernels"]
         dom = max(kern, key=lambda k: kern[k]["total_ms"])
-        traffic = measured_traffic(args.config, dom)
         kd = kern[dom]
         avg_ms = kd["total_ms"] / max(1, kd["launches"])
         per_launch_bytes = kd["bytes"] / max(1, kd["launches"])
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        cpu = None
-        if args.cpu_sample and world == 1:  # the CPU baseline is an N=1 figure
-            cpu = cpu_baseline(hosts, hdrs, args.cpu_sample)
+        traffic = measured_traffic(args.config, dom)
+        copy_gbs = copy_peak_gbs(dev) if (args.copy_peak and world == 1) else None
+        cpu = cpu_baseline(hosts, hdrs) if (args.cpu_sample and world == 1) else None
+        px_rank = float(sum(h.width * h.height for h in hdrs))
         res = {
             "metric": "MPixels/s decoded (and images/s) at 1/2/4/8 MI355X; % HBM roofline",
             "value": tot_px / t_max / 1e6,
@@ -234,12 +508,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic (seeded sinusoid + noise, baseline encode q{args.quality} by "
+            "data": f"synthetic (seeded sinusoid + noise, baseline encode "
+                    f"{'q in {50,75,90,95}' if ss == 'mixed' else f'q{args.quality}'} by "
                     f"{'tools/jdenc.c' if jd_synth.default_encoder() == 'jdenc' else 'Pillow'}, std Huffman tables)",
-            "config": {"workload": desc, "config": args.config, "images_per_rank": batch,
-                       "global_batch": batch * world, "width": W, "height": H, "subsampling": ss,
+            "config": {"workload": desc, "config": args.config, "images_per_rank": n,
+                       "global_batch": int(allc[:, 6].sum()), "width": W, "height": H, "subsampling": ss,
                        "restart_rows": rrows, "parallelism": f"dp{world} (image sharding)",
-                       "entropy_path": args.path, "host_pipelined": pipelined},
+                       "entropy_path": args.path, "host_pipelined": pipelined,
+                       "bpp_file": 8 * jpeg_bytes / px_rank, "bpp_ecs": 8 * ecs / px_rank},
+            "world_size_seen": d["world_seen"],
+            "dist_backend": d["backend"],
+            "shards": {"images": [int(x) for x in allc[:, 6]], "ecs_MB": [round(x / 1e6, 3) for x in allc[:, 5]],
+                       "ecs_max_over_mean": float(allc[:, 5].max() / allc[:, 5].mean()),
+                       "balance": "greedy by estimated ECS bytes" if ss == "mixed" and world > 1 else "contiguous"},
+            "host": thread_info,
             "images_per_s": tot_img / t_max,
             "jpeg_MB_per_s": tot_bytes / t_max / 1e6,
             "ecs_MB_per_s": tot_ecs / t_max / 1e6,
@@ -247,9 +529,13 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,
+                         "measured_copy_peak": copy_gbs,
+                         "frac_of_measured_peak": achieved / copy_gbs if copy_gbs else None,
+                         "valu": valu_issue(args.config, dom, avg_ms),
                          "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
             "kernels_ms_per_step": {k: v["total_ms"] / max(1, v["launches"]) for k, v in kern.items()},
             "path_roofline_frac": ((ecs + 3 * pixels) / (t_max / args.steps) / 1e9) / HBM_PEAK_GBS,
+            "e2e_h2d": e2e,
             "cpu_baseline": cpu,
             "verified_bit_exact": verified,
             "gen_s": t_gen,

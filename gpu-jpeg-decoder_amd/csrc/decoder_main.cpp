@@ -1,6 +1,7 @@
-// decoder_main.cpp — CLI `decoder [--fancy] <jpeg> [outdir]`, mirroring the reference CLIs
+// decoder_main.cpp — CLI `decoder [--fancy] [--ppm] <jpeg> [outdir]`, mirroring the reference CLIs
 // (cpp-decoder/main.cpp:5-16 and cuda-decoder/main.cu:7-40): extract, decode, write `.array`.
-// --fancy selects triangular chroma upsampling (JD_FLAG_FANCY_UPSAMPLING).
+// --fancy selects triangular chroma upsampling (JD_FLAG_FANCY_UPSAMPLING); --ppm writes the binary
+// PPM of the reference's libjpeg comparison flow (testing/jpeglib_output_ppm/) instead.
 #include <cstdio>
 #include <exception>
 #include <string>
@@ -8,8 +9,15 @@
 #include "jpeg_parser.hpp"
 
 int main(int argc, char* argv[]) {
-    if (argc >= 2 && std::string(argv[1]) == "--fancy") {
-        jdamd::default_context_flags() |= JD_FLAG_FANCY_UPSAMPLING;
+    bool ppm = false;
+    while (argc >= 2 && argv[1][0] == '-' && argv[1][1] == '-') {
+        const std::string opt = argv[1];
+        if (opt == "--fancy") jdamd::default_context_flags() |= JD_FLAG_FANCY_UPSAMPLING;
+        else if (opt == "--ppm") ppm = true;
+        else {
+            std::fprintf(stderr, "decoder: unknown option %s\n", opt.c_str());
+            return 1;
+        }
         argv++;
         argc--;
     }
@@ -21,7 +29,8 @@ int main(int argc, char* argv[]) {
         jdamd::JPEGParser parser(argv[1]);
         parser.extract();
         parser.decode();
-        if (argc >= 3) parser.write(argv[2]);
+        if (ppm) parser.write_ppm(argc >= 3 ? argv[2] : ".");
+        else if (argc >= 3) parser.write(argv[2]);
         else parser.write();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "decoder: %s\n", e.what());

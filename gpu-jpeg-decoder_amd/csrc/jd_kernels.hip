@@ -1,14 +1,23 @@
-// jd_kernels.hip — gfx950 (CDNA4, wave64) kernels of the batched JPEG decode path.
+// jd_kernels.hip — gfx950 (CDNA4, wave64) kernels of the batched JPEG decode path, in launch order
+// (launch_kernel's slots; DESIGN.md §4.2 gives each one's work unit, bytes and bound):
 //
-//   k_scan        16 KiB of ECS per workgroup: stuffed-zero counts, RSTn / terminator positions
-//   k_index       one wave per image: chunk offsets in the un-stuffed stream, restart-interval
-//                 (segment) boundaries, RSTn order / count checks
-//   k_compact     16 KiB per workgroup: drops the stuffed 00 after every FF (byte compaction)
-//   k_subplan / k_decode<0,1,2> / k_chain
-//                 self-synchronising Huffman + DPCM/RLE decode, one lane per 512-bit
-//                 subsequence of a restart interval -> sparse coefficients (Stage 3 below)
-//   k_idct_color  one workgroup per 128-px tile: dequant + integer IDCT (LDS tile) + replicate
-//                 chroma upsample + YCbCr->RGB -> uint8 HWC
+//   k_scan         16 KiB of ECS per 256-thread workgroup: stuffed-zero counts, RSTn / terminator
+//                  positions (SWAR byte masks)
+//   k_index        one wave per image: chunk offsets in the un-stuffed stream, restart-interval
+//                  (segment) boundaries, RSTn order / count checks
+//   k_compact      16 KiB per workgroup: drops the stuffed 00 after every FF (byte compaction)
+//   k_subplan      one wave per image: pieces (<= piece_bits un-stuffed bits) of every interval
+//   k_piece<Scan>  one lane per piece: speculative, self-synchronising Huffman walk (MCU and
+//                  AC-entry counts, checkpoints); k_rescan re-walks the pieces whose speculative
+//                  start was wrong; k_chain / k_chain_fix verify the chain of pieces and prefix-sum
+//                  each piece's first MCU and entry slot
+//   k_piece<Write> one lane per piece: BlockInfo (DC difference, entry range) + sparse AC entries
+//   k_dc_sum / k_dc_scan   DC predictors at every IDCT tile's first block
+//   k_idct_color   one wave per tile (a run of <= 64 blocks of one MCU row): DC prediction,
+//                  dequantisation, integer IDCT in registers, replicate chroma upsampling and
+//                  YCbCr->RGB -> uint8 HWC; k_idct_color_exact takes the (never seen) tiles whose
+//                  coefficients are beyond the fast IDCT form's range
+//   k_colour_fancy (JD_FLAG_FANCY_UPSAMPLING only) libjpeg's triangular upsampling + colour
 //
 // Arithmetic follows the reference CPU decoder bit for bit (cpp-decoder/src/idct.cpp,
 // utils/color.cpp); the restatement used as checker lives in oracle/ (tests only).

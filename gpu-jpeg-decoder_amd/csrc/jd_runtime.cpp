@@ -158,6 +158,8 @@ struct jd_ctx {
 
     Pending pend[2];
     int slot = 0;  // the slot the next launch uses
+    hipStream_t last_stream = nullptr;  // stream of the pending launches (scratch pools are ordered on it)
+    uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     jd_stats stats{};
 
     std::vector<ParsedJpeg> parsed;
@@ -264,17 +266,19 @@ struct Plan {
     double pixels = 0, ecs_bytes = 0;
 };
 
-// Largest item prefix [lo, hi) whose sparse-coefficient slots stay within kMaxBatchEntries
-// (entry indices are image-relative; this only bounds the pool, 4 B per slot).
+// Largest item prefix [lo, hi) whose sparse-coefficient slots stay within the context's
+// max_batch_entries (default kMaxBatchEntries; entry indices are image-relative, this only bounds
+// the pool, 4 B per slot).  JD_MAX_BATCH_ENTRIES overrides it (tests force multi-way splits).
 constexpr uint64_t kMaxBatchEntries = 8ull << 30;
 int batch_split(jd_ctx* ctx, int lo, int n) {
+    const uint64_t limit = ctx->max_batch_entries;
     uint64_t cap = 0;
     int hi = lo;
     for (; hi < n; hi++) {
         if (ctx->pst[hi] != JD_OK) continue;
         const jd_header& h = ctx->parsed[hi].hdr;
         const uint64_t blocks = uint64_t(h.mcux) * h.mcuy * h.blocks_per_mcu;
-        if (hi > lo && cap + blocks * 64 > kMaxBatchEntries) break;
+        if (hi > lo && cap + blocks * 64 > limit) break;
         cap += blocks * 64;
     }
     return hi;
@@ -921,6 +925,11 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     ctx->parse_threads = pt;
     ctx->pool.reset(new Pool(pt - 1));
     ctx->host_timing = std::getenv("JD_HOST_TIMING") != nullptr;
+    ctx->max_batch_entries = kMaxBatchEntries;
+    if (const char* e = std::getenv("JD_MAX_BATCH_ENTRIES")) {
+        const unsigned long long v = std::strtoull(e, nullptr, 0);
+        if (v > 0) ctx->max_batch_entries = v;
+    }
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return JD_ERR_HIP;
@@ -942,7 +951,8 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_brk, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output, &ctx->comp})
+    for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_brk, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output,
+                       &ctx->comp, &ctx->planes})
         if (b->p) (void)hipFree(b->p);
     if (ctx->input_host.p) (void)hipHostFree(ctx->input_host.p);
     for (Pending& pd : ctx->pend) {
@@ -977,7 +987,15 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
         if (!items[i].jpeg || items[i].len > 0xFFFFFFF0ull) return JD_ERR_INVALID_ARG;
     if (hipSetDevice(ctx->device) != hipSuccess) return JD_ERR_HIP;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
-    // the host input staging buffer is reused per launch: with host inputs, collect first
+    // The scratch pools (plan, pieces, blocks, entries ...) are ordered by the stream alone: a
+    // launch on another stream than the pending batches' first collects them.
+    if (s != ctx->last_stream) {
+        const jd_status st = finish_all(ctx);
+        if (st != JD_OK) return st;
+        ctx->last_stream = s;
+    }
+    // The host input staging buffer and the output pool are reused per launch: with host inputs
+    // or host outputs, collect first, and collect every sub-batch before launching the next.
     bool host_inputs = false;
     for (int i = 0; i < n && !host_inputs; i++) host_inputs = !items[i].jpeg_dev;
     if (host_inputs || !rgb_on_device) {
@@ -996,8 +1014,10 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
         if (st != JD_OK) return st;
         if (async) {  // collect the previous launch (its slot is the current one now)
             st = finish_batch(ctx, ctx->pend[ctx->slot]);
-            if (st != JD_OK) return st;
+        } else {  // collect this sub-batch before the next one reuses the staging and output pools
+            st = finish_batch(ctx, ctx->pend[ctx->slot ^ 1]);
         }
+        if (st != JD_OK) return st;
         lo = hi;
     }
     return async ? JD_OK : finish_all(ctx);
@@ -1071,6 +1091,16 @@ jd_status jd_write_array(const char* path, const uint8_t* rgb, int width, int he
     }
     fclose(f);
     return JD_OK;
+}
+
+jd_status jd_write_ppm(const char* path, const uint8_t* rgb, int width, int height) {
+    if (!path || !rgb || width <= 0 || height <= 0) return JD_ERR_INVALID_ARG;
+    FILE* f = fopen(path, "wb");
+    if (!f) return JD_ERR_IO;
+    fprintf(f, "P6\n%d %d\n255\n", width, height);
+    const size_t n = size_t(width) * height * 3;
+    const bool ok = fwrite(rgb, 1, n, f) == n;
+    return (fclose(f) == 0 && ok) ? JD_OK : JD_ERR_IO;
 }
 
 jd_status jd_device_alloc(jd_ctx* ctx, size_t bytes, void** dptr) {

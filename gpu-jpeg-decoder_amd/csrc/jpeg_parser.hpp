@@ -64,11 +64,16 @@ class JPEGParser {
     // parser.cpp:197-209: "<outdir>/<name>.array" (the reference hard-codes
     // ../testing/cpp_output_arrays; testing/compare.py:41-43 expects "<impl>_output_arrays").
     void write(const std::string& outdir = "../testing/gpu_output_arrays") const {
-        std::string name = filename_;
-        const size_t dot = name.find_last_of('.');
-        if (dot != std::string::npos) name = name.substr(0, dot);
-        const std::string out = outdir + "/" + name + ".array";
+        const std::string out = outdir + "/" + stem() + ".array";
         jd_status st = jd_write_array(out.c_str(), rgb_.data(), hdr_.width, hdr_.height);
+        if (st != JD_OK) throw std::runtime_error(out + ": " + jd_status_str(st));
+    }
+
+    // The libjpeg comparison format of the reference's testing flow (testing/jpeglib_output_ppm/,
+    // jpeglib-implementation/process_ppm.py): "<outdir>/<name>.ppm", binary P6.
+    void write_ppm(const std::string& outdir) const {
+        const std::string out = outdir + "/" + stem() + ".ppm";
+        jd_status st = jd_write_ppm(out.c_str(), rgb_.data(), hdr_.width, hdr_.height);
         if (st != JD_OK) throw std::runtime_error(out + ": " + jd_status_str(st));
     }
 
@@ -78,6 +83,10 @@ class JPEGParser {
     const jd_header& header() const { return hdr_; }
 
   private:
+    std::string stem() const {
+        const size_t dot = filename_.find_last_of('.');
+        return dot == std::string::npos ? filename_ : filename_.substr(0, dot);
+    }
     std::string path_, filename_;
     std::vector<uint8_t> bytes_;
     std::vector<uint8_t> rgb_;

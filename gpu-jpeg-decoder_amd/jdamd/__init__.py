@@ -33,7 +33,7 @@ JD_FLAG_FORCE_LANES = 4
 JD_FLAG_FANCY_UPSAMPLING = 8
 JD_FLAG_FULL_PIECES = 16
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES, "full": JD_FLAG_FULL_PIECES}
-JD_ABI_VERSION = 3
+JD_ABI_VERSION = 4
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece_scan", "k_rescan", "k_chain",
                 "k_piece_write", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
@@ -78,7 +78,7 @@ class _Stats(ctypes.Structure):
 # Every symbol include/jd.h and include/jd_test.h declare (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = [
     "jd_ctx_create", "jd_ctx_destroy", "jd_parse", "jd_decode", "jd_decode_file", "jd_decode_batch",
-    "jd_decode_batch_async", "jd_decode_wait", "jd_write_array", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
+    "jd_decode_batch_async", "jd_decode_wait", "jd_write_array", "jd_write_ppm", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
     "jd_memcpy_h2d", "jd_memcpy_d2h", "jd_synchronize", "jd_get_stats", "jd_reset_stats",
     "jd_kernel_name", "jd_test_idct", "jd_test_idct_exact", "jd_test_color", "jd_debug_fetch", "jd_ctx_last_error",
 ]
@@ -109,6 +109,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         "jd_decode_batch_async": (c_int, [c_void_p, ctypes.POINTER(_Item), c_int, ctypes.POINTER(_Result), c_void_p]),
         "jd_decode_wait": (c_int, [c_void_p]),
         "jd_write_array": (c_int, [ctypes.c_char_p, c_void_p, c_int, c_int]),
+        "jd_write_ppm": (c_int, [ctypes.c_char_p, c_void_p, c_int, c_int]),
         "jd_status_str": (ctypes.c_char_p, [c_int]),
         "jd_abi_version": (c_int, []),
         "jd_device_alloc": (c_int, [c_void_p, c_size_t, ctypes.POINTER(c_void_p)]),
@@ -176,6 +177,15 @@ def write_array(path: str, rgb: np.ndarray) -> None:
     st = load_library().jd_write_array(path.encode(), rgb.ctypes.data, rgb.shape[1], rgb.shape[0])
     if st != JD_OK:
         raise JDError(st, "jd_write_array")
+
+
+def write_ppm(path: str, rgb: np.ndarray) -> None:
+    """Binary PPM (P6), the format of the reference's libjpeg comparison outputs
+    (testing/jpeglib_output_ppm/, read by jpeglib-implementation/process_ppm.py)."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    st = load_library().jd_write_ppm(path.encode(), rgb.ctypes.data, rgb.shape[1], rgb.shape[0])
+    if st != JD_OK:
+        raise JDError(st, "jd_write_ppm")
 
 
 class DeviceBuffer:

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define JD_ABI_VERSION 3
+#define JD_ABI_VERSION 4
 
 typedef enum jd_status {
     JD_OK = 0,
@@ -116,7 +116,9 @@ jd_status jd_decode_file(jd_ctx* ctx, const char* path, uint8_t* rgb, size_t rgb
 /* Batched decode of independent images.  Replaces batchDecodeKernel<<<N,T>>>(DeviceData*)
  * (cuda-decoder/src/parser.cu:663-682, driven by benchmark_thoughput/benchmark.cu:43-93).
  * hip_stream: hipStream_t to order the work on, or NULL for the context's own stream.  The call
- * returns after the batch completes; per-image status in results[i]. */
+ * returns after the batch completes; per-image status in results[i].  The context's scratch pools
+ * are ordered by stream only: a call on another stream than the one of still-pending
+ * jd_decode_batch_async launches first collects them (jd_decode_wait). */
 jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
                           int rgb_on_device, void* hip_stream);
 
@@ -135,6 +137,11 @@ jd_status jd_decode_wait(jd_ctx* ctx);
  * per line, no trailing newline.  Replaces JPEGParser::write() (cpp-decoder/src/parser.cpp:197-209)
  * and the CUDA write() (cuda-decoder/src/parser.cu:702-744). */
 jd_status jd_write_array(const char* path, const uint8_t* rgb, int width, int height);
+
+/* Binary PPM (P6) writer: "P6\n<W> <H>\n255\n" then the interleaved RGB bytes — the format of the
+ * reference's libjpeg comparison outputs (testing/jpeglib_output_ppm/<name>.ppm, read back by
+ * jpeglib-implementation/process_ppm.py into `.array` files for testing/compare.py). */
+jd_status jd_write_ppm(const char* path, const uint8_t* rgb, int width, int height);
 
 const char* jd_status_str(jd_status st);
 int jd_abi_version(void);

@@ -1,20 +1,24 @@
 """Multi-process path of bench.py on CPU: gloo, world_size 2.
 
 The decode path shards by image (no data-path collective); the only collective is one all-gather
-of per-rank counters, after which rank 0 reports max-over-ranks time and summed work.  Here the
-same functions bench.py uses run under gloo with two ranks.
+of per-rank counters, after which rank 0 reports max-over-ranks time and summed work.  Here
+bench.py's own rank/device selection (dist_setup), shard assignment (shard_seeds), host-thread
+split (host_threads) and counter all-gather run under gloo with two ranks.
 """
 import hashlib
 import os
 import socket
 import sys
 
-import pytest
+import numpy as np
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tools"), os.path.join(ROOT, "gpu-jpeg-decoder_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
 
 
 def _free_port():
@@ -24,42 +28,79 @@ def _free_port():
 
 
 def _worker(rank, world, port, batch, q):
-    sys.path.insert(0, ROOT)
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    for p in (ROOT, os.path.join(ROOT, "tools"), os.path.join(ROOT, "gpu-jpeg-decoder_amd")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), JD_DIST_BACKEND="gloo")
     import bench
     import jd_synth
 
-    seed0 = bench.rank_seed(rank, batch)
-    datas = jd_synth.make_batch(batch, 64, 48, 90, "4:2:0", 1, 0, seed0, workers=1)
-    digests = [hashlib.sha1(d).hexdigest() for d in datas]
+    d = bench.dist_setup()
+    threads, info = bench.host_threads(d)
+    seeds_c2 = bench.shard_seeds("c2", batch, d["rank"], d["world"])
+    seeds_c5 = bench.shard_seeds("c5", batch, d["rank"], d["world"])
+    jobs = jd_synth.make_jobs(seeds_c2, 64, 48, 90, "4:2:0", 1, 0)
+    digests = [hashlib.sha1(x).hexdigest() for x in jd_synth.make_images(jobs, workers=1)]
     elapsed = 1.0 + rank  # rank 1 is the slow one
     local = torch.tensor([elapsed, 64 * 48 * batch, batch, 100.0 * (rank + 1), 7.0], dtype=torch.float64)
     t_max, sums = bench.gather_counters(local, world)
-    q.put((rank, digests, t_max, sums))
+    mat = bench.gather_matrix(torch.tensor([float(rank), float(len(seeds_c5))], dtype=torch.float64), world)
+    q.put((rank, d, threads, info, seeds_c2, seeds_c5, digests, t_max, sums, mat.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_bench_sharding_and_counter_gather_gloo():
-    world, batch = 2, 3
+def test_bench_rank_setup_sharding_and_counter_gather_gloo():
+    world, batch = 2, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, batch, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=180) for _ in range(world)]
+    out = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    out.sort()
-    d0, d1 = set(out[0][1]), set(out[1][1])
-    assert len(d0) == batch and len(d1) == batch and not (d0 & d1), "ranks must decode disjoint images"
-    for _, _, t_max, sums in out:
+    out.sort(key=lambda t: t[0])
+    for rank, d, threads, info, _, _, _, t_max, sums, mat in out:
+        assert d["world_seen"] == world and d["rank"] == rank and d["backend"] == "gloo"
+        assert d["device_index"] == rank  # one device per local rank (no GPU here: index only)
+        assert 1 <= threads <= bench_share() and info["rank_cpus"] >= 1
         assert t_max == 2.0                      # max over ranks, not rank 0's own clock
         assert sums[0] == 2 * 64 * 48 * batch    # pixels summed over ranks
         assert sums[1] == 2 * batch
         assert sums[2] == 300.0
         assert sums[3] == 14.0
+        assert [r[0] for r in mat] == [0.0, 1.0] and sum(r[1] for r in mat) == world * batch
+    d0, d1 = set(out[0][6]), set(out[1][6])
+    assert len(d0) == batch and len(d1) == batch and not (d0 & d1), "ranks must decode disjoint images"
+    c2 = [set(o[4]) for o in out]
+    assert not (c2[0] & c2[1]) and c2[0] | c2[1] == set(range(world * batch))
+    c5 = [set(o[5]) for o in out]
+    assert not (c5[0] & c5[1]) and c5[0] | c5[1] == set(range(world * batch))
+    assert all(len(s) == batch for s in c5)
+
+
+def bench_share():
+    import bench
+
+    return bench.BOX_CPU_SHARE
+
+
+def test_mixed_shards_balance_entropy_bytes():
+    """C5-style mixed batch at 1080p (sizes vary 5x by subsampling and quality): the greedy
+    assignment by estimated ECS bytes balances the ranks' real encoded bytes better than
+    contiguous seed ranges."""
+    import bench
+    import jd_synth
+
+    world, batch = 4, 6
+    seeds = range(world * batch)
+    sizes = {s: len(b) for s, b in zip(seeds, jd_synth.make_images(jd_synth.make_jobs(seeds, 1920, 1080, mixed=True)))}
+    greedy = [sum(sizes[s] for s in bench.shard_seeds("c5", batch, r, world)) for r in range(world)]
+    contiguous = [sum(sizes[s] for s in range(r * batch, (r + 1) * batch)) for r in range(world)]
+    assert sorted(s for r in range(world) for s in bench.shard_seeds("c5", batch, r, world)) == list(seeds)
+    imb = lambda v: max(v) / np.mean(v)  # noqa: E731
+    assert imb(greedy) <= 1.08, greedy
+    assert imb(greedy) <= imb(contiguous), (greedy, contiguous)

@@ -65,22 +65,56 @@ def _one(args):
                   encoder=encoder)
 
 
-def make_batch(n: int, w: int, h: int, quality: int = 90, subsampling: str = "4:2:0", restart_rows: int = 0,
-               restart_blocks: int = 0, seed0: int = 0, workers: Optional[int] = None,
-               mixed: bool = False, encoder: Optional[str] = None) -> List[bytes]:
-    """n synthetic JPEGs.  mixed=True cycles 4:4:4 / 4:2:2 / 4:2:0 and draws quality from
-    {50, 75, 90, 95} by seed (BASELINE config 5), without restart markers."""
+MIXED_SUBSAMPLING = ("4:4:4", "4:2:2", "4:2:0")
+MIXED_QUALITY = (50, 75, 90, 95)
+# Bits per pixel of these synthetic images at 1080p (jdenc, standard tables), by subsampling and
+# quality: the ECS-size model bench.py balances mixed shards with (measured; 480x272 images run
+# about 8 % higher).
+BPP_1080P = {"4:4:4": (1.594, 2.247, 3.561, 5.467), "4:2:2": (1.237, 1.726, 2.765, 4.093),
+             "4:2:0": (0.972, 1.385, 2.260, 3.426)}
+
+
+def mixed_params(seed: int):
+    """(subsampling, quality) of image `seed` of a mixed batch (BASELINE config 5): subsampling
+    cycles with the seed, quality is drawn from {50, 75, 90, 95} by it."""
+    ss = MIXED_SUBSAMPLING[seed % 3]
+    q = MIXED_QUALITY[int(np.random.default_rng(seed + 7777).integers(0, 4))]
+    return ss, q
+
+
+def estimated_bytes(w: int, h: int, subsampling: str, quality: int) -> float:
+    """Model of an image's size (jdenc, standard tables) for shard balancing; 4:2:0 q90 otherwise."""
+    row = BPP_1080P.get(subsampling, BPP_1080P["4:2:0"])
+    qi = MIXED_QUALITY.index(quality) if quality in MIXED_QUALITY else 2
+    return w * h * row[qi] / 8.0
+
+
+def make_jobs(seeds, w, h, quality=90, subsampling="4:2:0", restart_rows=0, restart_blocks=0, mixed=False,
+              encoder=None):
     jobs = []
-    for i in range(n):
-        s = seed0 + i
+    for s in seeds:
         if mixed:
-            ss = ("4:4:4", "4:2:2", "4:2:0")[i % 3]
-            q = (50, 75, 90, 95)[np.random.default_rng(s + 7777).integers(0, 4)]
-            jobs.append((w, h, s, int(q), ss, 0, 0, encoder))
+            ss, q = mixed_params(int(s))
+            jobs.append((w, h, int(s), q, ss, 0, 0, encoder))
         else:
-            jobs.append((w, h, s, quality, subsampling, restart_rows, restart_blocks, encoder))
+            jobs.append((w, h, int(s), quality, subsampling, restart_rows, restart_blocks, encoder))
+    return jobs
+
+
+def make_images(jobs, workers: Optional[int] = None) -> List[bytes]:
+    n = len(jobs)
     workers = workers or min(16, os.cpu_count() or 1, max(1, n))
     if workers <= 1 or n < 4:
         return [_one(j) for j in jobs]
     with ProcessPoolExecutor(workers) as ex:
         return list(ex.map(_one, jobs, chunksize=max(1, n // (workers * 4))))
+
+
+def make_batch(n: int, w: int, h: int, quality: int = 90, subsampling: str = "4:2:0", restart_rows: int = 0,
+               restart_blocks: int = 0, seed0: int = 0, workers: Optional[int] = None,
+               mixed: bool = False, encoder: Optional[str] = None) -> List[bytes]:
+    """n synthetic JPEGs of seeds seed0 .. seed0+n-1.  mixed=True: BASELINE config 5 (mixed_params
+    per seed), without restart markers."""
+    jobs = make_jobs(range(seed0, seed0 + n), w, h, quality, subsampling, restart_rows, restart_blocks, mixed,
+                     encoder)
+    return make_images(jobs, workers)
