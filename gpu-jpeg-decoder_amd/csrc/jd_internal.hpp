@@ -174,7 +174,7 @@ struct alignas(16) CpRec {
     uint32_t bit, mcus, ents, flags;
 };
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
-constexpr int kTileMaxBlocks = 64;   // blocks per IDCT/colour tile (one lane each)
+constexpr int kTileMaxBlocks = 60;   // blocks per IDCT/colour tile (one lane each; k_idct_color's LDS)
 
 // Per-image status bits written by kernels (atomicOr); host maps them to jd_status.
 constexpr uint32_t kStCorrupt = 1u;     // bad code / overrun / DC range
@@ -234,7 +234,7 @@ struct BatchDev {
     uint32_t* entries;
     uint64_t entries_cap;         // entry slots allocated
     uint32_t* status;             // per image
-    unsigned long long* counters; // [0] AC entries written, [1] slow_tiles entries
+    unsigned long long* counters; // [0] AC entries written, [1] slow_tiles entries, [2] k_idct_color's tile queue
     uint32_t max_tiles;
     TileRef* slow_tiles;          // (image, tile) k_idct_color left to k_idct_color_exact; count in counters[1]
     uint32_t total_tiles;
@@ -242,6 +242,7 @@ struct BatchDev {
                                   // of components 0..2 at the tile's first block
     // fancy upsampling (JD_FLAG_FANCY_UPSAMPLING): k_idct_color writes component planes to HBM
     // (ImgDesc::planes), k_colour_fancy filters and colours them
+    unsigned long long* stamps;   // diagnostic builds (JD_STAMP): 8 s_memtime stamps per IDCT tile, else null
     uint32_t fancy;
     uint32_t max_fancy_wgs;       // k_colour_fancy workgroups per image (grid x)
 };

@@ -1766,19 +1766,20 @@ __device__ __forceinline__ uint32_t pk_clamp_add(uint32_t y, uint32_t t) {
 __device__ __forceinline__ uint32_t pair16(int lo, int hi) { return (uint32_t(lo) & 0xFFFFu) | (uint32_t(hi) << 16); }
 
 // Terms of the 8 >> SH chroma samples under 8 pixels as per-word pairs (word u = pixels 2u, 2u+1).
+// Returns the mask of samples (bit u) whose G needs the reference's double-precision path.
 template <int SH>
-__device__ __forceinline__ bool terms_words(const int16_t* s_pl, uint32_t cboff, uint32_t croff, uint32_t (&TR)[4],
-                                            uint32_t (&TG)[4], uint32_t (&TB)[4]) {
+__device__ __forceinline__ uint32_t terms_words(const int16_t* s_pl, uint32_t cboff, uint32_t croff, uint32_t (&TR)[4],
+                                                uint32_t (&TG)[4], uint32_t (&TB)[4]) {
     constexpr int NU = 8 >> SH;
     int cb[8], cr[8];
     load_plane<SH>(s_pl, cboff, cb);
     load_plane<SH>(s_pl, croff, cr);
     ChromaTerms t[NU];
-    bool ex = false;
+    uint32_t ex = 0;
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         t[u] = chroma_terms(cb[u], cr[u]);
-        ex = ex || t[u].exact;
+        ex |= t[u].exact ? (1u << u) : 0u;
     }
 #pragma unroll
     for (int w = 0; w < 4; w++) {
@@ -1789,6 +1790,24 @@ __device__ __forceinline__ bool terms_words(const int16_t* s_pl, uint32_t cboff,
         TB[w] = pair16(t[a].b, t[c].b);
     }
     return ex;
+}
+
+// The rare fix-up of the packed path: the G byte of every pixel of this row whose chroma sample
+// is in exmask, recomputed with the reference's double-precision formula (color.cpp:13-17).
+template <int SH>
+__device__ __forceinline__ void fix_g_exact(const uint4& Yq, const int16_t* s_pl, uint32_t cboff, uint32_t croff,
+                                            uint32_t exmask, uint32_t (&w)[6]) {
+    const uint32_t Y[4] = {Yq.x, Yq.y, Yq.z, Yq.w};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int u = j >> SH;
+        if ((exmask >> u) & 1u) {
+            const int y = (j & 1) ? int32_t(Y[j >> 1]) >> 16 : int(int16_t(Y[j >> 1] & 0xFFFFu));
+            const int g = color_g_exact(y, s_pl[cboff + u], s_pl[croff + u]);
+            const int byte = 3 * j + 1;  // channel G of pixel j: byte 3j + 1 of the 24
+            w[byte >> 2] = (w[byte >> 2] & ~(0xFFu << (8 * (byte & 3)))) | (uint32_t(g) << (8 * (byte & 3)));
+        }
+    }
 }
 
 // 8 pixels of one row: Y as 4 words of int16 pairs -> 24 RGB bytes in 6 words (pack24's order).
@@ -1852,104 +1871,173 @@ __device__ __forceinline__ size_t fancy_plane_off(const ImgDesc& im, uint32_t c)
     return off;
 }
 
-// staging (64 rows of 66 int16 = 33 words: odd pitch, conflict-free read-back) and then the
-// component planes share s_buf; planes need at most 64*64 + 64*2*6 int16 (§ host tile choice)
-constexpr int kIdctBufWords = 2464;
+// LDS of a tile (8112 B, so 20 waves fit a CU: 5 per SIMD, which the kernel's 96 VGPRs allow too):
+//  * staging: kTileMaxBlocks rows of 64 int16 (128 B, zig-zag order), the 16-byte quads of lane l's
+//    row XOR-swizzled by (l >> 1) & 7 so that a wave's ds_read_b128 of one quad index from every row
+//    is bank-conflict free (the 16 lanes of each of its four lane groups hit 16 distinct quad slots)
+//  * then, reusing the same words, the tile's component planes (int16, unpadded: exactly the tile's
+//    kTileMaxBlocks * 64 samples)
+//  * the quant steps of the image's components
+constexpr int kIdctBufWords = kTileMaxBlocks * 32;
 constexpr int kQzWords = 3 * 36;  // quant steps per component, zig-zag order, as u16 pairs (pitch 36
                                   // words: 16-byte rows; a wave reads at most 3 distinct rows)
+static_assert(kIdctBufWords * 4 + kQzWords * 4 <= 8192, "k_idct_color must fit 20 waves per CU");
+// Byte address (in s_buf) of quad q of lane l's staging row; base = staging_base(l).
+__device__ __forceinline__ uint32_t staging_base(uint32_t l) { return l * 128u + (((l >> 1) & 7u) << 4); }
+#ifndef JD_PRE_QUADS
+#define JD_PRE_QUADS 4
+#endif
+constexpr int kPreQuads = JD_PRE_QUADS;  // entry quads per lane loaded before the DC prediction
 
-// One tile.  EXACT = false (k_idct_color): a wave with a coefficient beyond the fast IDCT's range
-// (never seen in real images) appends its tile to slow_tiles and leaves; EXACT = true
-// (k_idct_color_exact) decodes those tiles with the exact IDCT form.
-template <bool EXACT>
-__device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint32_t tile, uint32_t* s_buf, int* s_qz) {
-    const ImgDesc& im = b.imgs[img];
-    if (tile >= im.tiles_x * im.tiles_y) return;
-    const uint32_t lane = threadIdx.x;
-    const TileGeo G = tile_geo(im, tile);
-    const uint32_t TM = im.tile_mcus, bpm = im.bpm, nc = im.ncomp;
-    const uint32_t m0 = G.m0, r0 = G.g0 / im.mcux, nm = G.nm;
-    if (lane < 16 * nc) {  // quant steps: lane = 4 steps of one component (64 steps = 16 lanes)
+// A tile's lane: lane j owns block j of the tile (MCU m, block bb within the MCU).
+struct TileLaneGeo {
+    uint32_t m, bb, comp;
+    bool have;
+};
+__device__ __forceinline__ TileLaneGeo tile_lane_geo(const ImgDesc& im, const TileGeo& G, uint32_t lane) {
+    TileLaneGeo L;
+    L.m = div_small(lane, magic16(im.bpm));
+    L.bb = lane - L.m * im.bpm;
+    L.have = L.m < G.nm;
+    L.comp = (im.block_pattern >> (2 * L.bb)) & 3u;
+    return L;
+}
+
+__device__ __forceinline__ BlockInfo load_block_info(const BatchDev& b, const ImgDesc& im, const TileGeo& G,
+                                                     const TileLaneGeo& L) {
+    return L.have ? b.blocks[im.block_base + uint64_t(G.g0 + L.m) * im.bpm + L.bb] : BlockInfo{0u, 0u};
+}
+
+// The lane's AC entries: [first, first + cnt) of the image's entry array, read as 16-byte quads
+// from the quad holding the first one (lead = its position in that quad).  A block of a corrupt
+// stream may never have been written: never index past the image's entries.
+struct EntryRange {
+    const uint32_t* ep;  // 16-byte aligned
+    uint32_t lead;
+    int cnt, n4;         // entries, quads (cnt == 0: no quad is touched)
+};
+__device__ __forceinline__ EntryRange entry_range(const BatchDev& b, const ImgDesc& im, const BlockInfo& bi, bool have) {
+    EntryRange r;
+    r.cnt = have ? int(bi.cnt_dc >> 26) : 0;
+    if (uint64_t(bi.entry_start) + uint64_t(r.cnt) > im.entry_cap) r.cnt = 0;
+    r.lead = bi.entry_start & 3u;
+    r.ep = b.entries + im.entry_base + (bi.entry_start - r.lead);
+    r.n4 = r.cnt > 0 ? int(r.lead + uint32_t(r.cnt) + 3u) >> 2 : 0;
+    return r;
+}
+
+// The first kPreQuads quads (the entry buffer is padded by 64 B past its last slot).
+__device__ __forceinline__ void load_entry_quads(const EntryRange& r, uint4 (&E)[kPreQuads]) {
+#pragma unroll
+    for (int u = 0; u < kPreQuads; u++)
+        E[u] = (u < r.n4) ? *reinterpret_cast<const uint4*>(r.ep + 4 * u) : make_uint4(0, 0, 0, 0);
+}
+
+// Entries of quad index qi (its 4 words in w) to the lane's staging row at their zig-zag positions:
+// int16 zz of the row is at byte 2 zz, swizzled (staging_base): row base ^ (2 zz & 0x7E).
+__device__ __forceinline__ void scatter_quad(uint8_t* s_bytes, uint32_t base, const uint4& v, int qi,
+                                             const EntryRange& r) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int i = 4 * qi + q - int(r.lead);
+        if (i >= 0 && i < r.cnt) *reinterpret_cast<int16_t*>(s_bytes + (base ^ ((w[q] << 1) & 0x7Eu))) = int16_t(w[q] >> 16);
+    }
+}
+
+// Sparse -> dense for the lane's block: the prefetched quads, then the rest (blocks with more
+// than 4 * kPreQuads - lead entries) four quads in flight at a time.
+__device__ __forceinline__ void scatter_entries(uint32_t* s_buf, uint32_t base, const EntryRange& r,
+                                                const uint4 (&E)[kPreQuads]) {
+    uint8_t* row = reinterpret_cast<uint8_t*>(s_buf);
+#if !(JD_ABL & 4)
+#pragma unroll
+    for (int u = 0; u < kPreQuads; u++) scatter_quad(row, base, E[u], u, r);
+    for (int c = kPreQuads; c < r.n4; c += 4) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            v[u] = (c + u < r.n4) ? *reinterpret_cast<const uint4*>(r.ep + 4 * (c + u)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; u++) scatter_quad(row, base, v[u], c + u, r);
+    }
+#endif
+}
+
+// DC prediction (parser.cpp:106-111): segmented scan of the tile's DC differences onto its entry
+// predictors (tile_dc, k_dc_scan); a block that starts an interval resets its component's
+// predictor.  Exact int, as the reference's int predictor: the int16 staging is bypassed.
+__device__ __forceinline__ int tile_dc_predict(const TileGeo& G, const TileLaneGeo& L, const BlockInfo& bi,
+                                               const DcPred& cin, uint32_t lane) {
+    const int d = L.have ? int32_t(bi.cnt_dc << 6) >> 6 : 0;
+    const bool start = L.have && L.bb == 0 && tile_mcu_starts(G, L.m);
+    const uint64_t smask = __ballot(start);
+    const uint32_t comp = L.comp;
+    const int p0 = wave_scan_dpp(comp == 0 ? d : 0);
+    const int p1 = wave_scan_dpp(comp == 1 ? d : 0);
+    const int p2 = wave_scan_dpp(comp == 2 ? d : 0);
+    int dc = comp == 0 ? p0 : (comp == 1 ? p1 : p2);
+    const uint64_t upto = smask & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+    if (upto == 0) dc += comp == 0 ? cin.p0 : (comp == 1 ? cin.p1 : cin.p2);
+    if (smask & ~1ull) {  // wave-uniform: an interval starts inside the tile
+        const int ls = upto ? 63 - int(__clzll(upto)) : 0;  // my segment's first lane
+        const int src = max(ls - 1, 0);
+        const int q0 = __shfl(p0, src, 64), q1 = __shfl(p1, src, 64), q2 = __shfl(p2, src, 64);
+        if (upto && ls > 0) dc -= comp == 0 ? q0 : (comp == 1 ? q1 : q2);
+    }
+    return dc;
+}
+
+// Quant steps of the image's components to LDS (lane = 4 steps of one component).
+__device__ __forceinline__ void stage_quant(const BatchDev& b, const ImgDesc& im, int* s_qz, uint32_t lane) {
+    if (lane < 16 * im.ncomp) {
         const uint32_t c = lane >> 4, q = lane & 15u;
         const uint2 v = *reinterpret_cast<const uint2*>(b.qtabs + size_t(im.qslot[c]) * 64 + 4 * q);
         *reinterpret_cast<uint2*>(s_qz + c * 36 + 2 * q) = v;
     }
-    constexpr int kRow16 = 33;  // words per staging row
+}
+
+__device__ __forceinline__ void zero_staging(uint32_t* s_buf, uint32_t lane) {
     uint4* z4 = reinterpret_cast<uint4*>(s_buf);
 #pragma unroll
-    for (uint32_t k = 0; k < (64 * kRow16 + 3) / 4 / kIdctThreads + 1; k++) {
+    for (uint32_t k = 0; k < (kIdctBufWords / 4 + kIdctThreads - 1) / kIdctThreads; k++) {
         const uint32_t i = lane + k * kIdctThreads;
-        if (i < (64 * kRow16 + 3) / 4) z4[i] = make_uint4(0, 0, 0, 0);
+        if (i < kIdctBufWords / 4) z4[i] = make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
+}
 
-    // 1. sparse -> dense (my block): quantised coefficients at their zig-zag positions
-    //    (parser.cpp:111,130: the dequantisation happens on read-back, in zig-zag correspondence)
-    const uint32_t m = div_small(lane, magic16(bpm)), bb = lane - m * bpm;
-    const bool have = m < nm;
-    const uint32_t mi = m, mr = 0;
-    const uint32_t comp = (im.block_pattern >> (2 * bb)) & 3u;
-    int16_t* row = reinterpret_cast<int16_t*>(s_buf + lane * kRow16);
-    const BlockInfo bi = have ? b.blocks[im.block_base + uint64_t(G.g0 + m) * bpm + bb] : BlockInfo{0u, 0u};
-    int dc_pred;
-    {  // DC prediction: segmented scan of the tile's DC differences onto its entry predictors
-        // (tile_dc, k_dc_scan); a block that starts an interval resets its component's predictor
-        const int d = have ? int32_t(bi.cnt_dc << 6) >> 6 : 0;
-        const bool start = have && bb == 0 && tile_mcu_starts(G, m);
-        const uint64_t smask = __ballot(start);
-        const int p0 = wave_scan_dpp(comp == 0 ? d : 0);
-        const int p1 = wave_scan_dpp(comp == 1 ? d : 0);
-        const int p2 = wave_scan_dpp(comp == 2 ? d : 0);
-        const DcPred cin = b.tile_dc[im.tile_base + tile];
-        int dc = comp == 0 ? p0 : (comp == 1 ? p1 : p2);
-        const uint64_t upto = smask & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
-        if (upto == 0) {
-            dc += comp == 0 ? cin.p0 : (comp == 1 ? cin.p1 : cin.p2);
-        }
-        if (smask & ~1ull) {  // wave-uniform: an interval starts inside the tile
-            const int ls = upto ? 63 - int(__clzll(upto)) : 0;  // my segment's first lane
-            const int src = max(ls - 1, 0);
-            const int q0 = __shfl(p0, src, 64), q1 = __shfl(p1, src, 64), q2 = __shfl(p2, src, 64);
-            if (upto && ls > 0) dc -= comp == 0 ? q0 : (comp == 1 ? q1 : q2);
-        }
-        dc_pred = dc;  // exact int, as the reference's int predictor (parser.cpp:106-111): the
-                       // staging below is int16, so DC bypasses it
-    }
-    if (have) {
-        // a block of a corrupt stream may never have been written: never index past the entries
-        int cnt = int(bi.cnt_dc >> 26);
-        if (uint64_t(bi.entry_start) + uint64_t(cnt) > im.entry_cap) cnt = 0;
-        // entries in 16-byte loads, four in flight at a time (the entry buffer is padded by 64 B)
-        const uint32_t lead = bi.entry_start & 3u;
-        const uint32_t* ep = b.entries + im.entry_base + (bi.entry_start - lead);
-        const int n4 = cnt > 0 ? int(lead + uint32_t(cnt) + 3u) >> 2 : 0;  // cnt == 0: touch nothing
-#if JD_ABL & 4
-        if (lane == 1000)
-#endif
-        for (int c = 0; c < n4; c += 4) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                v[u] = (c + u < n4) ? *reinterpret_cast<const uint4*>(ep + 4 * (c + u)) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int i = 4 * (c + u) + q - int(lead);
-                    if (i >= 0 && i < cnt) row[w[q] & 63u] = int16_t(w[q] >> 16);
-                }
-            }
-        }
-    }
-    __syncthreads();
-
-    // 2. dequantise in zig-zag order (24-bit multiplies: |coef| < 2^15, q < 2^16) into natural
-    //    positions (a compile-time permutation of registers), then the IDCT in registers
+// The rest of a tile once its staging rows hold the quantised coefficients (zig-zag order) and
+// dc_pred the lane's DC: dequantisation, IDCT, planes, upsample + colour + store.
+//  * EXACT = false (k_idct_color): a wave with a coefficient beyond the fast IDCT's range (never
+//    seen in real images) appends its tile to slow_tiles and returns false;
+//  * EXACT = true (k_idct_color_exact) decodes those tiles with the exact IDCT form.
+template <bool EXACT, class Mid>
+__device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDesc& im, uint32_t img, uint32_t tile,
+                                                 const TileGeo& G, const TileLaneGeo& L, int dc_pred,
+                                                 uint32_t* s_buf, const int* s_qz, Mid&& mid) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t TM = im.tile_mcus, nc = im.ncomp;
+    const uint32_t m0 = G.m0, r0 = G.g0 / im.mcux;
+    const uint32_t mi = L.m, mr = 0, bb = L.bb, comp = L.comp;
+    const bool have = L.have;
+    // dequantise in zig-zag order (24-bit multiplies: |coef| < 2^15, q < 2^16) into natural
+    // positions (a compile-time permutation of registers), then the IDCT in registers
     //    The fast IDCT form needs every dequantised coefficient within +-2^16: an AC coefficient
     //    c is when |c| <= 2^(k-1) with 2^(k-1) * (largest quant step) < 2^16 (host: im.qmask),
     //    i.e. when bits k-1..15 of c all equal its sign: c ^ (c << 1) has bits k..15 clear.
-    const uint32_t* rw = s_buf + lane * kRow16;
+    // the lane's staging row as 8 quads (swizzled: quad q at base ^ 16 q); lanes without a block
+    // read row 0 (their results are never used)
+    const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_buf);
+    const uint32_t sbase = staging_base(have ? lane : 0u);
+    uint32_t rw[32];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const uint4 v = *reinterpret_cast<const uint4*>(s_bytes + (sbase ^ (16u * q)));
+        rw[4 * q + 0] = v.x;
+        rw[4 * q + 1] = v.y;
+        rw[4 * q + 2] = v.z;
+        rw[4 * q + 3] = v.w;
+    }
     const uint4* qz4 = reinterpret_cast<const uint4*>(s_qz + comp * 36);
     const int dq0 = dc_pred * int(reinterpret_cast<const uint16_t*>(s_qz)[comp * 72]);
     if (!EXACT) {  // range test before dequantising: the branch then holds no 64-value block
@@ -1965,7 +2053,8 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
                 const uint32_t k = uint32_t(atomicAdd(&b.counters[1], 1ull));
                 b.slow_tiles[k] = TileRef{img, tile};
             }
-            return;
+            mid();
+            return false;
         }
     }
     int blk[64];
@@ -1984,6 +2073,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
 #if !(JD_ABL & 2)
     idct_block(blk, !EXACT);
 #endif
+    mid();  // (k_idct_color: the next tile's entry loads, issued here so they are not live across the IDCT)
     if (b.fancy) {  // wave-uniform: component planes to HBM, k_colour_fancy takes it from there
         if (have) {
             const uint32_t hc = im.h[comp], vc = im.v[comp];
@@ -2001,11 +2091,11 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
                 *gptr(reinterpret_cast<u32x4*>(dst + size_t(r) * (im.mcux * hc * 8))) = u32x4{q.x, q.y, q.z, q.w};
             }
         }
-        return;
+        return true;
     }
     __syncthreads();  // every row read back before the planes overwrite the staging area
 
-    // 3. component planes (int16), pitch = plane width + 8 samples
+    // component planes (int16), pitch = plane width
     int16_t* s_pl = reinterpret_cast<int16_t*>(s_buf);  // planes reuse the staging area
     uint32_t pbase[3] = {0u, 0u, 0u}, ppitch[3] = {8u, 8u, 8u};
     {
@@ -2013,7 +2103,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             if (uint32_t(c) < nc) {
-                ppitch[c] = TM * im.h[c] * 8 + 8;
+                ppitch[c] = TM * im.h[c] * 8;
                 pbase[c] = off;
                 off += ppitch[c] * im.v[c] * 8;  // one MCU row
             }
@@ -2038,8 +2128,8 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
     }
     __syncthreads();
 
-    // 4. upsample + colour: 8 pixels of one row per lane-step, or of two rows when both chroma
-    //    planes are vertically subsampled (the two rows share their chroma samples and terms)
+    // upsample + colour: 8 pixels of one row per lane-step, or of two rows when both chroma
+    // planes are vertically subsampled (the two rows share their chroma samples and terms)
     const uint32_t lg_mw = im.lg_mw, lg_mh = im.lg_mh;
     const uint32_t gpr = (TM << lg_mw) >> 3;  // 8-pixel groups per tile row
     const uint32_t th = 1u << lg_mh;
@@ -2054,7 +2144,7 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
     const uint32_t step_y = kIdctThreads / gpr, step_c = kIdctThreads - step_y * gpr;
     uint32_t gy = gpr <= 64u ? div_small(lane, magic16(gpr)) : 0u, gc = lane - gy * gpr;
 #if JD_ABL & 1
-    if (lane < 1000) return;
+    if (lane < 1000) return true;
 #endif
     for (; gy < ngy; gy += step_y + (gc + step_c >= gpr ? 1u : 0u), gc = gc + step_c >= gpr ? gc + step_c - gpr : gc + step_c) {
         const uint32_t py = gy * rows, gx = gc << 3;
@@ -2064,74 +2154,132 @@ __device__ __forceinline__ void idct_tile(const BatchDev& b, uint32_t img, uint3
         const uint32_t cboff = pbase[1] + (py >> shy1) * ppitch[1] + (gx >> shx1);
         const uint32_t croff = pbase[2] + (py >> shy2) * ppitch[2] + (gx >> shx2);
         uint32_t w0[6], w1[6];
-        bool slow = true;
-        if (cmode <= 2u) {  // wave-uniform
-            uint32_t TR[4], TG[4], TB[4];
-            bool ex;
+        if (cmode <= 2u) {  // wave-uniform: both chroma planes share one horizontal factor
+            // packed integer colour for every pixel; G of the few pixels whose chroma sample needs
+            // the reference's double-precision path is patched afterwards (about 5 % of the
+            // lane-steps have one such sample in some lane)
+            uint32_t TR[4], TG[4], TB[4], ex;
             switch (cmode) {
                 case 0: ex = terms_words<0>(s_pl, cboff, croff, TR, TG, TB); break;
                 case 1: ex = terms_words<1>(s_pl, cboff, croff, TR, TG, TB); break;
                 default: ex = terms_words<2>(s_pl, cboff, croff, TR, TG, TB); break;
             }
-            if (!__any(ex)) {  // uniform over the lanes in this step
-                row_rgb_packed(*reinterpret_cast<const uint4*>(s_pl + yoff), TR, TG, TB, w0);
-                if (pair) row_rgb_packed(*reinterpret_cast<const uint4*>(s_pl + yoff + ppitch[0]), TR, TG, TB, w1);
-                slow = false;
+            const uint4 Y0q = *reinterpret_cast<const uint4*>(s_pl + yoff);
+            row_rgb_packed(Y0q, TR, TG, TB, w0);
+            uint4 Y1q = make_uint4(0, 0, 0, 0);
+            if (pair) {
+                Y1q = *reinterpret_cast<const uint4*>(s_pl + yoff + ppitch[0]);
+                row_rgb_packed(Y1q, TR, TG, TB, w1);
             }
-        }
-        if (slow) {
-        int Y0[8], Y1[8];
-        load_plane<0>(s_pl, yoff, Y0);
-        if (pair) load_plane<0>(s_pl, yoff + ppitch[0], Y1);
-        if (pair) {
-            switch (cmode) {  // wave-uniform
-                case 0: colour16<0>(Y0, Y1, s_pl, cboff, croff, w0, w1); break;
-                case 1: colour16<1>(Y0, Y1, s_pl, cboff, croff, w0, w1); break;
-                default: colour16<2>(Y0, Y1, s_pl, cboff, croff, w0, w1); break;
-            }
-        } else {
-            uint32_t rgb[8][3];
-            switch (cmode) {  // wave-uniform
-                case 0: colour8<0>(Y0, s_pl, cboff, croff, rgb); break;
-                case 1: colour8<1>(Y0, s_pl, cboff, croff, rgb); break;
-                case 2: colour8<2>(Y0, s_pl, cboff, croff, rgb); break;
-                case 3: colour8<3>(Y0, s_pl, cboff, croff, rgb); break;
-                default: {  // chroma planes with different horizontal factors
-                    int Cb[8], Cr[8];
-                    load8_samples(s_pl, cboff, shx1, Cb);
-                    load8_samples(s_pl, croff, shx2, Cr);
-#pragma unroll
-                    for (int j = 0; j < 8; j++)
-                        colour_px(Y0[j], Cb[j], Cr[j], chroma_terms(Cb[j], Cr[j]), rgb[j][0], rgb[j][1], rgb[j][2]);
+            if (__any(ex != 0u)) {  // uniform over the lanes in this step
+                switch (cmode) {
+                    case 0: fix_g_exact<0>(Y0q, s_pl, cboff, croff, ex, w0); break;
+                    case 1: fix_g_exact<1>(Y0q, s_pl, cboff, croff, ex, w0); break;
+                    default: fix_g_exact<2>(Y0q, s_pl, cboff, croff, ex, w0); break;
+                }
+                if (pair) {
+                    switch (cmode) {
+                        case 0: fix_g_exact<0>(Y1q, s_pl, cboff, croff, ex, w1); break;
+                        case 1: fix_g_exact<1>(Y1q, s_pl, cboff, croff, ex, w1); break;
+                        default: fix_g_exact<2>(Y1q, s_pl, cboff, croff, ex, w1); break;
+                    }
                 }
             }
+        } else {  // grayscale, or chroma planes with different horizontal factors: per pixel
+            int Y0[8];
+            load_plane<0>(s_pl, yoff, Y0);
+            uint32_t rgb[8][3];
+            if (cmode == 3u) {
+                colour8<3>(Y0, s_pl, cboff, croff, rgb);
+            } else {
+                int Cb[8], Cr[8];
+                load8_samples(s_pl, cboff, shx1, Cb);
+                load8_samples(s_pl, croff, shx2, Cr);
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    colour_px(Y0[j], Cb[j], Cr[j], chroma_terms(Cb[j], Cr[j]), rgb[j][0], rgb[j][1], rgb[j][2]);
+            }
             pack24(rgb, w0);
-        }
         }
 #if JD_ABL & 32
         if (w0[0] == 0x12345678u && w1[3] == 0x9abcdef0u)
 #endif
         {
-        store24(out + (size_t(y) * W + x) * 3, w0, min(8u, W - x));
-        if (pair && y + 1 < H) store24(out + (size_t(y + 1) * W + x) * 3, w1, min(8u, W - x));
+            store24(out + (size_t(y) * W + x) * 3, w0, min(8u, W - x));
+            if (pair && y + 1 < H) store24(out + (size_t(y + 1) * W + x) * 3, w1, min(8u, W - x));
         }
     }
+    return true;
 }
 
-__global__ __launch_bounds__(kIdctThreads, 4) void k_idct_color(BatchDev b) {
+typedef __attribute__((address_space(4))) const DcPred const_dcpred;
+__device__ __forceinline__ DcPred load_dcpred(const BatchDev& b, const ImgDesc& im, uint32_t tile) {
+    const_dcpred* p = (const_dcpred*)(size_t)(b.tile_dc + im.tile_base + tile);  // uniform: a scalar load
+    return DcPred{p->p0, p->p1, p->p2, p->flag};
+}
+
+#ifndef JD_IDCT_LB
+#define JD_IDCT_LB 5  // 96 VGPRs: 5 waves per SIMD (LDS allows 20 per CU)
+#endif
+#ifndef JD_STAMP
+#define JD_STAMP 0  // diagnostic builds: per-tile s_memtime stamps at the phase boundaries (BatchDev::stamps)
+#endif
+#define JD_STAMP_AT(k)                                                                                     \
+    do {                                                                                                   \
+        if (JD_STAMP && b.stamps && lane == 0) b.stamps[size_t(im.tile_base + tile) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
+// One wave per tile (grid: tiles x images).
+__global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
     __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
-    idct_tile<false>(b, blockIdx.y, blockIdx.x, s_buf, s_qz);
+    const uint32_t lane = threadIdx.x, img = blockIdx.y, tile = blockIdx.x;
+    const ImgDesc& im = b.imgs[img];
+    if (tile >= im.tiles_x * im.tiles_y) return;
+    JD_STAMP_AT(0);
+    const TileGeo G = tile_geo(im, tile);
+    const TileLaneGeo L = tile_lane_geo(im, G, lane);
+    const BlockInfo bi = load_block_info(b, im, G, L);
+    const DcPred dcin = load_dcpred(b, im, tile);
+    stage_quant(b, im, s_qz, lane);
+    zero_staging(s_buf, lane);
+    const EntryRange R = entry_range(b, im, bi, L.have);
+    uint4 E[kPreQuads];
+    load_entry_quads(R, E);
+    const int dc_pred = tile_dc_predict(G, L, bi, dcin, lane);
+    JD_STAMP_AT(1);
+    __syncthreads();
+    scatter_entries(s_buf, staging_base(lane), R, E);
+    __syncthreads();
+    JD_STAMP_AT(2);
+    idct_colour_tile<false>(b, im, img, tile, G, L, dc_pred, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
+    JD_STAMP_AT(4);
 }
 
 // The tiles k_idct_color left (grid-stride over the list; empty in practice).
 __global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
     __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
+    const uint32_t lane = threadIdx.x;
     const uint32_t n = uint32_t(min(b.counters[1], (unsigned long long)b.total_tiles));
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const TileRef t = b.slow_tiles[i];
-        idct_tile<true>(b, t.img, t.tile, s_buf, s_qz);
+        const TileRef tr = b.slow_tiles[i];
+        const ImgDesc& im = b.imgs[tr.img];
+        if (tr.tile >= im.tiles_x * im.tiles_y) continue;
+        const TileGeo G = tile_geo(im, tr.tile);
+        const TileLaneGeo L = tile_lane_geo(im, G, lane);
+        __syncthreads();
+        stage_quant(b, im, s_qz, lane);
+        zero_staging(s_buf, lane);
+        const BlockInfo bi = load_block_info(b, im, G, L);
+        const int dc_pred = tile_dc_predict(G, L, bi, b.tile_dc[im.tile_base + tr.tile], lane);
+        __syncthreads();
+        const EntryRange R = entry_range(b, im, bi, L.have);
+        uint4 E[kPreQuads];
+        load_entry_quads(R, E);
+        scatter_entries(s_buf, staging_base(lane), R, E);
+        __syncthreads();
+        idct_colour_tile<true>(b, im, tr.img, tr.tile, G, L, dc_pred, s_buf, s_qz, [] {});
     }
 }
 

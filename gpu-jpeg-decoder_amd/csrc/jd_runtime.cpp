@@ -153,7 +153,7 @@ struct jd_ctx {
     size_t lut_dev_count = 0;
 
     // pools
-    DevBuf plan, chunk_brk, blocks, entries, input, output, comp, planes;
+    DevBuf plan, chunk_brk, blocks, entries, input, output, comp, planes, stamps;
     PinBuf input_host;
 
     Pending pend[2];
@@ -668,7 +668,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_chain = put(blob, P.chain_seg);
         const size_t o_chts = put(blob, P.chain_wg_tableset);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
-        const size_t o_ctr = put(blob, std::vector<unsigned long long>(2, 0));
+        const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // entries, slow tiles, IDCT queue
         const size_t upload = blob.size();
         // device-written scratch after the uploaded part (no initialisation needed)
         size_t end = upload;
@@ -743,6 +743,11 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
         b.max_tiles = P.max_tiles;
+        if (std::getenv("JD_STAMPS")) {  // diagnostic builds (JD_STAMP): per-tile phase stamps
+            HIPCHK(ctx, ensure_dev(ctx->stamps, size_t(P.total_tiles) * 64));
+            HIPCHK(ctx, hipMemsetAsync(ctx->stamps.p, 0, size_t(P.total_tiles) * 64, s));
+            b.stamps = static_cast<unsigned long long*>(ctx->stamps.p);
+        }
         b.fancy = fancy ? 1u : 0u;
         b.max_fancy_wgs = max_fancy_wgs;
 
@@ -952,7 +957,7 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_brk, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output,
-                       &ctx->comp, &ctx->planes})
+                       &ctx->comp, &ctx->planes, &ctx->stamps})
         if (b->p) (void)hipFree(b->p);
     if (ctx->input_host.p) (void)hipHostFree(ctx->input_host.p);
     for (Pending& pd : ctx->pend) {
@@ -1171,6 +1176,7 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
         case 12: src = b.piece_mcu0; n = size_t(b.nsub) * 4; break;
         case 13: src = b.piece_ent0; n = size_t(b.nsub) * 4; break;
         case 14: src = b.piece_cp; n = size_t(b.nsub) * kCpRecords * sizeof(CpRec); break;
+        case 15: src = b.stamps; n = b.stamps ? size_t(b.total_tiles) * 64 : 0; break;
         default: return JD_ERR_INVALID_ARG;
     }
     *nbytes = n;

@@ -378,7 +378,7 @@ class Decoder:
                     "piece_end": (6, np.uint32, 1), "piece_nmcu": (7, np.uint32, 1), "piece_nent": (8, np.uint32, 1),
                     "sub_seg": (9, np.uint32, 1), "status": (10, np.uint32, 1), "entries": (11, np.uint32, 1),
                     "piece_mcu0": (12, np.uint32, 1), "piece_ent0": (13, np.uint32, 1),
-                    "piece_cp": (14, np.uint32, 36)}
+                    "piece_cp": (14, np.uint32, 36), "stamps": (15, np.uint64, 8)}
 
     def debug_fetch(self, name: str) -> np.ndarray:
         """Internal array of the most recent batch (white-box tests and debugging)."""
