@@ -242,6 +242,10 @@ struct BatchDev {
                                   // of components 0..2 at the tile's first block
     // fancy upsampling (JD_FLAG_FANCY_UPSAMPLING): k_idct_color writes component planes to HBM
     // (ImgDesc::planes), k_colour_fancy filters and colours them
+    // k_idct_color<M>: the batch's images of each sampling layout (kModeGen, kMode420, kMode422,
+    // kMode444 in jd_kernels.hip): mode_imgs[mode_off[m] .. + mode_cnt[m]), at most mode_max_tiles[m] tiles
+    const uint32_t* mode_imgs;
+    uint32_t mode_off[4], mode_cnt[4], mode_max_tiles[4];
     unsigned long long* stamps;   // diagnostic builds (JD_STAMP): 8 s_memtime stamps per IDCT tile, else null
     uint32_t fancy;
     uint32_t max_fancy_wgs;       // k_colour_fancy workgroups per image (grid x)

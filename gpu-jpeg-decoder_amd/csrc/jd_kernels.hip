@@ -1283,14 +1283,60 @@ __device__ __forceinline__ uint32_t div_small(uint32_t x, uint32_t magic) { retu
 // MCUs in (g0 % DRI computed once per wave), the others every DRI MCUs after it.
 struct TileGeo {
     uint32_t m0, nm, g0;  // first MCU column, MCUs in the tile, raster index of its first MCU
+    uint32_t ty;          // MCU row of the tile
     uint32_t ri, ms;      // restart interval (0: none) and the first interval start (>= 64: none)
     uint32_t ri_magic;    // magic16(ri) when 0 < ri < tile_mcus (several starts), else 0
 };
+
+// Sampling layouts k_idct_color is specialised for (compile-time block pattern, tile width, plane
+// geometry and colour mode); every other layout takes the generic instance, which reads them from
+// the ImgDesc.  The host (jd_runtime.cpp image_mode) classifies each image the same way and its
+// tile choice (tile_mcus = kTileMaxBlocks / bpm) matches tm below.
+constexpr int kModeGen = 0, kMode420 = 1, kMode422 = 2, kMode444 = 3;
+template <int M>
+struct TMode {  // generic: from the image descriptor
+    static constexpr bool kFixed = false;
+    __device__ static uint32_t bpm(const ImgDesc& im) { return im.bpm; }
+    __device__ static uint32_t tm(const ImgDesc& im) { return im.tile_mcus; }
+    __device__ static uint32_t pattern(const ImgDesc& im) { return im.block_pattern; }
+    __device__ static uint32_t ncomp(const ImgDesc& im) { return im.ncomp; }
+    __device__ static uint32_t h(const ImgDesc& im, uint32_t c) { return im.h[c]; }
+    __device__ static uint32_t v(const ImgDesc& im, uint32_t c) { return im.v[c]; }
+    __device__ static uint32_t cb0(const ImgDesc& im, uint32_t c) { return im.comp_block0[c]; }
+    __device__ static uint32_t shx(const ImgDesc& im, uint32_t c) { return im.shx[c]; }
+    __device__ static uint32_t shy(const ImgDesc& im, uint32_t c) { return im.shy[c]; }
+    __device__ static uint32_t lg_mw(const ImgDesc& im) { return im.lg_mw; }
+    __device__ static uint32_t lg_mh(const ImgDesc& im) { return im.lg_mh; }
+};
+// H1 x V1 luma blocks, one Cb and one Cr block per MCU
+template <uint32_t H1, uint32_t V1>
+struct TModeYcc {
+    static constexpr bool kFixed = true;
+    static constexpr uint32_t kBpm = H1 * V1 + 2;
+    __device__ static constexpr uint32_t bpm(const ImgDesc&) { return kBpm; }
+    __device__ static constexpr uint32_t tm(const ImgDesc&) { return uint32_t(kTileMaxBlocks) / kBpm; }
+    __device__ static constexpr uint32_t pattern(const ImgDesc&) { return (1u << (2 * H1 * V1)) | (2u << (2 * H1 * V1 + 2)); }
+    __device__ static constexpr uint32_t ncomp(const ImgDesc&) { return 3; }
+    __device__ static constexpr uint32_t h(const ImgDesc&, uint32_t c) { return c == 0 ? H1 : 1u; }
+    __device__ static constexpr uint32_t v(const ImgDesc&, uint32_t c) { return c == 0 ? V1 : 1u; }
+    __device__ static constexpr uint32_t cb0(const ImgDesc&, uint32_t c) { return c == 0 ? 0u : H1 * V1 + c - 1; }
+    __device__ static constexpr uint32_t shx(const ImgDesc&, uint32_t c) { return c == 0 ? 0u : (H1 == 2 ? 1u : 0u); }
+    __device__ static constexpr uint32_t shy(const ImgDesc&, uint32_t c) { return c == 0 ? 0u : (V1 == 2 ? 1u : 0u); }
+    __device__ static constexpr uint32_t lg_mw(const ImgDesc&) { return H1 == 2 ? 4u : 3u; }
+    __device__ static constexpr uint32_t lg_mh(const ImgDesc&) { return V1 == 2 ? 4u : 3u; }
+};
+template <> struct TMode<kMode420> : TModeYcc<2, 2> {};
+template <> struct TMode<kMode422> : TModeYcc<2, 1> {};
+template <> struct TMode<kMode444> : TModeYcc<1, 1> {};
+
+template <int M = kModeGen>
 __device__ __forceinline__ TileGeo tile_geo(const ImgDesc& im, uint32_t tile) {
     TileGeo G;
+    const uint32_t TM = TMode<M>::tm(im);
     const uint32_t ty = tile / im.tiles_x, tx = tile - ty * im.tiles_x;
-    G.m0 = tx * im.tile_mcus;
-    G.nm = min(im.tile_mcus, im.mcux - G.m0);
+    G.ty = ty;
+    G.m0 = tx * TM;
+    G.nm = min(TM, im.mcux - G.m0);
     G.g0 = ty * im.mcux + G.m0;
     G.ri = im.restart_interval;
     if (G.ri) {
@@ -1299,7 +1345,7 @@ __device__ __forceinline__ TileGeo tile_geo(const ImgDesc& im, uint32_t tile) {
     } else {
         G.ms = G.g0 == 0 ? 0u : 64u;
     }
-    G.ri_magic = (G.ri && G.ri < im.tile_mcus) ? magic16(G.ri) : 0u;
+    G.ri_magic = (G.ri && G.ri < TM) ? magic16(G.ri) : 0u;
     return G;
 }
 // MCU m of the tile (m < 64) starts an interval
@@ -1894,18 +1940,21 @@ struct TileLaneGeo {
     uint32_t m, bb, comp;
     bool have;
 };
+template <int M = kModeGen>
 __device__ __forceinline__ TileLaneGeo tile_lane_geo(const ImgDesc& im, const TileGeo& G, uint32_t lane) {
     TileLaneGeo L;
-    L.m = div_small(lane, magic16(im.bpm));
-    L.bb = lane - L.m * im.bpm;
+    const uint32_t bpm = TMode<M>::bpm(im);
+    L.m = TMode<M>::kFixed ? lane / bpm : div_small(lane, magic16(bpm));
+    L.bb = lane - L.m * bpm;
     L.have = L.m < G.nm;
-    L.comp = (im.block_pattern >> (2 * L.bb)) & 3u;
+    L.comp = (TMode<M>::pattern(im) >> (2 * L.bb)) & 3u;
     return L;
 }
 
+template <int M = kModeGen>
 __device__ __forceinline__ BlockInfo load_block_info(const BatchDev& b, const ImgDesc& im, const TileGeo& G,
                                                      const TileLaneGeo& L) {
-    return L.have ? b.blocks[im.block_base + uint64_t(G.g0 + L.m) * im.bpm + L.bb] : BlockInfo{0u, 0u};
+    return L.have ? b.blocks[im.block_base + uint64_t(G.g0 + L.m) * TMode<M>::bpm(im) + L.bb] : BlockInfo{0u, 0u};
 }
 
 // The lane's AC entries: [first, first + cnt) of the image's entry array, read as 16-byte quads
@@ -2011,13 +2060,14 @@ __device__ __forceinline__ void zero_staging(uint32_t* s_buf, uint32_t lane) {
 //  * EXACT = false (k_idct_color): a wave with a coefficient beyond the fast IDCT's range (never
 //    seen in real images) appends its tile to slow_tiles and returns false;
 //  * EXACT = true (k_idct_color_exact) decodes those tiles with the exact IDCT form.
-template <bool EXACT, class Mid>
+template <bool EXACT, int M, class Mid>
 __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDesc& im, uint32_t img, uint32_t tile,
                                                  const TileGeo& G, const TileLaneGeo& L, int dc_pred,
                                                  uint32_t* s_buf, const int* s_qz, Mid&& mid) {
     const uint32_t lane = threadIdx.x;
-    const uint32_t TM = im.tile_mcus, nc = im.ncomp;
-    const uint32_t m0 = G.m0, r0 = G.g0 / im.mcux;
+    using TM_ = TMode<M>;
+    const uint32_t TM = TM_::tm(im), nc = TM_::ncomp(im);
+    const uint32_t m0 = G.m0, r0 = G.ty;
     const uint32_t mi = L.m, mr = 0, bb = L.bb, comp = L.comp;
     const bool have = L.have;
     // dequantise in zig-zag order (24-bit multiplies: |coef| < 2^15, q < 2^16) into natural
@@ -2076,8 +2126,8 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
     mid();  // (k_idct_color: the next tile's entry loads, issued here so they are not live across the IDCT)
     if (b.fancy) {  // wave-uniform: component planes to HBM, k_colour_fancy takes it from there
         if (have) {
-            const uint32_t hc = im.h[comp], vc = im.v[comp];
-            const uint32_t t = bb - im.comp_block0[comp];
+            const uint32_t hc = TM_::h(im, comp), vc = TM_::v(im, comp);
+            const uint32_t t = bb - TM_::cb0(im, comp);
             const uint32_t tyb = t >> __builtin_ctz(hc), txb = t - tyb * hc;  // hc in {1, 2, 4}
             int16_t* dst = reinterpret_cast<int16_t*>(im.planes) + fancy_plane_off(im, comp) +
                            size_t(((r0 + mr) * vc + tyb) * 8) * (im.mcux * hc * 8) + ((m0 + mi) * hc + txb) * 8;
@@ -2103,19 +2153,19 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             if (uint32_t(c) < nc) {
-                ppitch[c] = TM * im.h[c] * 8;
+                ppitch[c] = TM * TM_::h(im, c) * 8;
                 pbase[c] = off;
-                off += ppitch[c] * im.v[c] * 8;  // one MCU row
+                off += ppitch[c] * TM_::v(im, c) * 8;  // one MCU row
             }
         }
     }
     if (have) {
-        const uint32_t hc = im.h[comp];
-        const uint32_t t = bb - im.comp_block0[comp];
+        const uint32_t hc = TM_::h(im, comp);
+        const uint32_t t = bb - TM_::cb0(im, comp);
         const uint32_t tyb = t >> __builtin_ctz(hc), txb = t - tyb * hc;  // hc in {1, 2, 4}
         const uint32_t pitch = comp == 0 ? ppitch[0] : (comp == 1 ? ppitch[1] : ppitch[2]);
         const uint32_t base = comp == 0 ? pbase[0] : (comp == 1 ? pbase[1] : pbase[2]);
-        int16_t* dst = s_pl + base + ((mr * im.v[comp] + tyb) * 8) * pitch + (mi * hc + txb) * 8;
+        int16_t* dst = s_pl + base + ((mr * TM_::v(im, comp) + tyb) * 8) * pitch + (mi * hc + txb) * 8;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             uint4 q;
@@ -2130,12 +2180,12 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
 
     // upsample + colour: 8 pixels of one row per lane-step, or of two rows when both chroma
     // planes are vertically subsampled (the two rows share their chroma samples and terms)
-    const uint32_t lg_mw = im.lg_mw, lg_mh = im.lg_mh;
+    const uint32_t lg_mw = TM_::lg_mw(im), lg_mh = TM_::lg_mh(im);
     const uint32_t gpr = (TM << lg_mw) >> 3;  // 8-pixel groups per tile row
     const uint32_t th = 1u << lg_mh;
     const uint32_t W = im.width, H = im.height;
     const uint32_t x_tile = m0 << lg_mw, y_tile = r0 << lg_mh;
-    const uint32_t shx1 = im.shx[1], shy1 = im.shy[1], shx2 = im.shx[2], shy2 = im.shy[2];
+    const uint32_t shx1 = TM_::shx(im, 1), shy1 = TM_::shy(im, 1), shx2 = TM_::shx(im, 2), shy2 = TM_::shy(im, 2);
     const uint32_t cmode = nc == 1 ? 3u : (shx1 == shx2 ? shx1 : 4u);
     const bool pair = cmode <= 2u && shy1 >= 1u && shy2 >= 1u;  // wave-uniform; th is even then
     const uint32_t rows = pair ? 2u : 1u, ngy = th / rows;
@@ -2229,17 +2279,18 @@ __device__ __forceinline__ DcPred load_dcpred(const BatchDev& b, const ImgDesc& 
         if (JD_STAMP && b.stamps && lane == 0) b.stamps[size_t(im.tile_base + tile) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// One wave per tile (grid: tiles x images).
+// One wave per tile; grid: tiles x the batch's images of sampling layout M (b.mode_imgs).
+template <int M>
 __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
     __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
-    const uint32_t lane = threadIdx.x, img = blockIdx.y, tile = blockIdx.x;
+    const uint32_t lane = threadIdx.x, img = b.mode_imgs[b.mode_off[M] + blockIdx.y], tile = blockIdx.x;
     const ImgDesc& im = b.imgs[img];
     if (tile >= im.tiles_x * im.tiles_y) return;
     JD_STAMP_AT(0);
-    const TileGeo G = tile_geo(im, tile);
-    const TileLaneGeo L = tile_lane_geo(im, G, lane);
-    const BlockInfo bi = load_block_info(b, im, G, L);
+    const TileGeo G = tile_geo<M>(im, tile);
+    const TileLaneGeo L = tile_lane_geo<M>(im, G, lane);
+    const BlockInfo bi = load_block_info<M>(b, im, G, L);
     const DcPred dcin = load_dcpred(b, im, tile);
     stage_quant(b, im, s_qz, lane);
     zero_staging(s_buf, lane);
@@ -2252,7 +2303,7 @@ __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDe
     scatter_entries(s_buf, staging_base(lane), R, E);
     __syncthreads();
     JD_STAMP_AT(2);
-    idct_colour_tile<false>(b, im, img, tile, G, L, dc_pred, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
+    idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
     JD_STAMP_AT(4);
 }
 
@@ -2279,7 +2330,7 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
         load_entry_quads(R, E);
         scatter_entries(s_buf, staging_base(lane), R, E);
         __syncthreads();
-        idct_colour_tile<true>(b, im, tr.img, tr.tile, G, L, dc_pred, s_buf, s_qz, [] {});
+        idct_colour_tile<true, kModeGen>(b, im, tr.img, tr.tile, G, L, dc_pred, s_buf, s_qz, [] {});
     }
 }
 
@@ -2432,7 +2483,15 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             break;
         case 9:
             if (!b.max_tiles) break;
-            hipLaunchKernelGGL(k_idct_color, dim3(b.max_tiles, b.nimg), dim3(kIdctThreads), 0, s, b);
+            // one launch per sampling layout present in the batch (k_idct_color<M> is specialised)
+            if (b.mode_cnt[kModeGen])
+                hipLaunchKernelGGL(k_idct_color<kModeGen>, dim3(b.mode_max_tiles[kModeGen], b.mode_cnt[kModeGen]), dim3(kIdctThreads), 0, s, b);
+            if (b.mode_cnt[kMode420])
+                hipLaunchKernelGGL(k_idct_color<kMode420>, dim3(b.mode_max_tiles[kMode420], b.mode_cnt[kMode420]), dim3(kIdctThreads), 0, s, b);
+            if (b.mode_cnt[kMode422])
+                hipLaunchKernelGGL(k_idct_color<kMode422>, dim3(b.mode_max_tiles[kMode422], b.mode_cnt[kMode422]), dim3(kIdctThreads), 0, s, b);
+            if (b.mode_cnt[kMode444])
+                hipLaunchKernelGGL(k_idct_color<kMode444>, dim3(b.mode_max_tiles[kMode444], b.mode_cnt[kMode444]), dim3(kIdctThreads), 0, s, b);
             hipLaunchKernelGGL(k_idct_color_exact, dim3(1024), dim3(kIdctThreads), 0, s, b);
             break;
         case 10:

@@ -264,7 +264,20 @@ struct Plan {
     uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0;
     uint64_t total_blocks = 0, total_entry_cap = 0, comp_bytes = 0;
     double pixels = 0, ecs_bytes = 0;
+    std::vector<uint32_t> mode_imgs;  // images grouped by sampling layout (k_idct_color<M>)
+    uint32_t mode_off[4] = {0, 0, 0, 0}, mode_cnt[4] = {0, 0, 0, 0}, mode_max_tiles[4] = {0, 0, 0, 0};
 };
+
+// Sampling layout of an image for k_idct_color's specialised instances (jd_kernels.hip TMode):
+// 1 = 4:2:0 (Y 2x2), 2 = 4:2:2 (Y 2x1), 3 = 4:4:4, each with one Cb and one Cr block per MCU in
+// frame order; 0 = anything else (generic instance).
+uint32_t image_mode(const ImgDesc& d) {
+    if (d.ncomp != 3 || d.h[1] != 1 || d.v[1] != 1 || d.h[2] != 1 || d.v[2] != 1) return 0;
+    if (d.h[0] == 2 && d.v[0] == 2) return 1;
+    if (d.h[0] == 2 && d.v[0] == 1) return 2;
+    if (d.h[0] == 1 && d.v[0] == 1) return 3;
+    return 0;
+}
 
 // Largest item prefix [lo, hi) whose sparse-coefficient slots stay within the context's
 // max_batch_entries (default kMaxBatchEntries; entry indices are image-relative, this only bounds
@@ -503,10 +516,20 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             }
         }
     });
-    for (ImgDesc& d : P.imgs) {
+    std::vector<uint32_t> by_mode[4];
+    for (size_t i = 0; i < P.imgs.size(); i++) {
+        ImgDesc& d = P.imgs[i];
         d.tile_base = P.total_tiles;
         P.total_tiles += d.tiles_x * d.tiles_y;
         P.max_tiles = std::max(P.max_tiles, d.tiles_x * d.tiles_y);
+        const uint32_t m = image_mode(d);
+        by_mode[m].push_back(uint32_t(i));
+        P.mode_max_tiles[m] = std::max(P.mode_max_tiles[m], d.tiles_x * d.tiles_y);
+    }
+    for (int m = 0; m < 4; m++) {
+        P.mode_off[m] = uint32_t(P.mode_imgs.size());
+        P.mode_cnt[m] = uint32_t(by_mode[m].size());
+        P.mode_imgs.insert(P.mode_imgs.end(), by_mode[m].begin(), by_mode[m].end());
     }
     const double tb_segs = tbms();
     // 3. piece slots: per image ceil(ECS bits / piece_bits) + nseg (interval lengths are only known
@@ -667,6 +690,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_wgts = put(blob, P.wg_tableset);
         const size_t o_chain = put(blob, P.chain_seg);
         const size_t o_chts = put(blob, P.chain_wg_tableset);
+        const size_t o_modes = put(blob, P.mode_imgs);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
         const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // entries, slow tiles, IDCT queue
         const size_t upload = blob.size();
@@ -743,6 +767,12 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
         b.max_tiles = P.max_tiles;
+        b.mode_imgs = reinterpret_cast<const uint32_t*>(base + o_modes);
+        for (int m = 0; m < 4; m++) {
+            b.mode_off[m] = P.mode_off[m];
+            b.mode_cnt[m] = P.mode_cnt[m];
+            b.mode_max_tiles[m] = P.mode_max_tiles[m];
+        }
         if (std::getenv("JD_STAMPS")) {  // diagnostic builds (JD_STAMP): per-tile phase stamps
             HIPCHK(ctx, ensure_dev(ctx->stamps, size_t(P.total_tiles) * 64));
             HIPCHK(ctx, hipMemsetAsync(ctx->stamps.p, 0, size_t(P.total_tiles) * 64, s));
