@@ -39,6 +39,7 @@ constexpr uint8_t kNatOfZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 typedef __attribute__((address_space(1))) const uint8_t gu8;
 // Output pointers as global (not flat) addresses: a flat store also counts on lgkmcnt, so every
@@ -1545,37 +1546,6 @@ __device__ __forceinline__ void idct_col(int* blk) {
 //
 // k_idct_color takes the fast form when every lane of the wave is in range (wave-uniform), which
 // real images always are; tests/test_gpu.py::test_idct_kat covers both over int32 inputs.
-__device__ __forceinline__ void idct_row_fast(int* blk) {
-    const int x1 = blk[4] << 11, x0 = (blk[0] << 11) + 128;
-    const int b1 = blk[1], b2 = blk[2], b3 = blk[3], b5 = blk[5], b6 = blk[6], b7 = blk[7];
-    int x4 = __mul24(b1, kC1) + __mul24(b7, kC7);
-    int x5 = __mul24(b1, kC7) + __mul24(b7, -kC1);
-    int x6 = __mul24(b5, kC5) + __mul24(b3, kC3);
-    int x7 = __mul24(b5, kC3) + __mul24(b3, -kC5);
-    int x2 = __mul24(b2, kC6) + __mul24(b6, -kC2);
-    int x3 = __mul24(b2, kC2) + __mul24(b6, kC6);
-    int x8 = x0 + x1;
-    int y0 = x0 - x1;
-    const int y1 = x4 + x6;
-    x4 -= x6;
-    x6 = x5 + x7;
-    x5 -= x7;
-    x7 = x8 + x3;
-    x8 -= x3;
-    x3 = y0 + x2;
-    y0 -= x2;
-    x2 = (181 * (x4 + x5) + 128) >> 8;
-    x4 = (181 * (x4 - x5) + 128) >> 8;
-    blk[0] = (x7 + y1) >> 8;
-    blk[1] = (x3 + x2) >> 8;
-    blk[2] = (y0 + x4) >> 8;
-    blk[3] = (x8 + x6) >> 8;
-    blk[4] = (x8 - x6) >> 8;
-    blk[5] = (y0 - x4) >> 8;
-    blk[6] = (x3 - x2) >> 8;
-    blk[7] = (x7 - y1) >> 8;
-}
-
 __device__ __forceinline__ void idct_col_fast(int* blk) {
     const int x1 = blk[8 * 4] << 8, x0 = (blk[0] << 8) + 8192;
     const int b1 = blk[8 * 1], b2 = blk[8 * 2], b3 = blk[8 * 3], b5 = blk[8 * 5], b6 = blk[8 * 6], b7 = blk[8 * 7];
@@ -1624,21 +1594,73 @@ __device__ __forceinline__ void idct_col_exact(int* blk) {
     for (int k = 0; k < 8; k++) blk[8 * k] = dc_only ? s : blk[8 * k];
 }
 
-// Both forms on a block of dequantised coefficients in natural order (blk[0] = DC); fast when
-// the caller knows every coefficient is within +-2^16.  The decode path instantiates them in
-// different kernels (k_idct_color / k_idct_color_exact): together they would make it spill.
-__device__ __forceinline__ void idct_block(int (&blk)[64], bool fast) {
-    if (fast) {
+// The exact form on a block of dequantised coefficients in natural order (blk[0] = DC).
+__device__ __forceinline__ void idct_block_exact(int (&blk)[64]) {
 #pragma unroll
-        for (int r = 0; r < 8; r++) idct_row_fast(blk + 8 * r);
+    for (int r = 0; r < 8; r++) idct_row_exact(blk + 8 * r);
 #pragma unroll
-        for (int c = 0; c < 8; c++) idct_col_fast(blk + c);
-    } else {
-#pragma unroll
-        for (int r = 0; r < 8; r++) idct_row_exact(blk + 8 * r);
-#pragma unroll
-        for (int c = 0; c < 8; c++) idct_col_exact(blk + c);
+    for (int c = 0; c < 8; c++) idct_col_exact(blk + c);
+}
+
+// The fast form when every dequantised coefficient fits int16 (k_idct_color's range test).  The
+// row pass multiplies int16 pairs by constant pairs with v_dot2_i32_i16 (one instruction per pair
+// of products: C1 b1 + C7 b7 = C7 (b1 + b7) + (C1 - C7) b1 and so on, equal in int32), its x0 +- x1
+// terms included ((b0 << 11) + 128 +- (b4 << 11) = 2048 b0 +- 2048 b4 + 128); the inputs stay the
+// zig-zag-ordered packed words the dequantisation produced (v_pk_mul_lo_u16), each natural pair
+// picked by one v_perm_b32.  The column pass is the 24-bit one (row outputs stay within +-2^23).
+struct ZzOfNat {  // zig-zag index of each natural position (inverse of kNatOfZz)
+    uint8_t v[64];
+    constexpr ZzOfNat() : v() {
+        for (int z = 0; z < 64; z++) v[kNatOfZz[z]] = uint8_t(z);
     }
+};
+constexpr ZzOfNat kZzOfNat{};
+constexpr uint32_t pk16(int lo, int hi) { return (uint32_t(lo) & 0xFFFFu) | (uint32_t(hi) << 16); }
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t k, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, k), c, false);
+}
+// (natural n_lo, natural n_hi) as one int16 pair from the zig-zag pair words dw
+__device__ __forceinline__ uint32_t nat_pair(const uint32_t (&dw)[32], int n_lo, int n_hi) {
+    const int zl = kZzOfNat.v[n_lo], zh = kZzOfNat.v[n_hi];
+    const uint32_t sel = uint32_t(2 * (zl & 1)) | (uint32_t(2 * (zl & 1) + 1) << 8) | (uint32_t(4 + 2 * (zh & 1)) << 16) |
+                         (uint32_t(5 + 2 * (zh & 1)) << 24);
+    return __builtin_amdgcn_perm(dw[zh >> 1], dw[zl >> 1], sel);
+}
+__device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, int* out) {
+    const uint32_t P0 = nat_pair(dw, 8 * r + 0, 8 * r + 4), P1 = nat_pair(dw, 8 * r + 1, 8 * r + 7);
+    const uint32_t P2 = nat_pair(dw, 8 * r + 5, 8 * r + 3), P3 = nat_pair(dw, 8 * r + 2, 8 * r + 6);
+    int x8 = dot2(P0, pk16(2048, 2048), 128);
+    int y0 = dot2(P0, pk16(2048, -2048), 128);
+    int x4 = dot2(P1, pk16(kC1, kC7), 0);
+    int x5 = dot2(P1, pk16(kC7, -kC1), 0);
+    int x6 = dot2(P2, pk16(kC5, kC3), 0);
+    int x7 = dot2(P2, pk16(kC3, -kC5), 0);
+    int x2 = dot2(P3, pk16(kC6, -kC2), 0);
+    int x3 = dot2(P3, pk16(kC2, kC6), 0);
+    const int y1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = y0 + x2;
+    y0 -= x2;
+    x2 = (181 * (x4 + x5) + 128) >> 8;
+    x4 = (181 * (x4 - x5) + 128) >> 8;
+    out[0] = (x7 + y1) >> 8;
+    out[1] = (x3 + x2) >> 8;
+    out[2] = (y0 + x4) >> 8;
+    out[3] = (x8 + x6) >> 8;
+    out[4] = (x8 - x6) >> 8;
+    out[5] = (y0 - x4) >> 8;
+    out[6] = (x3 - x2) >> 8;
+    out[7] = (x7 - y1) >> 8;
+}
+__device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], int (&blk)[64]) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) idct_row_dot2(dw, r, blk + 8 * r);
+#pragma unroll
+    for (int c = 0; c < 8; c++) idct_col_fast(blk + c);
 }
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
@@ -1661,16 +1683,16 @@ struct ChromaTerms {
     int r, b, g;
     bool exact;
 };
-// The three floors in float (full-rate conversions and multiplies instead of 32-bit mul_hi):
-// R and B as floor((2m + 1) / 2000) with m < 2^20, at least 1/4000 from an integer, where the
-// float error is < 1.1e-7 relative; G's quotient from float(n) / 587000 (|n| < 2^28, error
-// < 5e-5), its remainder exact in integers.  Equal to the integer definition above for every
-// (cb, cr) in [-256, 255]^2 (tests/test_oracle.py::test_chroma_terms_float_exhaustive, and the
-// GPU's all-2^27 test_color_exhaustive).
+// R and B as one 24-bit multiply-add and a shift each: floor(1402 cr / 1000) + 128 =
+// (91881 cr + 128 * 2^16) >> 16 and floor(1772 cb / 1000) + 128 = (58065 cb + 128 * 2^15 + 32) >> 15
+// for every cr, cb in [-256, 255] (magic constants found by exhaustive search; the products stay
+// below 2^31).  G's quotient from float(n) / 587000 (|n| < 2^28, error < 5e-5), its remainder exact
+// in integers.  Equal to the integer definitions above for every (cb, cr) in [-256, 255]^2
+// (tests/test_oracle.py::test_chroma_terms_exhaustive, and the GPU's all-2^27 test_color_exhaustive).
 __device__ __forceinline__ ChromaTerms chroma_terms(int cb, int cr) {
     ChromaTerms t;
-    t.r = int(floorf(float(__mul24(cr, 2804) + 718001) * 0.0005f)) - 359 + 128;
-    t.b = int(floorf(float(__mul24(cb, 3544) + 908001) * 0.0005f)) - 454 + 128;
+    t.r = (__mul24(cr, 91881) + (128 << 16)) >> 16;
+    t.b = (__mul24(cb, 58065) + (128 << 15) + 32) >> 15;
     const int n = __mul24(cb, 202008) + __mul24(cr, 419198);
     const int q = int(floorf(float(n) * (1.0f / 587000.0f)));
     const int rem = n - __mul24(q, 587000);
@@ -1802,14 +1824,14 @@ __device__ __forceinline__ void colour16(const int (&Y0)[8], const int (&Y1)[8],
 // v_pk_add / v_pk_max / v_pk_min (3 VALU per two pixels and channel), then v_perm byte shuffles
 // into RGB order.  Taken when no chroma sample of the wave's lane-step needs the reference's
 // double-precision G (ChromaTerms::exact, about 2e-4 of the samples).
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_clamp_add(uint32_t y, uint32_t t) {
-    s16x2 r = __builtin_bit_cast(s16x2, y) + __builtin_bit_cast(s16x2, t);
-    r = __builtin_elementwise_max(r, (s16x2){0, 0});
-    r = __builtin_elementwise_min(r, (s16x2){255, 255});
-    return __builtin_bit_cast(uint32_t, r);
+// clamp(y + t, 0, 255) of two int16 lanes, as two bytes in the low half (v_sat_pk_u8_i16)
+__device__ __forceinline__ uint32_t pk_add_sat_u8(uint32_t y, uint32_t t) {
+    const s16x2 r = __builtin_bit_cast(s16x2, y) + __builtin_bit_cast(s16x2, t);  // |y + t| < 2^15
+    uint32_t o;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(o) : "v"(__builtin_bit_cast(uint32_t, r)));
+    return o;
 }
-__device__ __forceinline__ uint32_t pair16(int lo, int hi) { return (uint32_t(lo) & 0xFFFFu) | (uint32_t(hi) << 16); }
+__device__ __forceinline__ uint32_t pair16(int lo, int hi) { return __builtin_amdgcn_perm(uint32_t(hi), uint32_t(lo), 0x05040100u); }
 
 // Terms of the 8 >> SH chroma samples under 8 pixels as per-word pairs (word u = pixels 2u, 2u+1).
 // Returns the mask of samples (bit u) whose G needs the reference's double-precision path.
@@ -1856,24 +1878,25 @@ __device__ __forceinline__ void fix_g_exact(const uint4& Yq, const int16_t* s_pl
     }
 }
 
-// 8 pixels of one row: Y as 4 words of int16 pairs -> 24 RGB bytes in 6 words (pack24's order).
+// 8 pixels of one row: Y as 4 words of int16 pairs -> 24 RGB bytes in 6 words (pack24's order):
+// per pixel pair and channel one packed add and one saturating pack to bytes, then byte shuffles.
 __device__ __forceinline__ void row_rgb_packed(const uint4& Yq, const uint32_t (&TR)[4], const uint32_t (&TG)[4],
                                                const uint32_t (&TB)[4], uint32_t (&w)[6]) {
     const uint32_t Y[4] = {Yq.x, Yq.y, Yq.z, Yq.w};
-    uint32_t RG[4], B[4];
+    uint32_t RG[4], B[4];  // RG: r0 g0 r1 g1; B: b0 b1 in the low half
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-        const uint32_t r = pk_clamp_add(Y[u], TR[u]), g = pk_clamp_add(Y[u], TG[u]);
-        B[u] = pk_clamp_add(Y[u], TB[u]);
-        RG[u] = __builtin_amdgcn_perm(g, r, 0x06020400u);  // r0 g0 r1 g1
+        const uint32_t r = pk_add_sat_u8(Y[u], TR[u]), g = pk_add_sat_u8(Y[u], TG[u]);
+        B[u] = pk_add_sat_u8(Y[u], TB[u]);
+        RG[u] = __builtin_amdgcn_perm(g, r, 0x05010400u);
     }
     // perm(hi, lo, sel): selector bytes 0-3 take lo's bytes, 4-7 hi's, 0x0c a zero byte
     w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x02040100u);                                            // r0 g0 b0 r1
-    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0603u), 0x05040100u);  // g1 b1 r2 g2
-    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x06030204u);                                            // b2 r3 g3 b3
+    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0503u), 0x05040100u);  // g1 b1 r2 g2
+    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x05030204u);                                            // b2 r3 g3 b3
     w[3] = __builtin_amdgcn_perm(B[2], RG[2], 0x02040100u);                                            // r4 g4 b4 r5
-    w[4] = __builtin_amdgcn_perm(RG[3], __builtin_amdgcn_perm(B[2], RG[2], 0x0c0c0603u), 0x05040100u);  // g5 b5 r6 g6
-    w[5] = __builtin_amdgcn_perm(B[3], RG[3], 0x06030204u);                                            // b6 r7 g7 b7
+    w[4] = __builtin_amdgcn_perm(RG[3], __builtin_amdgcn_perm(B[2], RG[2], 0x0c0c0503u), 0x05040100u);  // g5 b5 r6 g6
+    w[5] = __builtin_amdgcn_perm(B[3], RG[3], 0x05030204u);                                            // b6 r7 g7 b7
 }
 
 // One wave per tile of tile_mcus x tile_mrows MCUs (host-chosen, <= 64 blocks):
@@ -2097,7 +2120,7 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             const uint32_t w = rw[p];
             acc |= w ^ (w << 1);
         }
-        const bool in_range = !have || ((acc & im.qmask) == 0 && uint32_t(dq0 + 65536) <= 131072u);
+        const bool in_range = !have || ((acc & im.qmask) == 0 && uint32_t(dq0 + 32768) <= 65535u);
         if (!__all(in_range)) {  // wave-uniform
             if (lane == 0) {
                 const uint32_t k = uint32_t(atomicAdd(&b.counters[1], 1ull));
@@ -2108,21 +2131,37 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         }
     }
     int blk[64];
+    if (!EXACT) {
+        // every dequantised coefficient fits int16: packed multiplies in zig-zag order, DC in place
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        uint32_t dw[32];
 #pragma unroll
-    for (int p4 = 0; p4 < 8; p4++) {
-        const uint4 qv = qz4[p4];
-        const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+        for (int p4 = 0; p4 < 8; p4++) {
+            const uint4 qv = qz4[p4];
+            const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int p = 4 * p4 + k;
-            const uint32_t w = rw[p];
-            blk[kNatOfZz[2 * p]] = p == 0 ? dq0 : __mul24(int(int16_t(w & 0xFFFFu)), int(qw[k] & 0xFFFFu));
-            blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, int(qw[k] >> 16));
+            for (int k = 0; k < 4; k++)
+                dw[4 * p4 + k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, rw[4 * p4 + k]) * __builtin_bit_cast(u16x2, qw[k]));
         }
-    }
+        dw[0] = __builtin_amdgcn_perm(dw[0], uint32_t(dq0), 0x07060100u);
 #if !(JD_ABL & 2)
-    idct_block(blk, !EXACT);
+        idct_block_dot2(dw, blk);
 #endif
+    } else {
+#pragma unroll
+        for (int p4 = 0; p4 < 8; p4++) {
+            const uint4 qv = qz4[p4];
+            const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int p = 4 * p4 + k;
+                const uint32_t w = rw[p];
+                blk[kNatOfZz[2 * p]] = p == 0 ? dq0 : __mul24(int(int16_t(w & 0xFFFFu)), int(qw[k] & 0xFFFFu));
+                blk[kNatOfZz[2 * p + 1]] = __mul24(int32_t(w) >> 16, int(qw[k] >> 16));
+            }
+        }
+        idct_block_exact(blk);
+    }
     mid();  // (k_idct_color: the next tile's entry loads, issued here so they are not live across the IDCT)
     if (b.fancy) {  // wave-uniform: component planes to HBM, k_colour_fancy takes it from there
         if (have) {
@@ -2408,19 +2447,23 @@ __global__ __launch_bounds__(256) void k_colour_fancy(BatchDev b) {
 // ------------------------------------------------------------------------------------------
 // Known-answer hooks
 // ------------------------------------------------------------------------------------------
-// exact_only = 0: the decode path's choice per block (fast form when every input is within
-// +-2^16); 1: the exact form whatever the inputs.
+// exact_only = 0: the decode path's choice per block (the int16 fast form when every input fits
+// int16, else the exact form); 1: the exact form whatever the inputs.
 __global__ void k_test_idct(const int32_t* in_zz, int32_t* out, int n, int exact_only) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int blk[64];
     bool in_range = !exact_only;
+    uint32_t dw[32];
 #pragma unroll
     for (int z = 0; z < 64; z++) {
-        blk[kNatOfZz[z]] = in_zz[size_t(i) * 64 + z];
-        in_range = in_range && uint32_t(blk[kNatOfZz[z]] + 65536) <= 131072u;
+        const int v = in_zz[size_t(i) * 64 + z];
+        blk[kNatOfZz[z]] = v;
+        in_range = in_range && uint32_t(v + 32768) <= 65535u;
+        if (z & 1) dw[z >> 1] = pk16(blk[kNatOfZz[z - 1]], v);
     }
-    idct_block(blk, in_range);
+    if (in_range) idct_block_dot2(dw, blk);
+    else idct_block_exact(blk);
 #pragma unroll
     for (int z = 0; z < 64; z++) out[size_t(i) * 64 + z] = blk[z];
 }

@@ -330,12 +330,12 @@ void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uin
         for (int j = 0; j < h.h[c] * h.v[c]; j++, b++) pat |= uint32_t(c) << (2 * b);
         d.qslot[c] = pi.qslot[c];
     }
-    {  // k_idct_color's fast-IDCT range test: |c| <= 2^(k-1) keeps |c * step| < 2^16
+    {  // k_idct_color's fast-IDCT range test: |c| <= 2^(k-1) keeps |c * step| < 2^15 (int16)
         uint32_t qmax = 1;
         for (int c = 0; c < h.ncomp; c++)
             for (int k = 0; k < 64; k++) qmax = std::max<uint32_t>(qmax, pj.q[h.tq[c]][k]);
         uint32_t k = 1;
-        while (k < 16 && (uint64_t(1) << k) * qmax < 65536) k++;  // largest k: 2^(k-1) * qmax < 2^16
+        while (k < 16 && (uint64_t(1) << k) * qmax < 32768) k++;  // largest k: 2^(k-1) * qmax < 2^15
         const uint32_t lo = (0xFFFFu << k) & 0xFFFFu;
         d.qmask = lo | (lo << 16);
     }

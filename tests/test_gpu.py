@@ -145,6 +145,10 @@ def test_idct_kat(decoder):
         sp[k, idx] = rng.integers(-1024, 1024, n) * rng.integers(1, 40, n)
     blocks.append(sp)
     blocks.append(rng.integers(-2048, 2048, (20000, 64), dtype=np.int32))
+    # the int16 fast form's corners (v_dot2_i32_i16 row pass: every input within int16)
+    corner = np.where(rng.random((4096, 64)) < 0.5, 32767, -32768).astype(np.int32)
+    corner[2048:][rng.random((2048, 64)) < 0.7] = 0
+    blocks.append(corner)
     a = np.concatenate(blocks)
     got = decoder.test_idct(a)
     want = jdoracle.idct(a)
@@ -152,9 +156,10 @@ def test_idct_kat(decoder):
 
 
 def test_idct_both_forms_over_int32(decoder):
-    """The fast form (24-bit multiplies, taken when every input is within +-2^16) and the exact form
-    (the reference's formulas and DC-only shortcuts, any int32 input; the oracle wraps like the
-    GPU, -fwrapv) against the oracle, at and beyond the fast form's range."""
+    """The decode path's forms against the oracle, at and beyond the fast form's range: the fast form
+    (int16 dot2 row pass + 24-bit column pass, taken when every input fits int16) and the exact
+    form (the reference's formulas and DC-only shortcuts, any int32 input; the oracle wraps like the
+    GPU, -fwrapv)."""
     rng = np.random.default_rng(2)
     n = 40000
     edge = rng.integers(-65536, 65537, (n, 64)).astype(np.int32)          # fast form, dense

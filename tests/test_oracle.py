@@ -148,23 +148,25 @@ def test_idct_shortcuts_equal_branch_free():
     assert np.array_equal(got, want)
 
 
-def test_chroma_terms_float_exhaustive():
-    """k_idct_color's chroma terms (jd_kernels.hip chroma_terms) take their floors in float32:
-    floor((2m + 1) * 0.0005f) for R and B, floor(float(n) * (1 / 587000.0f)) for G.  Equal to
-    the integer definitions for every (cb, cr) in [-256, 255]^2 (IEEE float32 emulated in numpy)."""
+def test_chroma_terms_exhaustive():
+    """k_idct_color's chroma terms (jd_kernels.hip chroma_terms): R and B as one 24-bit
+    multiply-add and a shift, (91881 cr + 128 * 2^16) >> 16 and (58065 cb + 128 * 2^15 + 32) >> 15;
+    G's quotient as floor(float(n) * (1 / 587000.0f)) with an exact integer remainder.  Equal to the
+    integer definitions for every (cb, cr) in [-256, 255]^2 (IEEE float32 emulated in numpy)."""
     cb, cr = np.meshgrid(np.arange(-256, 256, dtype=np.int64), np.arange(-256, 256, dtype=np.int64), indexing="ij")
     cb, cr = cb.ravel(), cr.ravel()
     f32 = np.float32
-    tr_i = (1402 * cr + 359000) // 1000 - 359 + 128
-    tb_i = (1772 * cb + 454000) // 1000 - 454 + 128
+    tr_i = np.floor_divide(1402 * cr, 1000) + 128
+    tb_i = np.floor_divide(1772 * cb, 1000) + 128
     n = 202008 * cb + 419198 * cr
     q_i = (n + 587000 * 512) // 587000 - 512
     rem_i = n - q_i * 587000
-    tr_f = np.floor((2804 * cr + 718001).astype(f32) * f32(0.0005)).astype(np.int64) - 359 + 128
-    tb_f = np.floor((3544 * cb + 908001).astype(f32) * f32(0.0005)).astype(np.int64) - 454 + 128
+    tr_m = (91881 * cr + (128 << 16)) >> 16
+    tb_m = (58065 * cb + (128 << 15) + 32) >> 15
+    assert np.abs(91881 * cr).max() < 2**31 and np.abs(58065 * cb).max() < 2**31
     q_f = np.floor(n.astype(f32) * f32(1.0 / 587000.0)).astype(np.int64)
     rem_f = n - q_f * 587000
-    assert (tr_i == tr_f).all() and (tb_i == tb_f).all() and (q_i == q_f).all()
+    assert (tr_i == tr_m).all() and (tb_i == tb_m).all() and (q_i == q_f).all()
     ex_i = (n != 0) & ((rem_i < 64) | (rem_i > 587000 - 64))
     ex_f = (n != 0) & ((rem_f < 64) | (rem_f > 587000 - 64))
     assert (ex_i == ex_f).all()
