@@ -151,7 +151,10 @@ constexpr uint32_t kPieceBits = JD_PIECE_BITS;
 constexpr uint32_t kPieceOverlap = JD_PIECE_OVERLAP;
 constexpr uint32_t kMinPieceBits = 512;      // adaptive floor (small batches)
 constexpr uint64_t kPieceTarget = 65536;    // pieces wanted per batch before shrinking stops
-constexpr int kPieceThreads = 256;  // one workgroup shares one copy of its table set in LDS
+#ifndef JD_PIECE_THREADS
+#define JD_PIECE_THREADS 256
+#endif
+constexpr int kPieceThreads = JD_PIECE_THREADS;  // one workgroup shares one copy of its table set in LDS
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;
@@ -174,7 +177,10 @@ struct alignas(16) CpRec {
     uint32_t bit, mcus, ents, flags;
 };
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
-constexpr int kTileMaxBlocks = 60;   // blocks per IDCT/colour tile (one lane each; k_idct_color's LDS)
+#ifndef JD_TILE_BLOCKS
+#define JD_TILE_BLOCKS 60
+#endif
+constexpr int kTileMaxBlocks = JD_TILE_BLOCKS;   // blocks per IDCT/colour tile (one lane each; k_idct_color's LDS)
 
 // Per-image status bits written by kernels (atomicOr); host maps them to jd_status.
 constexpr uint32_t kStCorrupt = 1u;     // bad code / overrun / DC range

@@ -457,7 +457,7 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 //   k_dc_sum/scan  per tile, the DC predictors at its first block (parser.cpp:106-111); the tile's
 //                  own wave in k_idct_color finishes the prediction
 //
-// A lane's bitstream streams through its own LDS row in windows of kWinAdv bytes: a round issues
+// A lane's bitstream streams through its own LDS row in windows of WIN bytes: a round issues
 // the loads of the NEXT window into registers, decodes every symbol whose refill word lies in the
 // current window, then commits the registers.  The only vmcnt wait per round is that commit
 // (gfx950 counts stores and loads on one vmcnt, so a wait inside the symbol loop would stall on
@@ -601,13 +601,19 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     for (uint32_t u = used + lane; u < im.sub_cap; u += 64) b.sub_seg[im.sub_base + u] = kInvalidImage;
 }
 
-#ifndef JD_WIN_ADV
-#define JD_WIN_ADV 64
+// Bytes a window round advances, per walk: the scan walks (k_piece<Scan>, k_rescan, k_chain_fix)
+// take 32-byte windows (smaller LDS rows: more waves per CU), the write walk 64-byte ones (fewer
+// rounds for its heavier per-round bookkeeping).
+#ifndef JD_WIN_SCAN
+#define JD_WIN_SCAN 32
 #endif
-constexpr int kWinAdv = JD_WIN_ADV;               // bytes a round advances
-constexpr int kWinLoads = kWinAdv / 16 + 1;       // 16-byte loads per window (advance + overlap)
-constexpr int kRowWords = 1 + 4 * kWinLoads;      // 21: odd pitch (last word unused)
-static_assert(kRowWords % 2 == 1, "row pitch must be odd");
+#ifndef JD_WIN_WRITE
+#define JD_WIN_WRITE 64
+#endif
+constexpr int kWinScan = JD_WIN_SCAN, kWinWrite = JD_WIN_WRITE;
+constexpr int win_loads(int win) { return win / 16 + 1; }        // 16-byte loads per window (advance + overlap)
+constexpr int row_words(int win) { return 1 + 4 * win_loads(win); }  // odd pitch (last word unused)
+static_assert(row_words(kWinScan) % 2 == 1 && row_words(kWinWrite) % 2 == 1, "row pitch must be odd");
 #ifndef JD_ABL  // experiment builds: 1 skip colour, 2 skip IDCT math, 4 skip the entry scatter, 8 / 16 skip the
                 // write pass's entry / BlockInfo stores
 #define JD_ABL 0
@@ -616,10 +622,10 @@ constexpr int kWalkScan = 0, kWalkWrite = 1;
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 
 constexpr int kRingWords = 8;  // write walk: per-lane ring of two entry quads (16-byte aligned)
-size_t piece_lds_bytes(uint32_t max_slots) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * kRowWords * 4;
+size_t piece_lds_bytes(uint32_t max_slots, int win) {
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * row_words(win) * 4;
 }
-static_assert((kPieceThreads * kRowWords * 4) % 16 == 0, "rings must start 16-byte aligned");
+static_assert((kPieceThreads * row_words(kWinWrite) * 4) % 16 == 0, "rings must start 16-byte aligned");
 
 // One walk over an interval's bits from `start`.
 //   scan : (true MCU-start state at `start` when warm_to == start, else speculative) until the
@@ -664,9 +670,10 @@ struct BitRow {
         nextw = row[rp];
     }
     __device__ __forceinline__ uint32_t bit() const { return uint32_t((rp << 5) + wb - s); }
+    template <int WIN>
     __device__ __forceinline__ void next_window() {
-        rp -= kWinAdv / 4;
-        wb += kWinAdv * 8;
+        rp -= WIN / 4;
+        wb += WIN * 8;
     }
 };
 
@@ -699,12 +706,13 @@ __device__ __forceinline__ uint32_t lut_fast(uint32_t tab, uint32_t peek) {
 // bytes, bound this pass.  Pieces start on a quad (k_chain aligns them); the last, partial quad
 // is stored dword by dword.  The walk stops after its last block; running past the interval's
 // data is checked once per window round (writes stay inside the piece's slots either way).
+template <int WIN>
 __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp,
                                            uint32_t acp, uint32_t* row, uint32_t* ring, bool active_in, Walk& W) {
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
-    for (int q = 0; q < kWinLoads; q++) {
+    for (int q = 0; q < win_loads(WIN); q++) {
         const u32x4 v = load16(wa + 16 * q, S.last);
         JD_ROW_FILL(row, v, q);
     }
@@ -746,12 +754,12 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
     uint32_t errs = 0;
     bool active = active_in && nblk > 0;
     while (true) {
-        const uintptr_t na = wa + kWinAdv;
-        u32x4 nx[kWinLoads];
+        const uintptr_t na = wa + WIN;
+        u32x4 nx[win_loads(WIN)];
 #pragma unroll
-        for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
+        for (int q = 0; q < win_loads(WIN); q++) nx[q] = load16(na + 16 * q, S.last);
         uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
-        while (active && R.rp <= kWinAdv / 4) {
+        while (active && R.rp <= WIN / 4) {
             it++;
             const uint32_t peek = R.peek();
             uint32_t e = lut_fast(tab, peek);
@@ -805,8 +813,8 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
         }
         if (__ballot(active) == 0) break;  // wave-uniform
 #pragma unroll
-        for (int q = 0; q < kWinLoads; q++) JD_ROW_FILL(row, nx[q], q);
-        R.next_window();
+        for (int q = 0; q < win_loads(WIN); q++) JD_ROW_FILL(row, nx[q], q);
+        R.template next_window<WIN>();
         wa = na;
     }
 #undef JD_FLUSH_Q
@@ -833,7 +841,7 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
 // bits; kScanJoin (a re-scan from the true start) stops at the first MCU boundary that is one of
 // those checkpoints and takes the rest of the counts from the speculative walk's totals.
 constexpr int kScanSpec = 0, kScanJoin = 1;
-template <int KIND>
+template <int KIND, int WIN>
 __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
                                           uint32_t* row, bool active_in, Walk& W, CpRec* cp, uint32_t cp_bits) {
     uint32_t cpb[kCpMax];  // join: checkpoint bits (0xFFFFFFFF: none / taken after an error)
@@ -854,7 +862,7 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
-    for (int q = 0; q < kWinLoads; q++) {
+    for (int q = 0; q < win_loads(WIN); q++) {
         const u32x4 v = load16(wa + 16 * q, S.last);
         JD_ROW_FILL(row, v, q);
     }
@@ -872,11 +880,11 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
     if (counting && W.start + 8 > sbits) active = false;  // starts at the data end: empty
     next_cp = W.start + cp_bits;
     while (true) {
-        const uintptr_t na = wa + kWinAdv;
-        u32x4 nx[kWinLoads];
+        const uintptr_t na = wa + WIN;
+        u32x4 nx[win_loads(WIN)];
 #pragma unroll
-        for (int q = 0; q < kWinLoads; q++) nx[q] = load16(na + 16 * q, S.last);
-        while (active && R.rp <= kWinAdv / 4) {
+        for (int q = 0; q < win_loads(WIN); q++) nx[q] = load16(na + 16 * q, S.last);
+        while (active && R.rp <= WIN / 4) {
             const uint32_t peek = R.peek();
             uint32_t e = lut_fast(tab, peek);
             if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
@@ -943,8 +951,8 @@ __device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lu
         }
         if (__ballot(active) == 0) break;  // wave-uniform
 #pragma unroll
-        for (int q = 0; q < kWinLoads; q++) JD_ROW_FILL(row, nx[q], q);
-        R.next_window();
+        for (int q = 0; q < win_loads(WIN); q++) JD_ROW_FILL(row, nx[q], q);
+        R.template next_window<WIN>();
         wa = na;
     }
     W.end = R.bit();
@@ -1030,11 +1038,11 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     }
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     if (MODE == kWalkScan)
-        walk_scan<kScanSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
+        walk_scan<kScanSpec, kWinScan>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinScan),
                              valid, W, cp, max(1u, piece_len(S, npc) / kCpMax));
     else
-        walk_write(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
-                   s_rows + kPieceThreads * kRowWords + threadIdx.x * kRingWords, valid, W);
+        walk_write<kWinWrite>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinWrite),
+                              s_rows + kPieceThreads * row_words(kWinWrite) + threadIdx.x * kRingWords, valid, W);
     if (MODE == kWalkWrite) {  // the walks end wave-uniformly: one counter atomic per wave, not per lane
         const int tot = wave_scan_dpp(valid ? int(W.ents) : 0);
         if ((threadIdx.x & 63u) == 63u && tot) atomicAdd(&b.counters[0], (unsigned long long)uint32_t(tot));
@@ -1095,7 +1103,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_rescan(BatchDev b) {
     W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * piece_len(S, npc), 0xFFFFFFFEu));
     W.nmcu = W.ent0 = 0;
     W.blk0 = 0;
-    walk_scan<kScanJoin>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords, need, W,
+    walk_scan<kScanJoin, kWinScan>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinScan), need, W,
                          b.piece_cp + size_t(u) * kCpRecords, max(1u, piece_len(S, npc) / kCpMax));
     if (!need) return;
     b.piece_bit[u] = W.start;
@@ -1233,7 +1241,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
             W.stop_at = (j + 1 == n) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * piece_len(S, n), 0xFFFFFFFEu));
             W.nmcu = W.ent0 = 0;
             W.blk0 = 0;
-            walk_scan<kScanJoin>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * kRowWords,
+            walk_scan<kScanJoin, kWinScan>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinScan),
                                  true, W, b.piece_cp + size_t(u) * kCpRecords, max(1u, piece_len(S, n) / kCpMax));
             pbit = expect;
             pend = W.m_end;
@@ -2318,32 +2326,57 @@ __device__ __forceinline__ DcPred load_dcpred(const BatchDev& b, const ImgDesc& 
         if (JD_STAMP && b.stamps && lane == 0) b.stamps[size_t(im.tile_base + tile) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// One wave per tile; grid: tiles x the batch's images of sampling layout M (b.mode_imgs).
+// One wave per kIdctTpw consecutive tiles of an image; grid: tile groups x the batch's images of
+// sampling layout M (b.mode_imgs).  The BlockInfo and DC predictors of all its tiles are loaded up
+// front, so only the first tile waits on the BlockInfo -> entries chain of two dependent HBM round
+// trips (the later tiles' BlockInfo arrives while the first is processed).
+#ifndef JD_TPW
+#define JD_TPW 1
+#endif
+constexpr uint32_t kIdctTpw = JD_TPW;
 template <int M>
 __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
     __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
-    const uint32_t lane = threadIdx.x, img = b.mode_imgs[b.mode_off[M] + blockIdx.y], tile = blockIdx.x;
+    const uint32_t lane = threadIdx.x, img = b.mode_imgs[b.mode_off[M] + blockIdx.y], tile0 = blockIdx.x * kIdctTpw;
     const ImgDesc& im = b.imgs[img];
-    if (tile >= im.tiles_x * im.tiles_y) return;
-    JD_STAMP_AT(0);
-    const TileGeo G = tile_geo<M>(im, tile);
-    const TileLaneGeo L = tile_lane_geo<M>(im, G, lane);
-    const BlockInfo bi = load_block_info<M>(b, im, G, L);
-    const DcPred dcin = load_dcpred(b, im, tile);
+    const uint32_t nt = im.tiles_x * im.tiles_y;
+    if (tile0 >= nt) return;
+    BlockInfo bis[kIdctTpw];
+    DcPred dcs[kIdctTpw];
+#pragma unroll
+    for (uint32_t k = 0; k < kIdctTpw; k++) {
+        bis[k] = BlockInfo{0u, 0u};
+        dcs[k] = DcPred{0, 0, 0, 0};
+        if (tile0 + k < nt) {  // wave-uniform
+            const TileGeo G = tile_geo<M>(im, tile0 + k);
+            bis[k] = load_block_info<M>(b, im, G, tile_lane_geo<M>(im, G, lane));
+            dcs[k] = load_dcpred(b, im, tile0 + k);
+        }
+    }
     stage_quant(b, im, s_qz, lane);
-    zero_staging(s_buf, lane);
-    const EntryRange R = entry_range(b, im, bi, L.have);
-    uint4 E[kPreQuads];
-    load_entry_quads(R, E);
-    const int dc_pred = tile_dc_predict(G, L, bi, dcin, lane);
-    JD_STAMP_AT(1);
-    __syncthreads();
-    scatter_entries(s_buf, staging_base(lane), R, E);
-    __syncthreads();
-    JD_STAMP_AT(2);
-    idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
-    JD_STAMP_AT(4);
+    auto one_tile = [&](uint32_t k, const BlockInfo& bi, const DcPred& dcin) {
+        const uint32_t tile = tile0 + k;
+        JD_STAMP_AT(0);
+        const TileGeo G = tile_geo<M>(im, tile);
+        const TileLaneGeo L = tile_lane_geo<M>(im, G, lane);
+        if (k) __syncthreads();  // the previous tile's plane reads before the zeroing
+        zero_staging(s_buf, lane);
+        const EntryRange R = entry_range(b, im, bi, L.have);
+        uint4 E[kPreQuads];
+        load_entry_quads(R, E);
+        const int dc_pred = tile_dc_predict(G, L, bi, dcin, lane);
+        JD_STAMP_AT(1);
+        __syncthreads();
+        scatter_entries(s_buf, staging_base(lane), R, E);
+        __syncthreads();
+        JD_STAMP_AT(2);
+        idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
+        JD_STAMP_AT(4);
+    };
+#pragma unroll
+    for (uint32_t k = 0; k < kIdctTpw; k++)
+        if (tile0 + k < nt) one_tile(k, bis[k], dcs[k]);  // wave-uniform; straight-line code per tile
 }
 
 // The tiles k_idct_color left (grid-stride over the list; empty in practice).
@@ -2481,11 +2514,11 @@ __global__ void k_test_color(const int32_t* ycc, uint8_t* rgb, int n) {
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots); }
+size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots, kWinWrite) + size_t(kPieceThreads) * kRingWords * 4; }
 
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     if (!b.nimg) return hipSuccess;
-    const size_t lds = piece_lds_bytes(b.max_slots);
+    const size_t lds = piece_lds_bytes(b.max_slots, kWinScan);
     switch (k) {
         case 0:
             if (b.max_chunks) hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
@@ -2516,7 +2549,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
         case 7:
             if (b.nsub)
                 hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads),
-                                   lds + size_t(kPieceThreads) * kRingWords * 4, s, b);
+                                   piece_lds_bytes(b.max_slots, kWinWrite) + size_t(kPieceThreads) * kRingWords * 4, s, b);
             break;
         case 8:
             if (!b.max_tiles) break;
@@ -2528,13 +2561,13 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             if (!b.max_tiles) break;
             // one launch per sampling layout present in the batch (k_idct_color<M> is specialised)
             if (b.mode_cnt[kModeGen])
-                hipLaunchKernelGGL(k_idct_color<kModeGen>, dim3(b.mode_max_tiles[kModeGen], b.mode_cnt[kModeGen]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kModeGen>, dim3((b.mode_max_tiles[kModeGen] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kModeGen]), dim3(kIdctThreads), 0, s, b);
             if (b.mode_cnt[kMode420])
-                hipLaunchKernelGGL(k_idct_color<kMode420>, dim3(b.mode_max_tiles[kMode420], b.mode_cnt[kMode420]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kMode420>, dim3((b.mode_max_tiles[kMode420] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kMode420]), dim3(kIdctThreads), 0, s, b);
             if (b.mode_cnt[kMode422])
-                hipLaunchKernelGGL(k_idct_color<kMode422>, dim3(b.mode_max_tiles[kMode422], b.mode_cnt[kMode422]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kMode422>, dim3((b.mode_max_tiles[kMode422] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kMode422]), dim3(kIdctThreads), 0, s, b);
             if (b.mode_cnt[kMode444])
-                hipLaunchKernelGGL(k_idct_color<kMode444>, dim3(b.mode_max_tiles[kMode444], b.mode_cnt[kMode444]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kMode444>, dim3((b.mode_max_tiles[kMode444] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kMode444]), dim3(kIdctThreads), 0, s, b);
             hipLaunchKernelGGL(k_idct_color_exact, dim3(1024), dim3(kIdctThreads), 0, s, b);
             break;
         case 10:
