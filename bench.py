@@ -428,7 +428,7 @@ def main():
         dec.decode_prepared(prepared, pipelined=pipelined)
     dec.wait()
     status = [r.status for r in prepared[1]]
-    if any(status):
+    if any(status) and args.verify:  # --verify 0: ablation builds decode wrong on purpose
         raise SystemExit(f"decode failed: statuses {sorted(set(status))}")
 
     # correctness spot check against the oracle (outside the timed region): head, middle, tail
@@ -456,7 +456,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if any(r.status for r in prepared[1]):  # the last timed batch's per-image statuses
+    if args.verify and any(r.status for r in prepared[1]):  # the last timed batch's per-image statuses
         raise SystemExit("decode failed inside the timed region")
     st = dec.stats()
 

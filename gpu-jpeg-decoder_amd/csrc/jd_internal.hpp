@@ -35,12 +35,7 @@ constexpr int kLutSize = 1 << kLutBits;
 //     bits 16..19 sz   magnitude bits (DC: symbol, AC: symbol & 15; a DC size above 15 is corrupt)
 //     bit  7      bad  corrupt code (slow path only)
 //   AC tables also describe the FOLLOWING symbol when the first is not EOB and both fit in the
-//   kLutBits; each AC table is built twice, in the format of the walk that reads it:
-//   scan  (k_piece<Scan>, k_rescan, k_chain_fix; HuffLut slot 2 id):
-//     bits 22..25 L2   bits of the second symbol (0: no pair)
-//     bits 26..31 adv2 its advance of z (EOB: 63, which ends any block after an AC symbol)
-//     bit  5      emit2
-//   write (k_piece<Write>; slot 2 id + 1):
+//   kLutBits:
 //     bits 20..23 L2   bits of the second symbol (0: no pair)
 //     bits 24..31 sym2 its run/size byte
 //   The coefficient is always EXTEND(the last sz of the L bits), so a decode step is one lookup
@@ -58,7 +53,6 @@ struct alignas(16) HuffLut {
 static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
 constexpr int kLutWords = int(sizeof(HuffLut) / 4);
 constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 7;
-constexpr uint32_t kEntEmit2 = 1u << 5;
 
 // Entry of a code of length l for symbol sym; 0 when it cannot be represented (l + sz > 31 or a
 // DC size beyond 15 bits: corrupt for 8-bit baseline, whose DC sizes are <= 11).
@@ -111,7 +105,8 @@ struct alignas(16) ImgDesc {
     uint64_t planes;                  // fancy upsampling: device address of the int16 component planes
     uint32_t qmask;                   // k_idct_color's range test of quantised AC coefficients (bits
                                       // k..15 and 16+k..31: |c| <= 2^(k-1), 2^(k-1) * max step < 2^16)
-    uint32_t entry_cap;               // AC-entry slots of this image (entry indices are image-relative)
+    uint32_t entry_cap;               // AC-entry slots of this image (entry indices are image-relative):
+                                      // its pieces' regions, then spare regions for re-walks
     uint64_t entry_base;              // first AC-entry slot of this image in BatchDev::entries
 };
 static_assert(sizeof(ImgDesc) % 16 == 0, "ImgDesc must stay 16-byte aligned");
@@ -165,17 +160,29 @@ constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cann
 #ifndef JD_CP_MAX
 #define JD_CP_MAX 8
 #endif
-constexpr int kCpMax = JD_CP_MAX;  // checkpoints per piece (k_rescan / k_chain shortcuts)
+constexpr int kCpMax = JD_CP_MAX;  // checkpoints per piece (k_redo / k_chain_fix joins)
 constexpr int kCpRecords = kCpMax + 1;
 
-// Speculative-scan checkpoints, kCpRecords per piece slot: kCpMax checkpoints, then the totals.
-//   checkpoint: {bit of an MCU boundary, MCUs and AC entries counted up to it, error so far}
-//   totals:     {end, MCUs, AC entries, error | checkpoints << 8}
-// A re-scan from the true start that reaches a checkpoint's bit at an MCU boundary is in the
-// speculative walk's state there, so it joins it: counts = its own + (totals - checkpoint).
+// Speculative-walk checkpoints, kCpRecords per piece slot: kCpMax checkpoints, then the totals.
+//   checkpoint: {bit of an MCU boundary, MCUs and AC entries written up to it (entries = offset in
+//                the piece's region), 0}
+//   totals:     {end, MCUs, AC entries, MCUs before the first error (kNoError: none)}
+// A re-walk from the true start that reaches a checkpoint's bit at an MCU boundary is in the
+// speculative walk's state there, so it joins it: the piece is then the re-walk's blocks followed
+// by the speculative walk's blocks from that checkpoint on (two segments, k_gather).
 struct alignas(16) CpRec {
     uint32_t bit, mcus, ents, flags;
 };
+constexpr uint32_t kNoError = 0xFFFFFFFFu;
+
+// Per-piece output region (image-relative AC-entry slots): AC entries ascend from its start, one
+// 32-bit record per block (AC-entry count << 16 | 16-bit DC difference) descends from its end.  An
+// emitted entry and a block each take at least 2 bits of the walk, so a piece of plen bits fills
+// at most plen / 2 + kRegionSlack words: the MCU that straddles the piece's end (<= 10 blocks x 64)
+// and one window round past the data end (<= 272), see jd_kernels.hip walk_piece.
+constexpr uint32_t kRegionSlack = 1040;
+JD_HD inline uint32_t region_words(uint32_t plen) { return ((plen + 1u) / 2u + kRegionSlack + 3u) & ~3u; }
+
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
 #ifndef JD_TILE_BLOCKS
 #define JD_TILE_BLOCKS 60
@@ -208,7 +215,6 @@ struct BatchDev {
     const uint32_t* seg_img;      // image of each segment
     uint32_t* seg_cstart;         // first un-stuffed byte of each segment (image-relative)
     uint32_t* seg_cend;           // end of each segment's data (image-relative, un-stuffed)
-    const uint32_t* seg_entry;    // first AC-entry slot of each segment (image-relative)
     uint32_t* seg_sub_base;       // first piece slot of each segment
     uint32_t* seg_nsub;           // pieces of each segment
     uint32_t nseg;
@@ -218,15 +224,21 @@ struct BatchDev {
     const uint32_t* wg_tableset;  // table set of each k_piece workgroup
     uint32_t max_slots;           // LUT slots staged per workgroup
     uint32_t piece_bits, piece_overlap;
-    uint32_t* piece_bit;          // first bit of the piece (an MCU boundary)
-    uint32_t* piece_end;          // scan: first MCU boundary at/after the piece's nominal end
-    uint32_t* piece_nmcu;         // scan: MCUs in the piece (chain: final)
-    uint32_t* piece_nent;         // scan: AC entries in the piece
+    uint32_t* seg_ent;            // k_subplan: first region word of each segment's pieces (image-relative)
+    uint32_t* img_pool;           // k_subplan: next free region word of each image (re-walk regions)
+    uint32_t* piece_bit;          // first bit of the piece (an MCU boundary; kNoPiece: none found)
+    uint32_t* piece_end;          // first MCU boundary at/after the piece's nominal end (or data end)
+    uint32_t* piece_nmcu;         // MCUs walked (chain: MCUs the piece contributes)
+    uint32_t* piece_nent;         // AC entries written
+    uint32_t* piece_emcu;         // MCUs before the first error (kNoError: none)
+    uint32_t* piece_abase;        // first word of the region holding segment A (image-relative)
+    uint32_t* piece_amcu;         // MCUs in segment A
+    uint32_t* piece_join;         // checkpoints recorded << 16 | (segment B = own region from
+                                  // checkpoint join - 1; 0 = none)
     uint32_t* piece_mcu0;         // chain: first MCU of the piece within its segment
-    uint32_t* piece_ent0;         // chain: first AC-entry slot of the piece
     uint32_t* seg_fix;            // k_chain: 1 = the interval needs k_chain_fix's serial walk
-    CpRec* piece_cp;              // scan: kCpRecords per piece slot (CpRec)
-    const uint32_t* chain_seg;    // k_chain: segment of each lane, grouped by table set
+    CpRec* piece_cp;              // kCpRecords per piece slot (CpRec)
+    const uint32_t* chain_seg;    // k_chain_fix: segment of each lane, grouped by table set
     uint32_t nchain;              // multiple of kPieceThreads
     const uint32_t* chain_wg_tableset;
     // scan / compaction

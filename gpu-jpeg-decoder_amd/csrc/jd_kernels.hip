@@ -7,11 +7,13 @@
 //                  (segment) boundaries, RSTn order / count checks
 //   k_compact      16 KiB per workgroup: drops the stuffed 00 after every FF (byte compaction)
 //   k_subplan      one wave per image: pieces (<= piece_bits un-stuffed bits) of every interval
-//   k_piece<Scan>  one lane per piece: speculative, self-synchronising Huffman walk (MCU and
-//                  AC-entry counts, checkpoints); k_rescan re-walks the pieces whose speculative
-//                  start was wrong; k_chain / k_chain_fix verify the chain of pieces and prefix-sum
-//                  each piece's first MCU and entry slot
-//   k_piece<Write> one lane per piece: BlockInfo (DC difference, entry range) + sparse AC entries
+//   k_piece        one lane per piece: a speculative, self-synchronising Huffman walk (warm-up
+//                  from before the piece, then block records + sparse AC entries into the piece's
+//                  own region, checkpoints); k_redo re-walks the pieces whose speculative start
+//                  was wrong (joining the speculative walk at a checkpoint); k_chain / k_chain_fix
+//                  verify the chain of pieces and prefix-sum each piece's first MCU
+//   k_gather       one wave per piece: block records -> BlockInfo (DC difference, entry range) at
+//                  the blocks' global positions
 //   k_dc_sum / k_dc_scan   DC predictors at every IDCT tile's first block
 //   k_idct_color   one wave per tile (a run of <= 64 blocks of one MCU row): DC prediction,
 //                  dequantisation, integer IDCT in registers, replicate chroma upsampling and
@@ -439,21 +441,21 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 // Stage 3: Huffman decode.  Every restart interval (the whole scan when there is no DRI) is cut
 // into pieces of piece_bits un-stuffed bits, one lane each — the reference's self-synchronising
 // decode (parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208) re-planned so that pieces
-// start on MCU boundaries and nothing runs serially:
+// start on MCU boundaries, every piece is decoded once, and nothing runs serially:
 //   k_subplan      per image: pieces of every interval (interval lengths are only known on the
-//                  GPU, after k_index)
-//   k_piece<Scan>  lane per piece j of n = ceil(bits / piece_bits) equal shares L = ceil(bits / n):
+//                  GPU, after k_index) and their output regions
+//   k_piece        lane per piece j of n = ceil(bits / piece_bits) equal shares L = ceil(bits / n):
 //                  starts piece_overlap bits before j*L with a guessed state (Huffman codes
 //                  self-synchronise; so does the MCU phase given a few thousand bits), takes the
-//                  first MCU boundary at/after j*L as the piece start, and counts MCUs and AC
-//                  entries up to the first MCU boundary at/after (j+1)*L.  Piece 0 starts at
-//                  bit 0 in the true state.
-//   k_rescan       lane per piece whose start is not its predecessor's end: re-scan from that end
+//                  first MCU boundary at/after j*L as the piece start, and from there writes its
+//                  blocks (a record per block, the AC entries) into its own region up to the first
+//                  MCU boundary at/after (j+1)*L.  Piece 0 starts at bit 0 in the true state.
+//   k_redo         lane per piece whose start is not its predecessor's end: re-walk from that end
+//                  into a spare region until it meets one of the speculative walk's checkpoints
 //   k_chain        wave per interval: piece j's end must be piece j+1's start (k_chain_fix walks
-//                  the rare interval where it still is not serially, re-scanning).  Prefix sums
-//                  give each piece its first MCU and AC-entry slot.
-//   k_piece<Write> lane per piece, from its verified MCU boundary: BlockInfo + AC entries, DC as
-//                  differences
+//                  the rare interval where it still is not serially, re-walking).  Prefix sums
+//                  give each piece its first MCU.
+//   k_gather       wave per piece: records -> BlockInfo (entry range, DC difference) in block order
 //   k_dc_sum/scan  per tile, the DC predictors at its first block (parser.cpp:106-111); the tile's
 //                  own wave in k_idct_color finishes the prediction
 //
@@ -467,7 +469,11 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 __device__ __forceinline__ u32x4 load16(uintptr_t a, uintptr_t last) {
     // clamped to the image's last mapped 16-byte chunk; bytes past an interval's end are never
     // consumed as data, so what a clamped load returns there is irrelevant
+#if JD_NT & 4
+    return __builtin_nontemporal_load(reinterpret_cast<gu32x4*>(a < last ? a : last));
+#else
     return *reinterpret_cast<gu32x4*>(a < last ? a : last);
+#endif
 }
 
 // Codes longer than kLutBits: the canonical limits decide the length (kLutBits+1 plus the number
@@ -509,7 +515,7 @@ struct SegInfo {
     uint32_t bits;     // un-stuffed data bits of the interval
     uintptr_t data;    // address of the interval's first un-stuffed byte
     uintptr_t last;    // last mapped 16-byte chunk of the image's un-stuffed region
-    uint32_t ent0;     // first AC-entry slot of the interval (image-relative)
+    uint32_t ent0;     // first region word of the interval's pieces (image-relative, k_subplan)
     uint32_t pattern, bpm;
     uint32_t* eimg;    // the image's AC entries (BatchDev::entries + ImgDesc::entry_base)
 };
@@ -534,7 +540,7 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
     S.bits = (cend - cstart) * 8;
     S.data = uintptr_t(im.comp) + cstart;
     S.last = (uintptr_t(im.comp) + (im.len - im.ecs_off) + 63) & ~uintptr_t(15);
-    S.ent0 = b.seg_entry[s];
+    S.ent0 = b.seg_ent[s];
     S.eimg = b.entries + im.entry_base;
     S.pattern = im.block_pattern;
     S.bpm = im.bpm;
@@ -543,10 +549,6 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
 // Nominal piece length of an interval cut into npc pieces: equal shares of its bits (at most
 // piece_bits), so the lanes of a wave walk about the same number of bits.
 __device__ __forceinline__ uint32_t piece_len(const SegInfo& S, uint32_t npc) { return (S.bits + npc - 1u) / npc; }
-
-// AC-entry slots of an interval: 63 per block (a block stores at most 63) plus 3 per MCU for
-// aligning every piece's first entry to a 16-byte quad (at most one pad per non-empty piece).
-__device__ __forceinline__ uint32_t seg_entry_cap(const SegInfo& S) { return 63u * S.nblk + 3u * (S.nblk / S.bpm); }
 
 __device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
     S.data = S.last = uintptr_t(b.imgs) & ~uintptr_t(15);
@@ -559,38 +561,45 @@ __device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
     S.bpm = 1;
 }
 
-// write: the write walk's table format (jd_internal.hpp), else the scan walks'
-__device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads,
-                                           bool write = false) {
+__device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads) {
     for (int slot = 0; slot < ts.nslots; slot++) {
-        const uint4* src = reinterpret_cast<const uint4*>(b.luts + 2 * ts.lut[slot] + (write ? 1 : 0));
+        const uint4* src = reinterpret_cast<const uint4*>(b.luts + ts.lut[slot]);
         uint4* dst = reinterpret_cast<uint4*>(s_lut + slot);
         for (int i = threadIdx.x; i < int(sizeof(HuffLut) / 16); i += nthreads) dst[i] = src[i];
     }
 }
 
-// Per image (one wave): pieces of every interval, interval -> piece map.
+// Per image (one wave): pieces of every interval, interval -> piece map, and each interval's
+// first region word: piece j of an interval of n pieces owns region_words(plen) words from
+// seg_ent + j * region_words(plen).  The image's spare words after them (img_pool) are handed
+// out to re-walks (k_redo, k_chain_fix).
 __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     const ImgDesc& im = b.imgs[blockIdx.x];
     const int lane = threadIdx.x;
-    uint32_t run = 0;
+    uint32_t run = 0, wrun = 0;
     for (uint32_t k0 = 0; k0 < im.nseg; k0 += 64) {
         const uint32_t k = k0 + lane;
-        uint32_t n = 0;
+        uint32_t n = 0, w = 0;
         if (k < im.nseg) {
             const uint32_t s = im.seg_base + k;
             const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
-            n = max(1u, uint32_t((uint64_t(ce - cs) * 8 + b.piece_bits - 1) / b.piece_bits));
+            const uint32_t bits = (ce - cs) * 8;
+            n = max(1u, uint32_t((uint64_t(bits) + b.piece_bits - 1) / b.piece_bits));
+            w = n * region_words((bits + n - 1u) / n);
         }
-        const uint32_t incl = wave_incl_scan(n);
+        const uint32_t incl = wave_incl_scan(n), wincl = wave_incl_scan(w);
         if (k < im.nseg) {
             const uint32_t s = im.seg_base + k;
             b.seg_sub_base[s] = im.sub_base + run + incl - n;
             b.seg_nsub[s] = n;
+            b.seg_ent[s] = wrun + wincl - w;
         }
         run += __shfl(int(incl), 63, 64);
+        wrun += __shfl(int(wincl), 63, 64);
     }
-    // run <= cap by construction (host bound: ceil(ECS bits / piece_bits) + nseg)
+    // run <= sub_cap and wrun <= entry_cap by construction (host bounds: ceil(ECS bits /
+    // piece_bits) + nseg pieces, ECS bits / 2 + kRegionSlack + 4 words per piece)
+    if (lane == 0) b.img_pool[blockIdx.x] = wrun;
     const uint32_t used = min(run, im.sub_cap);
     for (uint32_t k = 0; k < im.nseg; k++) {
         const uint32_t s = im.seg_base + k;
@@ -601,46 +610,29 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     for (uint32_t u = used + lane; u < im.sub_cap; u += 64) b.sub_seg[im.sub_base + u] = kInvalidImage;
 }
 
-// Bytes a window round advances, per walk: the scan walks (k_piece<Scan>, k_rescan, k_chain_fix)
-// take 32-byte windows (smaller LDS rows: more waves per CU), the write walk 64-byte ones (fewer
-// rounds for its heavier per-round bookkeeping).
-#ifndef JD_WIN_SCAN
-#define JD_WIN_SCAN 32
+// Bytes a window round advances (the piece walks' LDS rows hold one window plus a 16-byte
+// overlap per lane).
+#ifndef JD_WIN_PIECE
+#define JD_WIN_PIECE 32
 #endif
-#ifndef JD_WIN_WRITE
-#define JD_WIN_WRITE 64
-#endif
-constexpr int kWinScan = JD_WIN_SCAN, kWinWrite = JD_WIN_WRITE;
+constexpr int kWin = JD_WIN_PIECE;
 constexpr int win_loads(int win) { return win / 16 + 1; }        // 16-byte loads per window (advance + overlap)
 constexpr int row_words(int win) { return 1 + 4 * win_loads(win); }  // odd pitch (last word unused)
-static_assert(row_words(kWinScan) % 2 == 1 && row_words(kWinWrite) % 2 == 1, "row pitch must be odd");
+static_assert(row_words(kWin) % 2 == 1, "row pitch must be odd");
 #ifndef JD_ABL  // experiment builds: 1 skip colour, 2 skip IDCT math, 4 skip the entry scatter, 8 / 16 skip the
-                // write pass's entry / BlockInfo stores
+                // piece walk's entry / block-record stores
 #define JD_ABL 0
 #endif
-constexpr int kWalkScan = 0, kWalkWrite = 1;
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
+// items (entries + block records) one window round can add: every item takes >= 2 bits
+constexpr uint32_t kRoundItems = (kWin * 8 + 31) / 2 + 4;
+static_assert(kRegionSlack >= 640 + kRoundItems + 2, "region slack: straddling MCU + one round past the data");
 
-constexpr int kRingWords = 8;  // write walk: per-lane ring of two entry quads (16-byte aligned)
-size_t piece_lds_bytes(uint32_t max_slots, int win) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * row_words(win) * 4;
+constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte aligned)
+size_t piece_lds_bytes(uint32_t max_slots) {
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * (row_words(kWin) + kRingWords) * 4;
 }
-static_assert((kPieceThreads * row_words(kWinWrite) * 4) % 16 == 0, "rings must start 16-byte aligned");
-
-// One walk over an interval's bits from `start`.
-//   scan : (true MCU-start state at `start` when warm_to == start, else speculative) until the
-//          first MCU boundary at/after warm_to = the piece start; then MCUs and AC entries until
-//          the first MCU boundary at/after stop_at (or past the data end)
-//   write: nmcu MCUs from the MCU boundary `start`: BlockInfo (DC difference) + AC entries
-struct Walk {
-    uint32_t start, warm_to, stop_at;   // scan
-    uint32_t nmcu, ent0;                // write
-    uint64_t blk0;                      // write: global block of the first MCU's first block
-    uint32_t m_start, m_end, mcus, ents;  // scan results (m_start = kNoPiece: none found)
-    uint32_t end;                       // bit after the last symbol decoded
-    uint32_t ncp;                       // scan: checkpoints recorded
-    bool bad;
-};
+static_assert((kPieceThreads * row_words(kWin) * 4) % 16 == 0, "rings must start 16-byte aligned");
 
 // Stream reader over a lane's LDS row of big-endian words.  A and B are the words under the read
 // position and s = 32 - (bits of A consumed), 0..31 (s = 0: A is used up, the next symbol starts
@@ -685,9 +677,9 @@ struct BitRow {
         (row)[4 * (q) + 3] = __builtin_bswap32(v.w);  \
     } while (0)
 
-// Decoder state per symbol (both walks): z = coefficient index of the last symbol (DC: 0), b3 =
-// 3 x block within the MCU, tab = LDS byte offset of the next symbol's table (DC table of the
-// block after a block ends, else the block's AC table).
+// Decoder state per symbol: z = coefficient index of the last symbol (DC: 0), b3 = 3 x block
+// within the MCU, tab = LDS byte offset of the next symbol's table (DC table of the block after a
+// block ends, else the block's AC table).
 constexpr uint32_t kLutBytes = sizeof(HuffLut);
 // tab is an LDS address: lut_fast is one v_lshl_add of the index onto it and the LDS read (the
 // empty asm keeps the compiler from re-associating (peek >> 22) << 2 into a shift-and-mask).
@@ -699,67 +691,147 @@ __device__ __forceinline__ uint32_t lut_fast(uint32_t tab, uint32_t peek) {
     asm("" : "+v"(idx));
     return *reinterpret_cast<lds_u32*>(size_t((idx << 2) + tab));
 }
-//
-// The write walk: nmcu MCUs from the MCU boundary `start`: BlockInfo (DC difference) + AC entries.
-// AC entries collect in a per-lane LDS ring and leave as one 16-byte store per aligned quad
-// [4 fq, 4 fq + 4): a wave's 64 lanes store to 64 unrelated places, so store instructions, not
-// bytes, bound this pass.  Pieces start on a quad (k_chain aligns them); the last, partial quad
-// is stored dword by dword.  The walk stops after its last block; running past the interval's
-// data is checked once per window round (writes stay inside the piece's slots either way).
-template <int WIN>
-__device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp,
-                                           uint32_t acp, uint32_t* row, uint32_t* ring, bool active_in, Walk& W) {
+
+// Block record in a piece's region: AC-entry count (<= 63) << 16 | the 16-bit DC difference (a
+// DC size is <= 15 bits, jd_internal.hpp lut_entry).
+__device__ __forceinline__ uint32_t block_rec(uint32_t cnt, int dc) { return (min(cnt, 63u) << 16) | (uint32_t(dc) & 0xFFFFu); }
+
+// One piece walk.
+//   kSpec: from `start` (piece_overlap bits before the nominal start, with a guessed state) a
+//          warm-up that only follows the symbols to the first MCU boundary at/after warm_to, the
+//          piece start (warm_to == start: the true state at an MCU boundary, piece 0); then the
+//          writing walk, with a checkpoint at the first MCU boundary after every cp_bits bits.
+//   kRedo: the writing walk from the true MCU boundary `start`; it stops at the first MCU
+//          boundary that is one of the speculative walk's checkpoints (cpb) and joins it.
+// The writing walk stores, per block, one record (count, DC difference) and the AC entries, into
+// the region reg[0, rw), until the first MCU boundary at/after stop_at or the data end.  It
+// counts MCUs and notes the number of MCUs before the first error (bad code, bits past the data).
+// The chain decides which MCUs count (the last interval's trailing bytes are ignored, as the
+// oracle ignores them).
+struct PWalk {
+    uint32_t start, warm_to, stop_at;
+    uint32_t* reg;
+    uint32_t rw;
+    uint32_t m_start, m_end, mcus, ents, emcu, ncp, join;
+};
+constexpr int kSpec = 0, kRedo = 1;
+
+#ifndef JD_NT
+#define JD_NT 0  // experiment builds: 1 entry stores non-temporal
+#endif
+__device__ __forceinline__ void st_ent(uint4* p, const uint4& v) {
+    if (JD_NT & 1) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(p));
+    } else {
+        *p = v;
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
+                                           uint32_t* row, uint32_t* ring, bool active_in, PWalk& W, CpRec* cp,
+                                           uint32_t cp_bits, const uint32_t (&cpb)[kCpMax]) {
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
-    for (int q = 0; q < win_loads(WIN); q++) {
+    for (int q = 0; q < win_loads(kWin); q++) {
         const u32x4 v = load16(wa + 16 * q, S.last);
         JD_ROW_FILL(row, v, q);
     }
     BitRow R;
     R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
-    BlockInfo* const bout = b.blocks + W.blk0;
-    uint32_t* const eout = S.eimg;
-    const uint32_t nblk = W.nmcu * S.bpm;
+    const uint32_t sbits = S.bits;
     const uint32_t bpm3 = 3u * S.bpm;
     const uint32_t lbase = lds_addr(s_lutw);
     const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
+    uint32_t* const reg = W.reg;
+    uint32_t* const rec_top = W.reg + (W.rw - 1u);  // block record k at rec_top[-k]
     uint32_t z = 0, b3 = 0, tab = tab_dc0;
-    uint32_t ent = W.ent0, ent_blk = W.ent0, blk = 0;
-    int dcd = 0;
-    // Stores are deferred and issued every few loop iterations, so that one store instruction
-    // carries many lanes (a wave's store instructions, not its bytes, bound this pass).  An
-    // iteration emits at most two entries (a pair entry: two AC symbols), and a block takes at
-    // least two iterations (its DC symbol never pairs), so flushing one quad and one block every
-    // two iterations keeps at most 7 entries pending: one ring of two quads and one pending
-    // block suffice.  Entries go to the ring at slot ent & 7 (a symbol that emits nothing writes
-    // the next free slot without advancing, so its word is overwritten); a flush stores the
-    // completed quad fq straight from the ring.
-    uint32_t fq = W.ent0 >> 2;  // quads stored so far (pieces start on a quad)
-    uint32_t pbi0 = 0, pbi1 = 0, pblk = 0;
-    bool pend_b = false;
-#define JD_FLUSH_Q()                                                                                         \
-    do {                                                                                                     \
-        if (fq < (ent >> 2)) {                                                                               \
-            if (!(JD_ABL & 8) || ent == 0x7FFFFFFFu)                                                         \
-            *reinterpret_cast<uint4*>(eout + 4u * fq) = *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)); \
-            fq++;                                                                                            \
-        }                                                                                                    \
-    } while (0)
-#define JD_FLUSH_B()                                       \
-    do {                                                   \
-        if (pend_b) bout[pblk] = BlockInfo{pbi0, pbi1};    \
-        pend_b = false;                                    \
-    } while (0)
-    uint32_t errs = 0;
-    bool active = active_in && nblk > 0;
-    while (true) {
-        const uintptr_t na = wa + WIN;
-        u32x4 nx[win_loads(WIN)];
+    bool warm = KIND == kSpec && W.warm_to != W.start;
+    bool active = active_in;
+    uint32_t m_start = warm ? kNoPiece : W.start, m_end = W.start;
+    if (!warm && W.start + 8 > sbits) active = false;  // starts at the data end: empty
+    uint32_t next_cp = W.start + cp_bits, ncp = 0, join = 0;
+    // an MCU end at/after end_thr leaves fewer than 8 bits: the data end (padding before RSTn/EOI)
+    const uint32_t end_thr = sbits >= 8u ? sbits - 7u : 0u;
+    uint32_t thr = 0;  // the next bit at which an MCU end needs the slow branch (set when writing starts)
+    if (!warm) {
+        uint32_t nxt = next_cp;
+        if (KIND == kRedo) {
+            nxt = 0xFFFFFFFFu;
 #pragma unroll
-        for (int q = 0; q < win_loads(WIN); q++) nx[q] = load16(na + 16 * q, S.last);
+            for (int c = 0; c < kCpMax; c++) nxt = (cpb[c] > W.start) ? min(nxt, cpb[c]) : nxt;
+        }
+        thr = min(min(W.stop_at, end_thr), nxt);
+    }
+    uint32_t mcus = 0, emcu = kNoError, errs = 0;
+    uint32_t ent = 0, ent_blk = 0, blk = 0;
+    int dcd = 0;
+    // Stores are deferred and issued every other loop iteration, so that one store instruction
+    // carries many lanes.  An iteration emits at most two entries (a pair entry: two AC symbols),
+    // and a block takes at least two iterations (its DC symbol never pairs), so flushing one quad
+    // and one block record every two iterations keeps at most 7 entries pending: one ring of two
+    // quads and one pending record suffice.  Entries go to the ring at slot ent & 7 (a symbol that
+    // emits nothing writes the next free slot without advancing, so its word is overwritten); a
+    // flush stores the completed quad fq straight from the ring.
+    uint32_t fq = 0;  // quads stored so far (regions start on a quad)
+    uint32_t prec = 0, pblk = 0;
+    bool pend_b = false;
+#define JD_FLUSH_Q()                                                                                   \
+    do {                                                                                               \
+        if (fq < (ent >> 2)) {                                                                         \
+            if (!(JD_ABL & 8) || ent == 0x7FFFFFFFu)                                                   \
+                st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u))); \
+            fq++;                                                                                      \
+        }                                                                                              \
+    } while (0)
+#define JD_FLUSH_B()                                                     \
+    do {                                                                 \
+        if (pend_b && (!(JD_ABL & 16) || ent == 0x7FFFFFFFu)) rec_top[-int(pblk)] = prec; \
+        pend_b = false;                                                  \
+    } while (0)
+    while (true) {
+        const uintptr_t na = wa + kWin;
+        u32x4 nx[win_loads(kWin)];
+#pragma unroll
+        for (int q = 0; q < win_loads(kWin); q++) nx[q] = load16(na + 16 * q, S.last);
+        if (KIND == kSpec && __any(active && warm)) {  // wave-uniform
+            // warm-up: follow the symbols only (the write walk's table format: pair fields carry
+            // the second symbol's bits and run/size byte)
+            while (active && warm && R.rp <= kWin / 4) {
+                const uint32_t peek = R.peek();
+                uint32_t e = lut_fast(tab, peek);
+                if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
+                uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+                uint32_t L = e & 31u;
+                const uint32_t L2 = __builtin_amdgcn_ubfe(e, 20u, 4u);
+                if (L2 != 0u && zn < 63u) {
+                    const uint32_t s2 = e >> 24;
+                    zn += s2 ? (s2 >> 4) + 1u : 64u;
+                    L += L2;
+                }
+                R.skip(L, row);
+                const bool fin = zn >= 63u;
+                z = fin ? 0u : zn;
+                b3 += fin ? 3u : 0u;
+                tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
+                if (b3 == bpm3) {  // an MCU ends here
+                    b3 = 0;
+                    tab = tab_dc0;
+                    const uint32_t consumed = R.bit();
+                    if (consumed >= W.warm_to) {  // synchronised (or assumed so): the piece starts here
+                        warm = false;
+                        m_start = m_end = consumed;
+                        next_cp = consumed + cp_bits;
+                        thr = min(min(W.stop_at, end_thr), next_cp);
+                        if (consumed + 8 > sbits) active = false;
+                    }
+                }
+            }
+        }
         uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
-        while (active && R.rp <= WIN / 4) {
+        while (active && !warm && R.rp <= kWin / 4) {
             it++;
             const uint32_t peek = R.peek();
             uint32_t e = lut_fast(tab, peek);
@@ -786,35 +858,73 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
             }
             R.skip(L, row);
             const bool fin = zn >= 63u;
-            pbi0 = fin ? ent_blk : pbi0;
-            pbi1 = fin ? pack_cnt_dc(ent - ent_blk, dcd) : pbi1;
+            prec = fin ? block_rec(ent - ent_blk, dcd) : prec;
             pblk = fin ? blk : pblk;
             pend_b = pend_b || fin;
             if ((it & 1u) == 0u) {
                 JD_FLUSH_Q();
                 JD_FLUSH_B();
             }
-            if (fin) {
-                blk++;
-                ent_blk = ent;
-                active = blk < nblk;
-            }
+            blk += fin ? 1u : 0u;
+            ent_blk = fin ? ent : ent_blk;
             z = fin ? 0u : zn;
             b3 += fin ? 3u : 0u;
             tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
-            tab = (b3 == bpm3) ? tab_dc0 : tab;  // an MCU ends here
-            b3 = (b3 == bpm3) ? 0u : b3;
+            // MCU end: the common case only counts; the branch is taken at the next threshold
+            // (piece end, data end, checkpoint) or after an error
+            const bool mend = b3 == bpm3;
+            b3 = mend ? 0u : b3;
+            tab = mend ? tab_dc0 : tab;
+            mcus += mend ? 1u : 0u;
+            if (mend && (R.bit() >= thr || (errs & kEntBad))) {
+                const uint32_t consumed = R.bit();
+                if ((errs & kEntBad) || consumed > sbits) {  // an error in this MCU
+                    emcu = min(emcu, mcus - 1u);
+                    errs = 0;
+                }
+                uint32_t nxt = 0xFFFFFFFFu;
+                if (consumed >= W.stop_at || consumed >= end_thr) {  // the piece ends here
+                    m_end = consumed;
+                    active = false;
+                } else if (KIND == kSpec) {
+                    if (consumed >= next_cp && ncp < uint32_t(kCpMax)) {
+                        cp[ncp] = CpRec{consumed, mcus, ent, 0u};
+                        ncp++;
+                        next_cp = (ncp < uint32_t(kCpMax)) ? consumed + cp_bits : 0xFFFFFFFFu;
+                    }
+                    nxt = next_cp;
+                } else {
+                    bool hit = false;
+#pragma unroll
+                    for (int c = 0; c < kCpMax; c++) {
+                        hit = hit || cpb[c] == consumed;
+                        if (cpb[c] == consumed) join = uint32_t(c + 1);
+                        nxt = (cpb[c] > consumed) ? min(nxt, cpb[c]) : nxt;
+                    }
+                    if (hit) {  // in the speculative walk's state: join it
+                        m_end = consumed;
+                        active = false;
+                    }
+                }
+                thr = min(min(W.stop_at, end_thr), nxt);
+            }
         }
         JD_FLUSH_Q();
         JD_FLUSH_B();
-        if (active && R.bit() > S.bits) {  // past the interval's data
-            errs |= kEntBad;
+        if (active && R.bit() > sbits) {  // past the data
+            m_end = R.bit();
+            emcu = min(emcu, warm ? 0u : mcus);
+            active = false;
+        }
+        if (active && !warm && ent + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
+            m_end = R.bit();
+            emcu = min(emcu, mcus);
             active = false;
         }
         if (__ballot(active) == 0) break;  // wave-uniform
 #pragma unroll
-        for (int q = 0; q < win_loads(WIN); q++) JD_ROW_FILL(row, nx[q], q);
-        R.template next_window<WIN>();
+        for (int q = 0; q < win_loads(kWin); q++) JD_ROW_FILL(row, nx[q], q);
+        R.template next_window<kWin>();
         wa = na;
     }
 #undef JD_FLUSH_Q
@@ -822,153 +932,17 @@ __device__ __forceinline__ void walk_write(const BatchDev& b, const SegInfo& S, 
     if (ent & 3u) {  // the last, partial quad (every complete one is stored)
         const uint32_t r = ent & 3u, qb = ent - r;
         const uint4 q = *reinterpret_cast<const uint4*>(ring + 4u * ((qb >> 2) & 1u));
-        eout[qb] = q.x;
-        if (r >= 2u) eout[qb + 1u] = q.y;
-        if (r == 3u) eout[qb + 2u] = q.z;
+        reg[qb] = q.x;
+        if (r >= 2u) reg[qb + 1u] = q.y;
+        if (r == 3u) reg[qb + 2u] = q.z;
     }
-    W.end = R.bit();
-    W.bad = (errs & kEntBad) != 0 || (nblk > 0 && blk != nblk) || W.end > S.bits;
-    W.ents = ent - W.ent0;
-}
-
-// The scan walk: per symbol only the table lookup, the reader and the block state machine;
-// everything else happens at MCU boundaries (a branch taken by ~half the wave-steps) or once per
-// window round.  Entry counts are differences of a running count, the error flag is one OR of
-// the entry's bad bit, and running past the data is checked per round (the scan stores nothing
-// per symbol, so decoding a little garbage past the end is harmless).
-//
-// KIND kScanSpec records a checkpoint (CpRec) at the first MCU boundary after every cp_bits counted
-// bits; kScanJoin (a re-scan from the true start) stops at the first MCU boundary that is one of
-// those checkpoints and takes the rest of the counts from the speculative walk's totals.
-constexpr int kScanSpec = 0, kScanJoin = 1;
-template <int KIND, int WIN>
-__device__ __forceinline__ void walk_scan(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
-                                          uint32_t* row, bool active_in, Walk& W, CpRec* cp, uint32_t cp_bits) {
-    uint32_t cpb[kCpMax];  // join: checkpoint bits (0xFFFFFFFF: none / taken after an error)
-    CpRec tot = {0u, 0u, 0u, 0u};
-    if (KIND == kScanJoin) {
-        if (active_in) tot = cp[kCpMax];
-        const uint32_t ncp = tot.flags >> 8;
-#pragma unroll
-        for (int c = 0; c < kCpMax; c++) {
-            cpb[c] = 0xFFFFFFFFu;
-            if (active_in && uint32_t(c) < ncp) {
-                const CpRec r = cp[c];
-                if (!(r.flags & 1u)) cpb[c] = r.bit;
-            }
-        }
-    }
-    uint32_t joined = 0, ncp = 0, next_cp = 0;
-    const uintptr_t a_start = S.data + (W.start >> 3);
-    uintptr_t wa = a_start & ~uintptr_t(15);
-#pragma unroll
-    for (int q = 0; q < win_loads(WIN); q++) {
-        const u32x4 v = load16(wa + 16 * q, S.last);
-        JD_ROW_FILL(row, v, q);
-    }
-    BitRow R;
-    R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
-    const uint32_t sbits = S.bits;
-    const uint32_t bpm3 = 3u * S.bpm;
-    const uint32_t lbase = lds_addr(s_lutw);
-    const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
-    uint32_t z = 0, b3 = 0, tab = tab_dc0;
-    uint32_t counting = (W.warm_to == W.start) ? 1u : 0u;
-    uint32_t mcus = 0, ents = 0, ents0 = 0, m_start = counting ? W.start : kNoPiece, m_end = W.start;
-    uint32_t errs = 0;  // kEntBad: a bad code since counting began
-    bool active = active_in;
-    if (counting && W.start + 8 > sbits) active = false;  // starts at the data end: empty
-    next_cp = W.start + cp_bits;
-    while (true) {
-        const uintptr_t na = wa + WIN;
-        u32x4 nx[win_loads(WIN)];
-#pragma unroll
-        for (int q = 0; q < win_loads(WIN); q++) nx[q] = load16(na + 16 * q, S.last);
-        while (active && R.rp <= WIN / 4) {
-            const uint32_t peek = R.peek();
-            uint32_t e = lut_fast(tab, peek);
-            if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
-            errs |= e;
-            // EOB / ZRL / run-size (parser.cpp:114-134)
-            uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
-            uint32_t L = e & 31u;
-            ents += __builtin_amdgcn_ubfe(e & ~zn, 6u, 1u);  // emit flag, unless past index 63
-            const uint32_t L2 = __builtin_amdgcn_ubfe(e, 22u, 4u);
-            if (L2 != 0u && zn < 63u) {  // a pair entry, and the first symbol left the block open
-                const uint32_t z2 = zn + (e >> 26);
-                ents += __builtin_amdgcn_ubfe(e & ~(z2 >> 1), 5u, 1u);  // emit2 unless z2 > 63
-                zn = z2;
-                L += L2;
-            }
-            R.skip(L, row);
-            const bool fin = zn >= 63u;
-            z = fin ? 0u : zn;
-            b3 += fin ? 3u : 0u;
-            tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
-            if (b3 == bpm3) {  // an MCU ends here
-                b3 = 0;
-                tab = tab_dc0;
-                const uint32_t consumed = R.bit();
-                const bool at_end = consumed + 8 > sbits;
-                if (!counting) {
-                    if (consumed >= W.warm_to) {  // synchronised: the piece starts here
-                        counting = 1u;
-                        m_start = consumed;
-                        next_cp = consumed + cp_bits;
-                        ents0 = ents;
-                        errs = 0;
-                        if (at_end) {
-                            m_end = consumed;
-                            active = false;
-                        }
-                    }
-                } else {
-                    mcus++;
-                    if (consumed >= W.stop_at || at_end) {  // the piece ends here
-                        m_end = consumed;
-                        active = false;
-                    } else if (KIND == kScanSpec && consumed >= next_cp && ncp < uint32_t(kCpMax)) {
-                        cp[ncp] = CpRec{consumed, mcus, ents - ents0, (errs & kEntBad) ? 1u : 0u};
-                        ncp++;
-                        next_cp = consumed + cp_bits;
-                    } else if (KIND == kScanJoin) {
-                        uint32_t hit = 0;
-#pragma unroll
-                        for (int c = 0; c < kCpMax; c++) hit = (cpb[c] == consumed) ? uint32_t(c + 1) : hit;
-                        if (hit) {  // in the speculative walk's state: join it
-                            joined = hit;
-                            m_end = consumed;
-                            active = false;
-                        }
-                    }
-                }
-            }
-        }
-        if (active && R.bit() > sbits) {  // past the data
-            m_end = R.bit();
-            if (counting) errs |= kEntBad;
-            active = false;
-        }
-        if (__ballot(active) == 0) break;  // wave-uniform
-#pragma unroll
-        for (int q = 0; q < win_loads(WIN); q++) JD_ROW_FILL(row, nx[q], q);
-        R.template next_window<WIN>();
-        wa = na;
-    }
-    W.end = R.bit();
-    W.bad = counting && (errs & kEntBad);
     W.m_start = m_start;
     W.m_end = m_end;
     W.mcus = mcus;
-    W.ents = ents - ents0;
+    W.ents = ent;
+    W.emcu = emcu;
     W.ncp = ncp;
-    if (KIND == kScanJoin && joined) {
-        const CpRec c = cp[joined - 1];
-        W.m_end = tot.bit;
-        W.mcus += tot.mcus - c.mcus;
-        W.ents += tot.ents - c.ents;
-        W.bad = W.bad || (tot.flags & 1u);
-    }
+    W.join = join;
 }
 
 __device__ __forceinline__ void table_slots(const TableSet& ts, const SegInfo& S, uint32_t& dcp, uint32_t& acp) {
@@ -980,144 +954,173 @@ __device__ __forceinline__ void table_slots(const TableSet& ts, const SegInfo& S
     }
 }
 
-template <int MODE>
+// Piece geometry of lane/slot u in interval s.
+struct PieceGeo {
+    uint32_t j, npc, plen, rw, own;  // own: first word of the piece's region (image-relative)
+};
+__device__ __forceinline__ PieceGeo piece_geo(const BatchDev& b, const SegInfo& S, uint32_t s, uint32_t u) {
+    PieceGeo P;
+    P.j = u - b.seg_sub_base[s];
+    P.npc = b.seg_nsub[s];
+    P.plen = piece_len(S, P.npc);
+    P.rw = region_words(P.plen);
+    P.own = S.ent0 + P.j * P.rw;
+    return P;
+}
+__device__ __forceinline__ uint32_t piece_stop(const PieceGeo& P) {
+    return (P.j + 1 == P.npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(P.j + 1) * P.plen, 0xFFFFFFFEu));
+}
+
+// Lane per piece slot: the speculative walk (warm-up, then the writing walk into the piece's own
+// region).  Piece 0 of an interval starts at bit 0 in the true state.
 __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
-    stage_luts(b, ts, s_lut, kPieceThreads, MODE == kWalkWrite);
+    stage_luts(b, ts, s_lut, kPieceThreads);
     __syncthreads();
 
     const uint32_t u = blockIdx.x * kPieceThreads + threadIdx.x;
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
-    bool valid = s != kInvalidImage;
+    const bool valid = s != kInvalidImage;
     SegInfo S;
-    uint32_t j = 0, npc = 1, nmcu_seg = 0;
+    PieceGeo P{0u, 1u, 0u, 0u, 0u};
     if (valid) {
         seg_info(b, s, S);
-        j = u - b.seg_sub_base[s];
-        npc = b.seg_nsub[s];
-        nmcu_seg = S.nblk / S.bpm;
+        P = piece_geo(b, S, s, u);
     } else {
         seg_invalid(b, S);
     }
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    Walk W;
-    W.nmcu = 0;
-    W.ent0 = 0;
-    W.blk0 = 0;
-    if (MODE == kWalkScan) {
-        // piece 0 counts from bit 0 in the true state; piece j > 0 synchronises from
-        // piece_overlap bits before its nominal start (from bit 0, exactly, when that is closer)
-        const uint32_t plen = piece_len(S, npc);
-        const uint64_t pstart = uint64_t(j) * plen;
-        W.warm_to = (j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
-        W.start = (pstart <= b.piece_overlap) ? 0u : min(uint32_t(pstart - b.piece_overlap), W.warm_to);
-        W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(pstart + plen, 0xFFFFFFFEu));
-    } else {
-        W.start = valid ? b.piece_bit[u] : 0u;
-        W.warm_to = W.start;
-        W.stop_at = 0;
-        if (valid) {
-            const uint32_t m0 = b.piece_mcu0[u];
-            W.nmcu = b.piece_nmcu[u];
-            W.ent0 = b.piece_ent0[u];
-            // never write outside the interval (the chain flagged inconsistent counts as corrupt)
-            if (W.start == kNoPiece || W.start > S.bits || m0 + W.nmcu > nmcu_seg || (W.ent0 & 3u) ||
-                uint64_t(W.ent0) + 63ull * W.nmcu * S.bpm > uint64_t(S.ent0) + seg_entry_cap(S))
-                valid = false;
-            W.blk0 = S.blk0 + uint64_t(m0) * S.bpm;
-        }
-        if (!valid) {
-            seg_invalid(b, S);
-            W.start = W.warm_to = 0;
-            W.nmcu = 0;
-        }
-    }
+    PWalk W;
+    // piece j > 0 synchronises from piece_overlap bits before its nominal start (from bit 0,
+    // exactly, when that is closer)
+    const uint64_t pstart = uint64_t(P.j) * P.plen;
+    W.warm_to = (P.j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
+    W.start = (pstart <= b.piece_overlap) ? 0u : min(uint32_t(pstart - b.piece_overlap), W.warm_to);
+    W.stop_at = piece_stop(P);
+    W.reg = S.eimg + P.own;
+    W.rw = P.rw;
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
-    if (MODE == kWalkScan)
-        walk_scan<kScanSpec, kWinScan>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinScan),
-                             valid, W, cp, max(1u, piece_len(S, npc) / kCpMax));
-    else
-        walk_write<kWinWrite>(b, S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinWrite),
-                              s_rows + kPieceThreads * row_words(kWinWrite) + threadIdx.x * kRingWords, valid, W);
-    if (MODE == kWalkWrite) {  // the walks end wave-uniformly: one counter atomic per wave, not per lane
-        const int tot = wave_scan_dpp(valid ? int(W.ents) : 0);
-        if ((threadIdx.x & 63u) == 63u && tot) atomicAdd(&b.counters[0], (unsigned long long)uint32_t(tot));
-    }
+    const uint32_t none[kCpMax] = {};
+    walk_piece<kSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWin),
+                      s_rows + kPieceThreads * row_words(kWin) + threadIdx.x * kRingWords, valid, W, cp,
+                      max(1u, P.plen / kCpMax), none);
     if (!valid) return;
-    if (MODE == kWalkScan) {
-        // piece 0 starts at bit 0 whatever its walk found (it is the true state)
-        b.piece_bit[u] = (j == 0) ? 0u : W.m_start;
-        b.piece_end[u] = W.m_end;
-        b.piece_nmcu[u] = W.mcus | (W.bad ? 0x80000000u : 0u);  // bit 31: error while counting
-        b.piece_nent[u] = W.ents;
-        cp[kCpMax] = CpRec{W.m_end, W.mcus, W.ents, (W.bad ? 1u : 0u) | (W.ncp << 8)};
-    } else {
-        bool bad = W.bad;
-        if (j + 1 == npc && !bad) {
-            const uint32_t end = W.nmcu > 0 ? W.end : W.start;
-            if (end > S.bits) bad = true;
-            // after the last block only padding (< 1 byte) may precede the next RSTn: the
-            // oracle's restart looks for the marker right there (oracle/jdoracle.c br_restart)
-            const ImgDesc& im = b.imgs[b.seg_img[s]];
-            if (s + 1 < im.seg_base + im.nseg && (S.bits >> 3) > ((end + 7) >> 3)) bad = true;
-        }
-        if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
-    }
+    b.piece_bit[u] = (P.j == 0) ? 0u : W.m_start;
+    b.piece_end[u] = W.m_end;
+    b.piece_nmcu[u] = W.mcus;
+    b.piece_nent[u] = W.ents;
+    b.piece_emcu[u] = W.emcu;
+    b.piece_abase[u] = P.own;
+    b.piece_amcu[u] = W.mcus;
+    b.piece_join[u] = W.ncp << 16;
+    cp[kCpMax] = CpRec{W.m_end, W.mcus, W.ents, W.emcu};
 }
 
-// Lane per piece: re-scan, all at once, every piece whose speculative start disagrees with its
+// Re-walk piece u of interval s from its true start `expect` (its predecessor's end): into a
+// spare region of the image when one is left (joining the speculative walk at a checkpoint),
+// else over its own region (no join: that overwrites what the checkpoints describe).
+// Returns the piece's new end.
+__device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceGeo& P, uint32_t s, uint32_t u,
+                               uint32_t expect, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp, uint32_t* row,
+                               uint32_t* ring, bool need) {
+    CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
+    uint32_t ncp = 0, base = P.own;
+    CpRec tot{0u, 0u, 0u, kNoError};
+    uint32_t cpb[kCpMax];
+    if (need) {
+        ncp = b.piece_join[u] >> 16;
+        tot = cp[kCpMax];
+        const uint32_t img = b.seg_img[s];
+        const uint32_t a = atomicAdd(&b.img_pool[img], P.rw);
+        if (uint64_t(a) + P.rw <= b.imgs[img].entry_cap) base = a;
+        else ncp = 0;  // in place
+    }
+#pragma unroll
+    for (int c = 0; c < kCpMax; c++) cpb[c] = (need && uint32_t(c) < ncp) ? cp[c].bit : 0xFFFFFFFFu;
+    PWalk W;
+    W.start = W.warm_to = expect;
+    W.stop_at = piece_stop(P);
+    W.reg = S.eimg + base;
+    W.rw = P.rw;
+    walk_piece<kRedo>(S, s_lutw, dcp, acp, row, ring, need, W, cp, 0xFFFFFFFFu, cpb);
+    if (!need) return 0;
+    uint32_t end = W.m_end, mcus = W.mcus, ents = W.ents, emcu = W.emcu;
+    if (W.join) {
+        const CpRec c = cp[W.join - 1];
+        end = tot.bit;
+        mcus += tot.mcus - c.mcus;
+        ents += tot.ents - c.ents;
+        if (tot.flags != kNoError && tot.flags >= c.mcus) emcu = min(emcu, W.mcus + (tot.flags - c.mcus));
+    }
+    b.piece_bit[u] = expect;
+    b.piece_end[u] = end;
+    b.piece_nmcu[u] = mcus;
+    b.piece_nent[u] = ents;
+    b.piece_emcu[u] = emcu;
+    b.piece_abase[u] = base;
+    b.piece_amcu[u] = W.mcus;
+    b.piece_join[u] = (ncp << 16) | W.join;
+    return end;
+}
+
+// Lane per piece: re-walk, all at once, every piece whose speculative start disagrees with its
 // predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images).
-// Starting from that end is exact when the predecessor is right; if the predecessor is itself
-// re-scanned in this round the start may be stale, which k_chain's serial verification catches.
-__global__ __launch_bounds__(kPieceThreads) void k_rescan(BatchDev b) {
+// Starting from that end is exact when the predecessor is right; a predecessor re-walked in this
+// round keeps its end when it joins its speculative walk, and otherwise k_chain notices.
+__global__ __launch_bounds__(kPieceThreads) void k_redo(BatchDev b) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const uint32_t u = blockIdx.x * kPieceThreads + threadIdx.x;
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
-    uint32_t j = 0, npc = 1, expect = 0;
+    uint32_t expect = 0;
     bool need = false;
-    if (s != kInvalidImage) {
-        j = u - b.seg_sub_base[s];
-        npc = b.seg_nsub[s];
-        if (j > 0) {
-            expect = b.piece_end[u - 1];
-            need = b.piece_bit[u] != expect;
-        }
+    if (s != kInvalidImage && u != b.seg_sub_base[s]) {
+        expect = b.piece_end[u - 1];
+        need = b.piece_bit[u] != expect;
     }
     if (!__syncthreads_or(need)) return;  // workgroup-uniform
     const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
     stage_luts(b, ts, s_lut, kPieceThreads);
     __syncthreads();
     SegInfo S;
-    if (need) seg_info(b, s, S);
-    else seg_invalid(b, S);
+    PieceGeo P{0u, 1u, 0u, 0u, 0u};
+    if (need) {
+        seg_info(b, s, S);
+        P = piece_geo(b, S, s, u);
+    } else {
+        seg_invalid(b, S);
+    }
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    Walk W;
-    W.start = W.warm_to = expect;
-    W.stop_at = (j + 1 == npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * piece_len(S, npc), 0xFFFFFFFEu));
-    W.nmcu = W.ent0 = 0;
-    W.blk0 = 0;
-    walk_scan<kScanJoin, kWinScan>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinScan), need, W,
-                         b.piece_cp + size_t(u) * kCpRecords, max(1u, piece_len(S, npc) / kCpMax));
-    if (!need) return;
-    b.piece_bit[u] = W.start;
-    b.piece_end[u] = W.m_end;
-    b.piece_nmcu[u] = W.mcus | (W.bad ? 0x80000000u : 0u);
-    b.piece_nent[u] = W.ents;
+    redo_piece(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp,
+               s_rows + threadIdx.x * row_words(kWin), s_rows + kPieceThreads * row_words(kWin) + threadIdx.x * kRingWords,
+               need);
+}
+
+// The MCUs piece j contributes, given its first MCU m0 (the interval has nmcu_seg): a piece before
+// the last one that matters takes all it walked, error-free; the last takes the rest, which it must
+// have walked error-free — exactly, unless the interval is the scan's last, whose trailing bytes
+// are ignored (the oracle stops after the frame's MCUs).
+__device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_t m0, uint32_t nmcu_seg, bool last,
+                                               bool final_seg, bool& bad) {
+    if (!last) {
+        bad |= em != kNoError;
+        return pm;
+    }
+    const uint32_t take = nmcu_seg >= m0 ? nmcu_seg - m0 : 0u;
+    bad |= m0 > nmcu_seg || (final_seg ? pm < take : pm != take) || em < take;
+    return min(take, pm);
 }
 
 // One wave per interval, all pieces at once: verify that every piece starts where its predecessor
-// ended, and give each piece its first MCU and first AC-entry slot by prefix sums.  The serial
-// rule (piece j's entries start at the running count rounded up to a quad) is the same prefix:
-// align4(align4(e0) + ... ) = align4(e0) + sum of align4(count) over the earlier pieces.  An
-// interval where some speculative start still disagrees after k_rescan (a double failure, rare)
-// is flagged for k_chain_fix, which walks it serially with re-scans.
+// ended, and give each piece its first MCU and its MCU count by prefix sums.  An interval where
+// some start still disagrees after k_redo (a double failure, rare) is flagged for k_chain_fix,
+// which walks it serially with re-walks.
 __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -1126,16 +1129,16 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     seg_info(b, s, S);
     const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
     const uint32_t nmcu_seg = S.nblk / S.bpm;
-    const uint64_t ent_cap_end = uint64_t(S.ent0) + seg_entry_cap(S);
-    // The scan's last interval ends at EOI, and what follows its last MCU is ignored (the oracle
-    // stops after the frame's MCUs): the piece whose MCUs reach the interval's count is the last
-    // one that matters, and the pieces after it (decoding trailing bytes) are dropped.
+    const bool final_seg = seg_is_final(b, s);
+    // The scan's last interval ends at EOI, and what follows its last MCU is ignored: the piece
+    // whose MCUs reach the interval's count is the last one that matters, and the pieces after it
+    // (decoding trailing bytes) are dropped.
     uint32_t jl = n - 1;
-    if (seg_is_final(b, s)) {
+    if (final_seg) {
         uint32_t run = 0;
         for (uint32_t j0 = 0; j0 < n; j0 += 64) {
             const uint32_t j = j0 + lane;
-            const uint32_t pm = j < n ? (b.piece_nmcu[base + j] & 0x7FFFFFFFu) : 0u;
+            const uint32_t pm = j < n ? b.piece_nmcu[base + j] : 0u;
             const uint32_t inc = run + uint32_t(wave_scan_dpp(int(pm)));
             const uint64_t hit = __ballot(j < n && inc >= nmcu_seg);
             if (hit) {  // wave-uniform
@@ -1155,44 +1158,29 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
         return;
     }
     if (lane == 0) b.seg_fix[s] = 0u;
-    uint32_t mcu_run = 0, ent_run = (S.ent0 + 3u) & ~3u;
+    uint32_t mcu_run = 0;
     bool bad = false;
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
         const uint32_t j = j0 + lane;
-        const bool in = j <= jl;  // pieces past jl: no MCUs, no entries
-        uint32_t pm = in ? b.piece_nmcu[base + j] : 0u;
-        const uint32_t pe = in ? b.piece_nent[base + j] : 0u;
-        const bool last = j == jl;
-        // counting from a verified start is exact, so an error there is the stream's; the last
-        // piece's scan runs past the data on purpose (its write lane checks it exactly)
-        bad |= in && !last && (pm >> 31);
-        pm = (in && !last) ? (pm & 0x7FFFFFFFu) : 0u;
-        const uint32_t pe4 = in ? (pe + 3u) & ~3u : 0u;
-        const uint32_t im = uint32_t(wave_scan_dpp(int(pm))), ie = uint32_t(wave_scan_dpp(int(pe4)));
-        const uint32_t m0 = mcu_run + im - pm, e0 = ent_run + ie - pe4;
-        if (last) {  // the last piece takes the interval's remaining MCUs
-            bad |= m0 > nmcu_seg;
-            pm = nmcu_seg >= m0 ? nmcu_seg - m0 : 0u;
-        }
-        // a piece stores at most 63 entries per block: if that cannot fit, the counts are corrupt
-        if (in && uint64_t(e0) + 63ull * pm * S.bpm > ent_cap_end) {
-            bad = true;
-            pm = 0;
-        }
+        const bool in = j <= jl;  // pieces past jl: no MCUs
+        const uint32_t pm = in ? b.piece_nmcu[base + j] : 0u;
+        const uint32_t pin = (in && j != jl) ? pm : 0u;
+        const uint32_t im = uint32_t(wave_scan_dpp(int(pin)));
+        const uint32_t m0 = mcu_run + im - pin;
+        uint32_t take = 0;
+        if (in) take = piece_take(pm, b.piece_emcu[base + j], m0, nmcu_seg, j == jl, final_seg, bad);
         if (j < n) {
-            b.piece_mcu0[base + j] = m0;
-            b.piece_nmcu[base + j] = pm;
-            b.piece_ent0[base + j] = e0;
+            b.piece_mcu0[base + j] = min(m0, nmcu_seg);
+            b.piece_nmcu[base + j] = (m0 <= nmcu_seg) ? min(take, nmcu_seg - m0) : 0u;
         }
         mcu_run += __shfl(int(im), 63, 64);
-        ent_run += __shfl(int(ie), 63, 64);
     }
     if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
 }
 
 // One lane per interval flagged by k_chain (workgroups grouped by table set): walk its pieces in
-// order, re-scan every piece whose start disagrees with its predecessor's end (the workgroup
-// stages its tables only when some lane needs them), and prefix the counts serially.
+// order, re-walk every piece whose start disagrees with its predecessor's end (the workgroup
+// stages its tables only when some lane needs them), and take the counts serially.
 __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
@@ -1203,76 +1191,121 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
     const bool need = s != kInvalidImage;
     if (!__syncthreads_or(need)) return;  // workgroup-uniform: the common case
     const TableSet& ts = b.tablesets[b.chain_wg_tableset[blockIdx.x]];
-    const bool valid = need;
     SegInfo S;
     uint32_t base = 0, n = 0;
-    if (valid) {
+    if (need) {
         seg_info(b, s, S);
         base = b.seg_sub_base[s];
         n = b.seg_nsub[s];
     } else {
         seg_invalid(b, S);
     }
-    {
-        stage_luts(b, ts, s_lut, kPieceThreads);
-        __syncthreads();
-    }
-    if (!valid) return;
+    stage_luts(b, ts, s_lut, kPieceThreads);
+    __syncthreads();
+    if (!need) return;
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
+    uint32_t* const row = s_rows + threadIdx.x * row_words(kWin);
+    uint32_t* const ring = s_rows + kPieceThreads * row_words(kWin) + threadIdx.x * kRingWords;
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const bool final_seg = seg_is_final(b, s);  // trailing bytes after its last MCU are ignored
     bool bad = false, done = false;
-    uint32_t expect = 0, mcu_run = 0, ent_run = S.ent0;
+    uint32_t expect = 0, mcu_run = 0;
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t u = base + j;
-        if (done) {  // past the piece that completed the final interval: nothing to decode
+        if (done) {  // past the piece that completed the final interval: nothing to take
             b.piece_mcu0[u] = nmcu_seg;
             b.piece_nmcu[u] = 0u;
-            b.piece_ent0[u] = (ent_run + 3u) & ~3u;
             continue;
         }
-        uint32_t pbit = b.piece_bit[u], pend = b.piece_end[u], pm = b.piece_nmcu[u], pe = b.piece_nent[u];
-        bool pbad = (pm >> 31) != 0;  // the piece's scan hit an error while counting
-        pm &= 0x7FFFFFFFu;
-        if (pbit != expect) {  // the speculative start had not synchronised: re-scan from the truth
-            Walk W;
-            W.start = W.warm_to = expect;
-            W.stop_at = (j + 1 == n) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(j + 1) * piece_len(S, n), 0xFFFFFFFEu));
-            W.nmcu = W.ent0 = 0;
-            W.blk0 = 0;
-            walk_scan<kScanJoin, kWinScan>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWinScan),
-                                 true, W, b.piece_cp + size_t(u) * kCpRecords, max(1u, piece_len(S, n) / kCpMax));
-            pbit = expect;
-            pend = W.m_end;
-            pm = W.mcus;
-            pe = W.ents;
-            pbad = W.bad;
-            b.piece_bit[u] = pbit;
+        uint32_t pend = b.piece_end[u];
+        if (b.piece_bit[u] != expect) {  // the start had not synchronised: re-walk from the truth
+            const PieceGeo P = piece_geo(b, S, s, u);
+            pend = redo_piece(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, row, ring, true);
         }
-        // counting from a verified start is exact, so an error there is the stream's; the last
-        // piece's scan runs past the data on purpose (its write lane checks it exactly)
-        if (j + 1 < n && !(final_seg && mcu_run + pm >= nmcu_seg)) {
-            bad |= pbad;
-        } else {  // the last piece takes the interval's remaining MCUs
-            if (mcu_run > nmcu_seg) bad = true;
-            pm = nmcu_seg >= mcu_run ? nmcu_seg - mcu_run : 0u;
-            done = true;
-        }
-        ent_run = (ent_run + 3u) & ~3u;  // pieces start on a 16-byte quad of entries
-        // a piece stores at most 63 entries per block: if that cannot fit, the counts are corrupt
-        if (uint64_t(ent_run) + 63ull * pm * S.bpm > uint64_t(S.ent0) + seg_entry_cap(S)) {
-            bad = true;
-            pm = 0;
-        }
-        b.piece_mcu0[u] = mcu_run;
-        b.piece_nmcu[u] = pm;
-        b.piece_ent0[u] = ent_run;
-        mcu_run += pm;
-        ent_run += pe;
+        const uint32_t pm = b.piece_nmcu[u], em = b.piece_emcu[u];
+        const bool last = j + 1 == n || (final_seg && mcu_run + pm >= nmcu_seg);
+        const uint32_t take = piece_take(pm, em, mcu_run, nmcu_seg, last, final_seg, bad);
+        b.piece_mcu0[u] = min(mcu_run, nmcu_seg);
+        b.piece_nmcu[u] = (mcu_run <= nmcu_seg) ? min(take, nmcu_seg - mcu_run) : 0u;
+        mcu_run += take;
+        done = last;
         expect = pend;
     }
     if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+}
+
+// Lane per piece: the piece's block records -> BlockInfo at the blocks' global positions, entry
+// offsets by a running sum of the records' counts.  Segment A (the piece's own region, or a
+// re-walk's spare region) first, then segment B (the own region from the joined checkpoint on).
+// Segment A's records are read as aligned quads (a region starts and ends on a quad, so its top
+// record is the last word of one), two quads in flight; BlockInfo leaves in pairs (16-byte stores)
+// once the output index is even.  Segment B (rare: joined re-walks) reads word by word.
+__device__ __forceinline__ void put_block(BlockInfo* out, uint32_t k, uint32_t lead, uint32_t r, uint32_t& run, uint2& pend) {
+    const uint32_t cnt = r >> 16;
+    const uint2 v = make_uint2(run, pack_cnt_dc(cnt, int(int16_t(r & 0xFFFFu))));
+    run += cnt;
+    if (k == 1u && lead) {  // the first block sits at an odd index: alone
+        out[1] = BlockInfo{v.x, v.y};
+    } else if (k & 1u) {
+        if (!(JD_ABL & 32) || run == 0x7FFFFFFFu)
+            *reinterpret_cast<uint4*>(out + (k - 1u)) = make_uint4(pend.x, pend.y, v.x, v.y);
+    } else {
+        pend = v;
+    }
+}
+__device__ __forceinline__ uint32_t gather_run(BlockInfo* out, const uint32_t* rec_top, uint32_t nb, uint32_t ebase,
+                                               bool aligned) {
+    uint32_t run = ebase;
+    uint2 pend = make_uint2(0u, 0u);
+    // out is addressed by block parity from here on: index k of `out` is even iff it starts a pair
+    const uint32_t lead = uint32_t(reinterpret_cast<uintptr_t>(out) >> 3) & 1u;
+    BlockInfo* o = out - lead;
+    if (aligned) {
+        const uint4* q = reinterpret_cast<const uint4*>(rec_top - 3);  // records 0..3 = .w .z .y .x
+        for (uint32_t k0 = 0; k0 < nb; k0 += 8) {
+            const uint4 a = q[-int(k0 >> 2)];
+            const uint4 c = (k0 + 4 < nb) ? q[-int(k0 >> 2) - 1] : make_uint4(0, 0, 0, 0);
+            const uint32_t r[8] = {a.w, a.z, a.y, a.x, c.w, c.z, c.y, c.x};
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (k0 + i < nb) put_block(o, lead + k0 + i, lead, r[i], run, pend);
+        }
+    } else {
+        for (uint32_t k = 0; k < nb; k++) put_block(o, lead + k, lead, rec_top[-int(k)], run, pend);
+    }
+    if ((lead + nb) & 1u) out[nb - 1u] = BlockInfo{pend.x, pend.y};  // the last, unpaired block
+    return run - ebase;
+}
+__global__ __launch_bounds__(256) void k_gather(BatchDev b) {
+    __shared__ uint32_t s_ents;
+    if (threadIdx.x == 0) s_ents = 0;
+    __syncthreads();
+    const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
+    const uint32_t take = (s != kInvalidImage) ? b.piece_nmcu[u] : 0u;
+    uint32_t ents = 0;
+    if (take) {
+        SegInfo S;
+        seg_info(b, s, S);
+        const PieceGeo P = piece_geo(b, S, s, u);
+        const uint32_t m0 = b.piece_mcu0[u];
+        if (uint64_t(m0) + take <= S.nblk / S.bpm) {  // else corrupt counts (the chain flagged them)
+            BlockInfo* out = b.blocks + S.blk0 + uint64_t(m0) * S.bpm;
+            const uint32_t abase = b.piece_abase[u], amcu = b.piece_amcu[u], join = b.piece_join[u] & 0xFFFFu;
+            const uint32_t na = min(take, amcu);
+            ents = gather_run(out, S.eimg + abase + (P.rw - 1u), na * S.bpm, abase, true);
+            if (take > na && join) {
+                const CpRec c = b.piece_cp[size_t(u) * kCpRecords + join - 1];
+                ents += gather_run(out + na * S.bpm, S.eimg + P.own + (P.rw - 1u) - c.mcus * S.bpm, (take - na) * S.bpm,
+                                   P.own + c.ents, false);
+            }
+        }
+    }
+    const int tot = wave_scan_dpp(int(ents));
+    if ((threadIdx.x & 63u) == 63u && tot) atomicAdd(&s_ents, uint32_t(tot));
+    __syncthreads();
+    if (threadIdx.x == 0 && s_ents) atomicAdd(&b.counters[0], (unsigned long long)s_ents);
 }
 
 // DC prediction (parser.cpp:106-111: per component, the predictor restarts at 0 at every
@@ -2514,11 +2547,11 @@ __global__ void k_test_color(const int32_t* ycc, uint8_t* rgb, int n) {
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots, kWinWrite) + size_t(kPieceThreads) * kRingWords * 4; }
+size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots); }
 
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     if (!b.nimg) return hipSuccess;
-    const size_t lds = piece_lds_bytes(b.max_slots, kWinScan);
+    const size_t lds = piece_lds_bytes(b.max_slots);
     switch (k) {
         case 0:
             if (b.max_chunks) hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
@@ -2536,10 +2569,10 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             break;
         }
         case 4:
-            if (b.nsub) hipLaunchKernelGGL(k_piece<kWalkScan>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            if (b.nsub) hipLaunchKernelGGL(k_piece, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 5:
-            if (b.nsub) hipLaunchKernelGGL(k_rescan, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            if (b.nsub) hipLaunchKernelGGL(k_redo, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 6:
             if (!b.nseg) break;
@@ -2547,9 +2580,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             if (b.nchain) hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 7:
-            if (b.nsub)
-                hipLaunchKernelGGL(k_piece<kWalkWrite>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads),
-                                   piece_lds_bytes(b.max_slots, kWinWrite) + size_t(kPieceThreads) * kRingWords * 4, s, b);
+            if (b.nsub) hipLaunchKernelGGL(k_gather, dim3((b.nsub + 255) / 256), dim3(256), 0, s, b);
             break;
         case 8:
             if (!b.max_tiles) break;

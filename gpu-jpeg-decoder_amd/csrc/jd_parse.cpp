@@ -154,7 +154,7 @@ done:
 }
 
 
-bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut, bool write_pairs) {
+bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
     memset(lut, 0, sizeof(*lut));
     int code = 0, k = 0;
     int codes[256];
@@ -191,12 +191,8 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut, bool write_pairs) {
             const uint32_t e2 = one[(idx << L1) & (kLutSize - 1)], L2 = e2 & 31u;
             if (e2 == 0 || L2 > uint32_t(kLutBits) - L1) continue;  // needs bits beyond the index
             const uint32_t adv = (e2 >> 8) & 127u, sz2 = (e2 >> 16) & 15u;
-            if (write_pairs) {
-                const uint32_t sym2 = adv == 64u ? 0u : ((adv - 1u) << 4) | sz2;  // the run/size byte again
-                lut->fast[idx] = e1 | (L2 << 20) | (sym2 << 24);
-            } else {
-                lut->fast[idx] = e1 | (L2 << 22) | ((adv == 64u ? 63u : adv) << 26) | ((e2 & kEntEmit) ? kEntEmit2 : 0u);
-            }
+            const uint32_t sym2 = adv == 64u ? 0u : ((adv - 1u) << 4) | sz2;  // the run/size byte again
+            lut->fast[idx] = e1 | (L2 << 20) | (sym2 << 24);
         }
     }
     return true;

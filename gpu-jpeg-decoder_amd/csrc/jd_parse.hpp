@@ -33,8 +33,8 @@ jd_status parse_jpeg(const uint8_t* d, size_t n, ParsedJpeg* out);
 // Canonical code assignment (the reference's leftmost-first tree insertion,
 // cpp-decoder/src/huffmanTree.cpp:20-68) flattened into a LUT + canonical limits.
 // Returns false for an over-subscribed table.
-// write_pairs: the pair fields in the write walk's format (jd_internal.hpp), else the scan's.
-bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut, bool write_pairs = false);
+// AC entries carry the following symbol when both fit the index (jd_internal.hpp, HuffLut).
+bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut);
 
 // Content hash of a table (for de-duplication across a batch / across calls).
 uint64_t hash_huff(const HuffSpec& h, bool is_dc);

@@ -216,11 +216,10 @@ int lut_id(jd_ctx* ctx, const HuffSpec& s, bool is_dc, uint64_t h) {
             !memcmp(c.spec.vals, s.vals, size_t(s.nvals)))
             return it->second;
     }
-    HuffLut lut, lut_w;  // slots 2 id (scan format) and 2 id + 1 (write format)
-    if (!build_lut(s, is_dc, &lut, false) || !build_lut(s, is_dc, &lut_w, true)) return -1;
-    const int id = int(ctx->lut_host.size() / 2);
+    HuffLut lut;  // the piece walks' format (pair fields: second symbol's bits and run/size byte)
+    if (!build_lut(s, is_dc, &lut)) return -1;
+    const int id = int(ctx->lut_host.size());
     ctx->lut_host.push_back(lut);
-    ctx->lut_host.push_back(lut_w);
     ctx->lut_specs.push_back(CachedLut{s, is_dc});
     ctx->lut_by_hash.emplace(h, id);
     return id;
@@ -258,7 +257,7 @@ struct Plan {
     std::vector<int> item_of_img;
     std::vector<TableSet> tablesets;
     std::vector<uint16_t> qtabs;
-    std::vector<uint32_t> seg_img, seg_entry, wg_tableset;
+    std::vector<uint32_t> seg_img, wg_tableset;
     uint32_t piece_bits = kPieceBits, piece_overlap = kPieceOverlap;
     std::vector<uint32_t> chain_seg, chain_wg_tableset;  // k_chain lanes, grouped by table set
     uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0;
@@ -279,20 +278,38 @@ uint32_t image_mode(const ImgDesc& d) {
     return 0;
 }
 
-// Largest item prefix [lo, hi) whose sparse-coefficient slots stay within the context's
+// AC-entry region words of one image: its pieces' regions (jd_internal.hpp
+// region_words: at most ECS bits / 2 + kRegionSlack + 8 per piece slot) and spare regions for the
+// re-walks of pieces whose speculative start was wrong (~0.6 % of full-size pieces; with short
+// pieces, up to every piece).
+inline uint64_t piece_slots(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits) {
+    return (ecs_bytes * 8 + piece_bits - 1) / piece_bits + nseg;
+}
+inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits) {
+    const uint64_t bits = ecs_bytes * 8, slots = piece_slots(ecs_bytes, nseg, piece_bits);
+    const uint64_t spare = (piece_bits >= bits) ? 0 : (piece_bits >= 4096 ? slots / 16 + 8 : slots);
+    return bits / 2 + 4 + slots * (kRegionSlack + 8) + spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)));
+}
+inline uint32_t image_segments(const jd_header& h) {
+    const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
+    return h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
+}
+
+// Largest item prefix [lo, hi) whose sparse-coefficient words stay within the context's
 // max_batch_entries (default kMaxBatchEntries; entry indices are image-relative, this only bounds
-// the pool, 4 B per slot).  JD_MAX_BATCH_ENTRIES overrides it (tests force multi-way splits).
+// the pool, 4 B per word; estimated at full-size pieces).  JD_MAX_BATCH_ENTRIES overrides it
+// (tests force multi-way splits).
 constexpr uint64_t kMaxBatchEntries = 8ull << 30;
-int batch_split(jd_ctx* ctx, int lo, int n) {
+int batch_split(jd_ctx* ctx, int lo, int n, const jd_item* items) {
     const uint64_t limit = ctx->max_batch_entries;
     uint64_t cap = 0;
     int hi = lo;
     for (; hi < n; hi++) {
         if (ctx->pst[hi] != JD_OK) continue;
         const jd_header& h = ctx->parsed[hi].hdr;
-        const uint64_t blocks = uint64_t(h.mcux) * h.mcuy * h.blocks_per_mcu;
-        if (hi > lo && cap + blocks * 64 > limit) break;
-        cap += blocks * 64;
+        const uint64_t w = entry_words(items[hi].len - h.ecs_offset, image_segments(h), kPieceBits);
+        if (hi > lo && cap + w > limit) break;
+        cap += w;
     }
     return hi;
 }
@@ -369,10 +386,6 @@ void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uin
     d.comp = pi.comp;  // offset for now; rebased onto the pool in launch_batch
 }
 
-// Entry slots per MCU: 63 per block (a block stores at most 63) plus 3 for aligning piece starts
-// to 16-byte quads.
-inline uint64_t entry_slots_per_mcu(uint32_t bpm) { return uint64_t(bpm) * 63 + 3; }
-
 jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const std::vector<uint64_t>& dev_addr,
                      const std::vector<uint64_t>& out_addr, Plan& P) {
     const auto tb0 = std::chrono::steady_clock::now();
@@ -386,13 +399,13 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     const ParsedJpeg* prev = nullptr;
     int prev_ts = -1;
     uint16_t prev_qslot[3] = {0, 0, 0};
-    uint64_t block_cursor = 0, entry_cursor = 0, comp_cursor = 0;
+    uint64_t block_cursor = 0, comp_cursor = 0;
     uint32_t seg_cursor = 0, chunk_cursor = 0;
     for (int it = lo; it < hi; it++) {
         if (ctx->pst[it] != JD_OK) continue;
         const ParsedJpeg& pj = ctx->parsed[it];
         const jd_header& h = pj.hdr;
-        if (uint64_t(h.mcux) * h.mcuy * entry_slots_per_mcu(uint32_t(h.blocks_per_mcu)) > 0xFFFFFF00ull) {
+        if (entry_words(items[it].len - h.ecs_offset, image_segments(h), kMinPieceBits) > 0xFFFFFF00ull) {
             ctx->pst[it] = JD_ERR_CAPACITY;  // image-relative entry indices are 32-bit
             continue;
         }
@@ -469,13 +482,11 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         prev = &pj;
         prev_ts = ts;
         const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
-        pi.nseg = h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
+        pi.nseg = image_segments(h);
         pi.seg_base = seg_cursor;
         seg_cursor += pi.nseg;
         pi.block_base = block_cursor;
         block_cursor += nmcu * uint64_t(h.blocks_per_mcu);
-        pi.entry_base = entry_cursor;
-        entry_cursor += nmcu * entry_slots_per_mcu(uint32_t(h.blocks_per_mcu));
         const uint64_t a0 = (dev_addr[it] + uint64_t(h.ecs_offset)) & ~uint64_t(15);
         pi.nchunks = uint32_t((dev_addr[it] + items[it].len - a0 + kScanChunk - 1) / kScanChunk);
         pi.chunk_base = chunk_cursor;
@@ -496,7 +507,6 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     P.imgs.resize(nimg);
     P.item_of_img.resize(nimg);
     P.seg_img.resize(seg_cursor);
-    P.seg_entry.resize(seg_cursor);
     constexpr int kPer = 32;
     ctx->pool->run(int((nimg + kPer - 1) / kPer), [&](int t) {
         for (size_t i = size_t(t) * kPer; i < std::min(nimg, size_t(t + 1) * kPer); i++) {
@@ -504,16 +514,8 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             const ParsedJpeg& pj = ctx->parsed[pi.item];
             ImgDesc& d = P.imgs[i];
             fill_desc(pj, items[pi.item], dev_addr[pi.item], out_addr[pi.item], pi, d);
-            d.entry_base = pi.entry_base;
-            d.entry_cap = uint32_t(uint64_t(d.mcux) * d.mcuy * entry_slots_per_mcu(d.bpm));
             P.item_of_img[i] = pi.item;
-            const uint32_t nmcu = d.mcux * d.mcuy;
-            const uint64_t per = entry_slots_per_mcu(d.bpm);
-            for (uint32_t k = 0; k < d.nseg; k++) {
-                const uint32_t m0 = d.restart_interval ? k * d.restart_interval : 0u;
-                P.seg_img[d.seg_base + k] = uint32_t(i);
-                P.seg_entry[d.seg_base + k] = uint32_t(uint64_t(std::min(m0, nmcu)) * per);  // image-relative
-            }
+            for (uint32_t k = 0; k < d.nseg; k++) P.seg_img[d.seg_base + k] = uint32_t(i);
         }
     });
     std::vector<uint32_t> by_mode[4];
@@ -549,14 +551,17 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     // re-scanned (k_rescan / k_chain), which costs less than every lane walking 4096 extra bits
     P.piece_overlap = (ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES)) ? kPieceOverlap
                                                                              : std::min(kPieceOverlap, 2 * adaptive);
-    uint64_t sub = 0;
+    uint64_t sub = 0, entry_cursor = 0;
     P.chain_seg.reserve(seg_cursor + kPieceThreads * P.tablesets.size());
     for (size_t oi = 0; oi < order.size();) {
         const int ts = pim[order[oi]].ts;
         for (; oi < order.size() && pim[order[oi]].ts == ts; oi++) {
             ImgDesc& d = P.imgs[order[oi]];
             d.sub_base = uint32_t(sub);
-            d.sub_cap = uint32_t((uint64_t(d.len - d.ecs_off) * 8 + P.piece_bits - 1) / P.piece_bits + d.nseg);
+            d.sub_cap = uint32_t(piece_slots(d.len - d.ecs_off, d.nseg, P.piece_bits));
+            d.entry_base = entry_cursor;
+            d.entry_cap = uint32_t(entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits));
+            entry_cursor += align_up(size_t(d.entry_cap), 4);
             sub += d.sub_cap;
             for (uint32_t k = 0; k < d.nseg; k++) P.chain_seg.push_back(d.seg_base + k);
         }
@@ -686,7 +691,6 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_ts = put(blob, P.tablesets);
         const size_t o_q = put(blob, P.qtabs);
         const size_t o_segimg = put(blob, P.seg_img);
-        const size_t o_segent = put(blob, P.seg_entry);
         const size_t o_wgts = put(blob, P.wg_tableset);
         const size_t o_chain = put(blob, P.chain_seg);
         const size_t o_chts = put(blob, P.chain_wg_tableset);
@@ -704,8 +708,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_ssb = reserve(end, nseg * 4);
         const size_t o_sns = reserve(end, nseg * 4);
         const size_t o_subseg = reserve(end, nsub * 4);
-        size_t o_piece[6];
-        for (int q = 0; q < 6; q++) o_piece[q] = reserve(end, nsub * 4);
+        const size_t o_segent = reserve(end, nseg * 4);
+        const size_t o_pool = reserve(end, size_t(nimg) * 4);
+        size_t o_piece[9];
+        for (int q = 0; q < 9; q++) o_piece[q] = reserve(end, nsub * 4);
         const size_t o_cp = reserve(end, nsub * kCpRecords * sizeof(CpRec));
         const size_t o_fix = reserve(end, nseg * 4);
         const size_t o_tdc = reserve(end, size_t(P.total_tiles) * sizeof(DcPred));
@@ -729,7 +735,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.seg_img = reinterpret_cast<const uint32_t*>(base + o_segimg);
         b.seg_cstart = reinterpret_cast<uint32_t*>(base + o_cstart);
         b.seg_cend = reinterpret_cast<uint32_t*>(base + o_cend);
-        b.seg_entry = reinterpret_cast<const uint32_t*>(base + o_segent);
+        b.seg_ent = reinterpret_cast<uint32_t*>(base + o_segent);
+        b.img_pool = reinterpret_cast<uint32_t*>(base + o_pool);
         b.nseg = uint32_t(nseg);
         b.seg_sub_base = reinterpret_cast<uint32_t*>(base + o_ssb);
         b.seg_nsub = reinterpret_cast<uint32_t*>(base + o_sns);
@@ -741,15 +748,17 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.chain_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_chts);
         b.piece_bits = P.piece_bits;
         b.piece_overlap = P.piece_overlap;
-        uint32_t* const pc[6] = {reinterpret_cast<uint32_t*>(base + o_piece[0]), reinterpret_cast<uint32_t*>(base + o_piece[1]),
-                                 reinterpret_cast<uint32_t*>(base + o_piece[2]), reinterpret_cast<uint32_t*>(base + o_piece[3]),
-                                 reinterpret_cast<uint32_t*>(base + o_piece[4]), reinterpret_cast<uint32_t*>(base + o_piece[5])};
+        uint32_t* pc[9];
+        for (int q = 0; q < 9; q++) pc[q] = reinterpret_cast<uint32_t*>(base + o_piece[q]);
         b.piece_bit = pc[0];
         b.piece_end = pc[1];
         b.piece_nmcu = pc[2];
         b.piece_nent = pc[3];
         b.piece_mcu0 = pc[4];
-        b.piece_ent0 = pc[5];
+        b.piece_emcu = pc[5];
+        b.piece_abase = pc[6];
+        b.piece_amcu = pc[7];
+        b.piece_join = pc[8];
         b.piece_cp = reinterpret_cast<CpRec*>(base + o_cp);
         b.seg_fix = reinterpret_cast<uint32_t*>(base + o_fix);
         b.tile_dc = reinterpret_cast<DcPred*>(base + o_tdc);
@@ -865,10 +874,11 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
             pd.chunks * 12 + nsegd * 8,                        // k_index: per-chunk counters, boundaries
             2 * ecs,                                           // k_compact: read + write the ECS
             nsubd * 4 + nsegd * 16,                            // k_subplan: piece map
-            ecs * std::min(overlap_factor, 2.0) + nsubd * 16,  // k_piece_scan: bits incl. overlap, counts out
-            nsubd * 8,                                         // k_rescan: start/end check per piece
-            nsubd * 28,                                        // k_chain: counts in, offsets out
-            ecs + blocks * 8 + entries * 4,                    // k_piece_write: ECS in, sparse coefficients out
+            ecs * std::min(overlap_factor, 2.0) + blocks * 4 + entries * 4 + nsubd * 32,  // k_piece: bits incl.
+                                                               // warm-up in, records + AC entries + counts out
+            nsubd * 8,                                         // k_redo: start/end check per piece
+            nsubd * 20,                                        // k_chain: counts in, first MCU / count out
+            blocks * 12 + nsubd * 24,                          // k_gather: records in, BlockInfo out
             blocks * 8 + pd.tiles * 48,                        // k_dc_pred: BlockInfo read, tile sums, scan
             blocks * 8 + entries * 4 + (fancy ? blocks * 128 : pd.pixels * 3),  // k_idct_color: coefficients
                                                                                  // in, RGB (fancy: planes) out
@@ -942,8 +952,8 @@ const char* jd_status_str(jd_status st) {
 const char* jd_ctx_last_error(jd_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
 
 const char* jd_kernel_name(int k) {
-    static const char* names[JD_NUM_KERNELS] = {"k_scan",      "k_index", "k_compact",     "k_subplan", "k_piece_scan",
-                                                "k_rescan",    "k_chain", "k_piece_write", "k_dc_pred", "k_idct_color", "k_colour_fancy"};
+    static const char* names[JD_NUM_KERNELS] = {"k_scan",  "k_index", "k_compact", "k_subplan",    "k_piece",       "k_redo",
+                                                "k_chain", "k_gather", "k_dc_pred", "k_idct_color", "k_colour_fancy"};
     return (k >= 0 && k < JD_NUM_KERNELS) ? names[k] : "?";
 }
 
@@ -1044,7 +1054,7 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
         std::fprintf(stderr, "host parse %.3f ms\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     for (int lo = 0; lo < n;) {
-        const int hi = batch_split(ctx, lo, n);
+        const int hi = batch_split(ctx, lo, n, items);
         jd_status st = launch_batch(ctx, items, lo, hi, results, rgb_on_device, s);
         if (st != JD_OK) return st;
         if (async) {  // collect the previous launch (its slot is the current one now)
@@ -1204,9 +1214,13 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
         case 10: src = b.status; n = size_t(b.nimg) * 4; break;
         case 11: src = b.entries; n = ctx->last_entries * 4; break;
         case 12: src = b.piece_mcu0; n = size_t(b.nsub) * 4; break;
-        case 13: src = b.piece_ent0; n = size_t(b.nsub) * 4; break;
+        case 13: src = b.piece_abase; n = size_t(b.nsub) * 4; break;
         case 14: src = b.piece_cp; n = size_t(b.nsub) * kCpRecords * sizeof(CpRec); break;
         case 15: src = b.stamps; n = b.stamps ? size_t(b.total_tiles) * 64 : 0; break;
+        case 16: src = b.piece_emcu; n = size_t(b.nsub) * 4; break;
+        case 17: src = b.piece_amcu; n = size_t(b.nsub) * 4; break;
+        case 18: src = b.piece_join; n = size_t(b.nsub) * 4; break;
+        case 19: src = b.seg_ent; n = size_t(b.nseg) * 4; break;
         default: return JD_ERR_INVALID_ARG;
     }
     *nbytes = n;

@@ -35,8 +35,8 @@ JD_FLAG_FULL_PIECES = 16
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES, "full": JD_FLAG_FULL_PIECES}
 JD_ABI_VERSION = 4
 JD_NUM_KERNELS = 11
-KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece_scan", "k_rescan", "k_chain",
-                "k_piece_write", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
+KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece", "k_redo", "k_chain",
+                "k_gather", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
 
 
 class JDError(RuntimeError):
@@ -377,8 +377,9 @@ class Decoder:
                     "seg_sub_base": (3, np.uint32, 1), "seg_nsub": (4, np.uint32, 1), "piece_bit": (5, np.uint32, 1),
                     "piece_end": (6, np.uint32, 1), "piece_nmcu": (7, np.uint32, 1), "piece_nent": (8, np.uint32, 1),
                     "sub_seg": (9, np.uint32, 1), "status": (10, np.uint32, 1), "entries": (11, np.uint32, 1),
-                    "piece_mcu0": (12, np.uint32, 1), "piece_ent0": (13, np.uint32, 1),
-                    "piece_cp": (14, np.uint32, 36), "stamps": (15, np.uint64, 8)}
+                    "piece_mcu0": (12, np.uint32, 1), "piece_abase": (13, np.uint32, 1),
+                    "piece_cp": (14, np.uint32, 36), "stamps": (15, np.uint64, 8), "piece_emcu": (16, np.uint32, 1),
+                    "piece_amcu": (17, np.uint32, 1), "piece_join": (18, np.uint32, 1), "seg_ent": (19, np.uint32, 1)}
 
     def debug_fetch(self, name: str) -> np.ndarray:
         """Internal array of the most recent batch (white-box tests and debugging)."""

@@ -156,8 +156,8 @@ jd_status jd_memcpy_d2h(jd_ctx* ctx, void* dst_host, const void* src_dev, size_t
 jd_status jd_synchronize(jd_ctx* ctx);
 
 /* Per-kernel timing (JD_FLAG_TIMING).
- * Kernels: 0 k_scan, 1 k_index, 2 k_compact, 3 k_subplan, 4 k_piece_scan, 5 k_rescan, 6 k_chain,
- * 7 k_piece_write, 8 k_dc_pred, 9 k_idct_color. */
+ * Kernels: 0 k_scan, 1 k_index, 2 k_compact, 3 k_subplan, 4 k_piece, 5 k_redo, 6 k_chain,
+ * 7 k_gather, 8 k_dc_pred, 9 k_idct_color, 10 k_colour_fancy. */
 #define JD_NUM_KERNELS 11
 typedef struct jd_stats {
     int launches[JD_NUM_KERNELS];

@@ -4,8 +4,8 @@ The decoder uses 1024-bit pieces here (path="sync"), so many pieces start specul
 some need the chain's re-scan.
 
   seg_cstart/seg_cend          -> un-stuffed interval lengths
-  piece_bit/mcu0/ent0          -> every piece starts on a true MCU boundary, with the right MCU
-                                  index and AC-entry offset
+  piece_bit/mcu0/abase         -> every piece starts on a true MCU boundary, with the right MCU
+                                  index; its blocks come from its own region (or a spare one)
   blocks                       -> per-block AC-entry counts and DC differences vs the oracle
                                   (the DC predictor itself runs inside k_idct_color)
 """
@@ -48,8 +48,9 @@ def test_intervals_and_piece_starts(sync_decoder, name):
     pbit = sync_decoder.debug_fetch("piece_bit")
     pm0 = sync_decoder.debug_fetch("piece_mcu0")
     pnm = sync_decoder.debug_fetch("piece_nmcu")
-    pe0 = sync_decoder.debug_fetch("piece_ent0")
-    prev_e0 = prev_e = 0
+    pab = sync_decoder.debug_fetch("piece_abase")
+    pjoin = sync_decoder.debug_fetch("piece_join")
+    sent = sync_decoder.debug_fetch("seg_ent")
     errs = []
     for s, seg in enumerate(truth):
         if (int(ce[s]) - int(cs[s])) * 8 != seg["bits"]:
@@ -59,6 +60,8 @@ def test_intervals_and_piece_starts(sync_decoder, name):
         if int(nsub[s]) != want_n:
             errs.append(f"seg {s}: pieces gpu {nsub[s]} want {want_n}")
             continue
+        plen = -(-seg["bits"] // want_n)
+        rw = ((plen + 1) // 2 + 1040 + 3) // 4 * 4  # jd_internal.hpp region_words
         starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
         nm = 0
         for j in range(want_n):
@@ -70,11 +73,12 @@ def test_intervals_and_piece_starts(sync_decoder, name):
             m, e = starts[b]
             if int(pm0[u]) != m and not (j == want_n - 1 and int(pnm[u]) == 0):
                 errs.append(f"seg {s} piece {j}: mcu0 gpu {pm0[u]} want {m}")
-            # every piece's first entry slot is the previous piece's end rounded up to a quad
-            want_e0 = (prev_e0 + (e - prev_e) + 3) // 4 * 4 if j > 0 else int(pe0[u])
-            if int(pe0[u]) != want_e0 or int(pe0[u]) % 4:
-                errs.append(f"seg {s} piece {j}: ent0 gpu {int(pe0[u])} want {want_e0}")
-            prev_e0, prev_e = int(pe0[u]), e
+            # segment A: the piece's own region, or (re-walked) a spare region past every own one
+            own = int(sent[s]) + j * rw
+            if int(pab[u]) != own and int(pab[u]) < own + rw:
+                errs.append(f"seg {s} piece {j}: region {int(pab[u])} overlaps own {own}")
+            if (int(pjoin[u]) & 0xFFFF) > (int(pjoin[u]) >> 16):
+                errs.append(f"seg {s} piece {j}: joined checkpoint {int(pjoin[u]) & 0xFFFF} of {int(pjoin[u]) >> 16}")
             nm += int(pnm[u])
         if nm != len(seg["starts"]) - 1:
             errs.append(f"seg {s}: MCUs gpu {nm} want {len(seg['starts']) - 1}")
@@ -85,8 +89,8 @@ def test_intervals_and_piece_starts(sync_decoder, name):
 
 @pytest.mark.parametrize("name", CASES)
 def test_scan_checkpoints(sync_decoder, name):
-    """Checkpoints (k_piece scan) sit on true MCU boundaries with the counts from the piece start,
-    for every piece whose speculative start synchronised (the join shortcut relies on both)."""
+    """Checkpoints (k_piece) sit on true MCU boundaries with the MCU and AC-entry counts from the
+    piece start, for every piece whose speculative start synchronised (the join relies on both)."""
     data = _load(name)
     try:
         sync_decoder.decode(data)
@@ -97,13 +101,13 @@ def test_scan_checkpoints(sync_decoder, name):
     nsub = sync_decoder.debug_fetch("seg_nsub")
     pbit = sync_decoder.debug_fetch("piece_bit")
     cp = sync_decoder.debug_fetch("piece_cp").reshape(-1, 9, 4)
+    pjoin = sync_decoder.debug_fetch("piece_join")
     checked = bad = 0
     for s, seg in enumerate(truth):
         starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
         for j in range(int(nsub[s])):
             u = int(ssb[s]) + j
-            tot = cp[u, 8]
-            ncp = int(tot[3]) >> 8
+            ncp = int(pjoin[u]) >> 16
             assert ncp <= 8
             b0 = int(pbit[u])
             if b0 not in starts or ncp == 0:
@@ -116,7 +120,7 @@ def test_scan_checkpoints(sync_decoder, name):
                 else:
                     bad += 1
     # a piece whose speculative start did not synchronise records its checkpoints on a wrong
-    # trajectory (k_rescan ignores them unless it meets one at an MCU boundary)
+    # trajectory (k_redo ignores them unless it meets one at an MCU boundary)
     assert checked > 0 and bad <= checked // 20, (checked, bad)
 
 

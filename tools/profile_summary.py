@@ -46,7 +46,7 @@ out = {"config": a.config, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, s
        "kernels": {}}
 for k in sorted(set(fetch) | set(write)):
     name = k.split("(")[0].replace("void ", "").replace("jd::", "")
-    name = {"k_piece<0>": "k_piece_scan", "k_piece<1>": "k_piece_write"}.get(name, name)
+    name = name
     f, w = fetch.get(k, 0.0), write.get(k, 0.0)
     out["kernels"][name] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes": 2 * f + w}
 with open(os.path.join(prof, f"{a.tag}_traffic.json"), "w") as fh:

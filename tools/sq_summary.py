@@ -26,7 +26,7 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(a.run_dir, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("jd::", "")
-        k = {"k_piece<0>": "k_piece_scan", "k_piece<1>": "k_piece_write"}.get(k, k)
+        k = k
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
             vals[k]["_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
