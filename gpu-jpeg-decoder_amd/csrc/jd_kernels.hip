@@ -1235,75 +1235,97 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
     if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
 }
 
-// Lane per piece: the piece's block records -> BlockInfo at the blocks' global positions, entry
-// offsets by a running sum of the records' counts.  Segment A (the piece's own region, or a
-// re-walk's spare region) first, then segment B (the own region from the joined checkpoint on).
-// Segment A's records are read as aligned quads (a region starts and ends on a quad, so its top
-// record is the last word of one), two quads in flight; BlockInfo leaves in pairs (16-byte stores)
-// once the output index is even.  Segment B (rare: joined re-walks) reads word by word.
-__device__ __forceinline__ void put_block(BlockInfo* out, uint32_t k, uint32_t lead, uint32_t r, uint32_t& run, uint2& pend) {
-    const uint32_t cnt = r >> 16;
-    const uint2 v = make_uint2(run, pack_cnt_dc(cnt, int(int16_t(r & 0xFFFFu))));
-    run += cnt;
-    if (k == 1u && lead) {  // the first block sits at an odd index: alone
-        out[1] = BlockInfo{v.x, v.y};
-    } else if (k & 1u) {
-        if (!(JD_ABL & 32) || run == 0x7FFFFFFFu)
-            *reinterpret_cast<uint4*>(out + (k - 1u)) = make_uint4(pend.x, pend.y, v.x, v.y);
-    } else {
-        pend = v;
-    }
+// k_gather: a piece's block records -> BlockInfo at the blocks' global positions, AC-entry offsets
+// by a prefix sum of the records' counts.  Segment A (the piece's own region, or a re-walk's spare
+// region) comes first, then segment B (the own region from the joined checkpoint on).
+// A wave takes 64 consecutive pieces: their descriptors lane-parallel, then four pieces at a time,
+// one per row of 16 lanes; lane t of a row handles records t, t + 16, ... of its piece, so every
+// load (64 B per row) and store (128 B per row) is contiguous, with eight loads in flight per lane.
+__device__ __forceinline__ int row_scan_dpp(int x) {  // inclusive, within each row of 16 lanes
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    return x;
 }
-__device__ __forceinline__ uint32_t gather_run(BlockInfo* out, const uint32_t* rec_top, uint32_t nb, uint32_t ebase,
-                                               bool aligned) {
+constexpr int kGatherLoads = 8;
+__device__ __forceinline__ uint32_t gather_rows(BlockInfo* out, const uint32_t* rec_top, uint32_t n, uint32_t ebase,
+                                                uint32_t lane) {
+    const uint32_t t = lane & 15u, last = lane | 15u;
     uint32_t run = ebase;
-    uint2 pend = make_uint2(0u, 0u);
-    // out is addressed by block parity from here on: index k of `out` is even iff it starts a pair
-    const uint32_t lead = uint32_t(reinterpret_cast<uintptr_t>(out) >> 3) & 1u;
-    BlockInfo* o = out - lead;
-    if (aligned) {
-        const uint4* q = reinterpret_cast<const uint4*>(rec_top - 3);  // records 0..3 = .w .z .y .x
-        for (uint32_t k0 = 0; k0 < nb; k0 += 8) {
-            const uint4 a = q[-int(k0 >> 2)];
-            const uint4 c = (k0 + 4 < nb) ? q[-int(k0 >> 2) - 1] : make_uint4(0, 0, 0, 0);
-            const uint32_t r[8] = {a.w, a.z, a.y, a.x, c.w, c.z, c.y, c.x};
+    for (uint32_t k0 = 0; __any(k0 < n); k0 += 16 * kGatherLoads) {  // wave-uniform trip count
+        uint32_t r[kGatherLoads];
 #pragma unroll
-            for (int i = 0; i < 8; i++)
-                if (k0 + i < nb) put_block(o, lead + k0 + i, lead, r[i], run, pend);
+        for (int i = 0; i < kGatherLoads; i++) {
+            const uint32_t k = k0 + t + 16u * i;
+            r[i] = (k < n && !(JD_ABL & 64)) ? rec_top[-int(k)] : 0u;
         }
-    } else {
-        for (uint32_t k = 0; k < nb; k++) put_block(o, lead + k, lead, rec_top[-int(k)], run, pend);
+#pragma unroll
+        for (int i = 0; i < kGatherLoads; i++) {
+            const uint32_t k = k0 + t + 16u * i;
+            const uint32_t cnt = r[i] >> 16;
+            const uint32_t incl = uint32_t(row_scan_dpp(int(cnt)));
+            if (k < n && (!(JD_ABL & 32) || run == 0x7FFFFFFFu))
+                out[k] = BlockInfo{run + incl - cnt, pack_cnt_dc(cnt, int(int16_t(r[i] & 0xFFFFu)))};
+            run += uint32_t(__shfl(int(incl), int(last), 64));
+        }
     }
-    if ((lead + nb) & 1u) out[nb - 1u] = BlockInfo{pend.x, pend.y};  // the last, unpaired block
     return run - ebase;
 }
 __global__ __launch_bounds__(256) void k_gather(BatchDev b) {
     __shared__ uint32_t s_ents;
     if (threadIdx.x == 0) s_ents = 0;
     __syncthreads();
-    const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t u = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + lane;
+    // 1. descriptors, lane = piece
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
     const uint32_t take = (s != kInvalidImage) ? b.piece_nmcu[u] : 0u;
-    uint32_t ents = 0;
+    uint32_t nA = 0, nB = 0, topA = 0, eA = 0, topB = 0, eB = 0;
+    uint64_t outi = 0, eimg = 0;
     if (take) {
         SegInfo S;
         seg_info(b, s, S);
         const PieceGeo P = piece_geo(b, S, s, u);
         const uint32_t m0 = b.piece_mcu0[u];
         if (uint64_t(m0) + take <= S.nblk / S.bpm) {  // else corrupt counts (the chain flagged them)
-            BlockInfo* out = b.blocks + S.blk0 + uint64_t(m0) * S.bpm;
+            outi = S.blk0 + uint64_t(m0) * S.bpm;
+            eimg = uint64_t(reinterpret_cast<uintptr_t>(S.eimg));
             const uint32_t abase = b.piece_abase[u], amcu = b.piece_amcu[u], join = b.piece_join[u] & 0xFFFFu;
             const uint32_t na = min(take, amcu);
-            ents = gather_run(out, S.eimg + abase + (P.rw - 1u), na * S.bpm, abase, true);
+            nA = na * S.bpm;
+            eA = abase;
+            topA = abase + P.rw - 1u;
             if (take > na && join) {
                 const CpRec c = b.piece_cp[size_t(u) * kCpRecords + join - 1];
-                ents += gather_run(out + na * S.bpm, S.eimg + P.own + (P.rw - 1u) - c.mcus * S.bpm, (take - na) * S.bpm,
-                                   P.own + c.ents, false);
+                nB = (take - na) * S.bpm;
+                eB = P.own + c.ents;
+                topB = P.own + P.rw - 1u - c.mcus * S.bpm;
             }
         }
     }
+    // 2. four pieces at a time, one per row
+    const uint64_t busy = __ballot(nA + nB > 0);
+    const uint32_t row = lane >> 4;
+    uint32_t ents = 0;
+    for (uint32_t g = 0; g < 16; g++) {
+        if (!((busy >> (4 * g)) & 0xFull)) continue;  // wave-uniform
+        const int p = int(4 * g + row);
+        const uint32_t pnA = __shfl(nA, p, 64), pnB = __shfl(nB, p, 64);
+        const uint32_t ptA = __shfl(topA, p, 64), peA = __shfl(eA, p, 64);
+        const uint32_t ptB = __shfl(topB, p, 64), peB = __shfl(eB, p, 64);
+        const uint64_t po = (uint64_t(uint32_t(__shfl(uint32_t(outi >> 32), p, 64))) << 32) |
+                            uint32_t(__shfl(uint32_t(outi), p, 64));
+        const uint64_t pe = (uint64_t(uint32_t(__shfl(uint32_t(eimg >> 32), p, 64))) << 32) |
+                            uint32_t(__shfl(uint32_t(eimg), p, 64));
+        const uint32_t* eptr = reinterpret_cast<const uint32_t*>(uintptr_t(pe));
+        BlockInfo* out = b.blocks + po;
+        uint32_t e = gather_rows(out, eptr + ptA, pnA, peA, lane);
+        if (__any(pnB > 0)) e += gather_rows(out + pnA, eptr + ptB, pnB, peB, lane);
+        ents += (lane & 15u) == 0u ? e : 0u;
+    }
     const int tot = wave_scan_dpp(int(ents));
-    if ((threadIdx.x & 63u) == 63u && tot) atomicAdd(&s_ents, uint32_t(tot));
+    if (lane == 63u && tot) atomicAdd(&s_ents, uint32_t(tot));
     __syncthreads();
     if (threadIdx.x == 0 && s_ents) atomicAdd(&b.counters[0], (unsigned long long)s_ents);
 }
@@ -2580,7 +2602,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             if (b.nchain) hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 7:
-            if (b.nsub) hipLaunchKernelGGL(k_gather, dim3((b.nsub + 255) / 256), dim3(256), 0, s, b);
+            if (b.nsub) hipLaunchKernelGGL(k_gather, dim3((b.nsub + 255) / 256), dim3(256), 0, s, b);  // 64 pieces per wave
             break;
         case 8:
             if (!b.max_tiles) break;
