@@ -115,9 +115,13 @@ class Pool {
 }  // namespace
 
 // One launched batch whose results are not collected yet (jd_decode_batch_async keeps two in
-// flight: the host plans batch k+1 while the GPU decodes batch k).
+// flight: the host plans batch k+1 while the GPU decodes batch k).  Each slot owns its device
+// scratch and, unless the caller names a stream, its own stream, so batch k+1's first kernels
+// run beside batch k's latency-bound tail (re-walks, chain, DC scan).
 struct Pending {
     bool active = false;
+    hipStream_t stream = nullptr;               // this slot's internal stream
+    DevBuf d_plan, d_brk, d_blocks, d_entries, d_comp, d_planes, d_stamps;  // device scratch of the batch
     jd_result* results = nullptr;
     int lo = 0, hi = 0;
     std::vector<jd_status> pst;                 // per item lo..hi: host-side status
@@ -152,13 +156,13 @@ struct jd_ctx {
     DevBuf lut_dev;
     size_t lut_dev_count = 0;
 
-    // pools
-    DevBuf plan, chunk_brk, blocks, entries, input, output, comp, planes, stamps;
+    // pools shared by the slots (host inputs / outputs: collected before reuse)
+    DevBuf input, output;
     PinBuf input_host;
 
     Pending pend[2];
     int slot = 0;  // the slot the next launch uses
-    hipStream_t last_stream = nullptr;  // stream of the pending launches (scratch pools are ordered on it)
+    const void* last_stream = nullptr;  // caller stream of the pending launches (nullptr: the slots' own)
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     jd_stats stats{};
 
@@ -664,8 +668,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     if (st != JD_OK) return st;
     const uint32_t nimg = uint32_t(P.imgs.size());
     if (nimg) {
-        HIPCHK(ctx, ensure_dev(ctx->comp, std::max<size_t>(16, P.comp_bytes)));
-        for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(ctx->comp.p);
+        HIPCHK(ctx, ensure_dev(pd.d_comp, std::max<size_t>(16, P.comp_bytes)));
+        for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(pd.d_comp.p);
         const bool fancy = (ctx->flags & JD_FLAG_FANCY_UPSAMPLING) != 0;
         uint32_t max_fancy_wgs = 0;
         if (fancy) {  // int16 component planes over the padded MCU grid, 256-B aligned per image
@@ -680,9 +684,9 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
                 const uint64_t groups = uint64_t((d.width + 7) / 8) * d.height;
                 max_fancy_wgs = std::max<uint32_t>(max_fancy_wgs, uint32_t((groups + 255) / 256));
             }
-            HIPCHK(ctx, ensure_dev(ctx->planes, std::max<size_t>(16, tot)));
+            HIPCHK(ctx, ensure_dev(pd.d_planes, std::max<size_t>(16, tot)));
             for (size_t i = 0; i < P.imgs.size(); i++)
-                P.imgs[i].planes = reinterpret_cast<uint64_t>(ctx->planes.p) + poff[i];
+                P.imgs[i].planes = reinterpret_cast<uint64_t>(pd.d_planes.p) + poff[i];
         }
         std::vector<uint8_t> blob;
         const size_t nseg = P.seg_img.size();
@@ -716,15 +720,15 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_fix = reserve(end, nseg * 4);
         const size_t o_tdc = reserve(end, size_t(P.total_tiles) * sizeof(DcPred));
         const size_t o_slow = reserve(end, size_t(P.total_tiles) * 8);
-        HIPCHK(ctx, ensure_dev(ctx->plan, end));
+        HIPCHK(ctx, ensure_dev(pd.d_plan, end));
         HIPCHK(ctx, ensure_pinned(pd.plan_host, pd.plan_cap, upload));
         memcpy(pd.plan_host, blob.data(), upload);
-        HIPCHK(ctx, hipMemcpyAsync(ctx->plan.p, pd.plan_host, upload, hipMemcpyHostToDevice, s));
-        HIPCHK(ctx, ensure_dev(ctx->chunk_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
-        HIPCHK(ctx, ensure_dev(ctx->blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
-        HIPCHK(ctx, ensure_dev(ctx->entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
+        HIPCHK(ctx, hipMemcpyAsync(pd.d_plan.p, pd.plan_host, upload, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, ensure_dev(pd.d_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
+        HIPCHK(ctx, ensure_dev(pd.d_blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
+        HIPCHK(ctx, ensure_dev(pd.d_entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
 
-        uint8_t* base = static_cast<uint8_t*>(ctx->plan.p);
+        uint8_t* base = static_cast<uint8_t*>(pd.d_plan.p);
         BatchDev b;
         memset(&b, 0, sizeof(b));
         b.imgs = reinterpret_cast<const ImgDesc*>(base + o_imgs);
@@ -769,10 +773,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.chunk_nbrk = reinterpret_cast<uint32_t*>(base + o_nbrk);
         b.chunk_drops = reinterpret_cast<uint32_t*>(base + o_drops);
         b.chunk_coff = reinterpret_cast<uint32_t*>(base + o_coff);
-        b.chunk_brk = static_cast<Break*>(ctx->chunk_brk.p);
-        b.blocks = static_cast<BlockInfo*>(ctx->blocks.p);
-        b.entries = static_cast<uint32_t*>(ctx->entries.p);
-        b.entries_cap = (ctx->entries.cap - 64) / 4;  // last 64 B: padding for 16-byte over-reads
+        b.chunk_brk = static_cast<Break*>(pd.d_brk.p);
+        b.blocks = static_cast<BlockInfo*>(pd.d_blocks.p);
+        b.entries = static_cast<uint32_t*>(pd.d_entries.p);
+        b.entries_cap = (pd.d_entries.cap - 64) / 4;  // last 64 B: padding for 16-byte over-reads
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
         b.max_tiles = P.max_tiles;
@@ -783,9 +787,9 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             b.mode_max_tiles[m] = P.mode_max_tiles[m];
         }
         if (std::getenv("JD_STAMPS")) {  // diagnostic builds (JD_STAMP): per-tile phase stamps
-            HIPCHK(ctx, ensure_dev(ctx->stamps, size_t(P.total_tiles) * 64));
-            HIPCHK(ctx, hipMemsetAsync(ctx->stamps.p, 0, size_t(P.total_tiles) * 64, s));
-            b.stamps = static_cast<unsigned long long*>(ctx->stamps.p);
+            HIPCHK(ctx, ensure_dev(pd.d_stamps, size_t(P.total_tiles) * 64));
+            HIPCHK(ctx, hipMemsetAsync(pd.d_stamps.p, 0, size_t(P.total_tiles) * 64, s));
+            b.stamps = static_cast<unsigned long long*>(pd.d_stamps.p);
         }
         b.fancy = fancy ? 1u : 0u;
         b.max_fancy_wgs = max_fancy_wgs;
@@ -980,7 +984,8 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
         return JD_ERR_HIP;
     }
     for (Pending& pd : ctx->pend) {
-        bool ok = hipEventCreateWithFlags(&pd.done, hipEventDisableTiming) == hipSuccess;
+        bool ok = hipStreamCreateWithFlags(&pd.stream, hipStreamNonBlocking) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&pd.done, hipEventDisableTiming) == hipSuccess;
         for (int k = 0; k < JD_NUM_KERNELS; k++)
             for (int j = 0; j < 2; j++) ok = ok && hipEventCreate(&pd.ev[k][j]) == hipSuccess;
         if (!ok) {
@@ -995,12 +1000,14 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
 jd_status jd_ctx_destroy(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->lut_dev, &ctx->plan, &ctx->chunk_brk, &ctx->blocks, &ctx->entries, &ctx->input, &ctx->output,
-                       &ctx->comp, &ctx->planes, &ctx->stamps})
+    (void)hipDeviceSynchronize();
+    for (DevBuf* b : {&ctx->lut_dev, &ctx->input, &ctx->output})
         if (b->p) (void)hipFree(b->p);
     if (ctx->input_host.p) (void)hipHostFree(ctx->input_host.p);
     for (Pending& pd : ctx->pend) {
+        for (DevBuf* b : {&pd.d_plan, &pd.d_brk, &pd.d_blocks, &pd.d_entries, &pd.d_comp, &pd.d_planes, &pd.d_stamps})
+            if (b->p) (void)hipFree(b->p);
+        if (pd.stream) (void)hipStreamDestroy(pd.stream);
         if (pd.host) (void)hipHostFree(pd.host);
         if (pd.plan_host) (void)hipHostFree(pd.plan_host);
         if (pd.done) (void)hipEventDestroy(pd.done);
@@ -1031,13 +1038,12 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
     for (int i = 0; i < n; i++)
         if (!items[i].jpeg || items[i].len > 0xFFFFFFF0ull) return JD_ERR_INVALID_ARG;
     if (hipSetDevice(ctx->device) != hipSuccess) return JD_ERR_HIP;
-    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
-    // The scratch pools (plan, pieces, blocks, entries ...) are ordered by the stream alone: a
-    // launch on another stream than the pending batches' first collects them.
-    if (s != ctx->last_stream) {
+    // Without a caller stream each slot runs on its own stream; a caller stream orders both slots.
+    // Switching streams first collects the pending batches.
+    if (hip_stream != ctx->last_stream) {
         const jd_status st = finish_all(ctx);
         if (st != JD_OK) return st;
-        ctx->last_stream = s;
+        ctx->last_stream = hip_stream;
     }
     // The host input staging buffer and the output pool are reused per launch: with host inputs
     // or host outputs, collect first, and collect every sub-batch before launching the next.
@@ -1055,6 +1061,7 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     for (int lo = 0; lo < n;) {
         const int hi = batch_split(ctx, lo, n, items);
+        hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->pend[ctx->slot].stream;
         jd_status st = launch_batch(ctx, items, lo, hi, results, rgb_on_device, s);
         if (st != JD_OK) return st;
         if (async) {  // collect the previous launch (its slot is the current one now)
@@ -1225,7 +1232,7 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
     }
     *nbytes = n;
     if (dst && src && n) {
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, hipDeviceSynchronize());  // the last batch ran on a slot's stream
         HIPCHK(ctx, hipMemcpy(dst, src, std::min(n, cap), hipMemcpyDeviceToHost));
     }
     return JD_OK;
