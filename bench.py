@@ -365,6 +365,8 @@ def main():
     ap.add_argument("--verify", type=int, default=1, help="check images {0, n/2, n-1} bit-exact vs the oracle")
     ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the H2D-inclusive run (0: skip)")
     ap.add_argument("--copy-peak", type=int, default=1, help="measure an in-run HBM copy peak")
+    ap.add_argument("--kernel-steps", type=int, default=3,
+                    help="serialized (non-overlapped) steps after the timed region for per-kernel times")
     ap.add_argument("--path", default="auto", choices=["auto", "sync", "lanes", "full"],
                     help="entropy-decode path (auto: lanes for images with restart intervals)")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -462,6 +464,13 @@ def main():
     elapsed = time.perf_counter() - t0
     if args.verify and any(r.status for b in batches for r in b[1]):  # the last timed batches' statuses
         raise SystemExit("decode failed inside the timed region")
+    st_overlap = dec.stats()
+    # per-kernel times for the roofline from serialized batches (outside the timed region): in the
+    # timed loop consecutive batches overlap on the slot streams, so a kernel's hipEvent span there
+    # includes the other batch's kernels
+    dec.reset_stats()
+    for k in range(max(1, args.kernel_steps)):
+        dec.decode_prepared(batches[k & 1], pipelined=False)
     st = dec.stats()
 
     # PCIe-inclusive rate (not `value`): the JPEG bytes handed over in host memory, RGB to HBM
@@ -536,8 +545,11 @@ def main():
                          "measured_copy_peak": copy_gbs,
                          "frac_of_measured_peak": achieved / copy_gbs if copy_gbs else None,
                          "valu": valu_issue(args.config, dom, avg_ms),
-                         "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
+                         "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes,
+                         "timing": f"hipEvents on the decode stream, {max(1, args.kernel_steps)} serialized batches"},
             "kernels_ms_per_step": {k: v["total_ms"] / max(1, v["launches"]) for k, v in kern.items()},
+            "kernels_ms_per_step_overlapped": {k: v["total_ms"] / max(1, v["launches"])
+                                               for k, v in st_overlap["kernels"].items()},
             "path_roofline_frac": ((ecs + 3 * pixels) / (t_max / args.steps) / 1e9) / HBM_PEAK_GBS,
             "e2e_h2d": e2e,
             "cpu_baseline": cpu,

@@ -132,12 +132,14 @@ struct Break {
 constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
 
 // Huffman decode geometry: every interval is cut into pieces of piece_bits un-stuffed bits, one
-// lane each; a piece's scan synchronises from piece_overlap bits before its start (jd_kernels.hip
-// Stage 3; reference: parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208).  4:2:0 MCU
-// phase needs a few thousand bits to lock: speculative starts failed 45 % / 12 % / 0 % of the
-// time at 1024 / 2048 / 4096 bits on the bench images (tools/jd_trace.py emulate()).
+// lane each; a piece's walk synchronises from piece_overlap bits before its start (jd_kernels.hip
+// k_piece; reference: parallelHuffManDecode, cuda-decoder/src/parser.cu:132-208).  4:2:0 MCU
+// phase needs a few thousand bits to lock: speculative starts failed 45 % / 12 % / 0.6 % of the
+// time at 1024 / 2048 / 4096 bits on the bench images (tools/jd_trace.py emulate()).  16384-bit
+// pieces (the warm-up is a fifth of a lane's walk) measured best against 8192 / 24576 / 32768 on
+// C2, C3 and C5 once consecutive batches overlap (their longer tails are hidden).
 #ifndef JD_PIECE_BITS
-#define JD_PIECE_BITS 8192
+#define JD_PIECE_BITS 16384
 #endif
 #ifndef JD_PIECE_OVERLAP
 #define JD_PIECE_OVERLAP 4096
