@@ -1035,7 +1035,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
         ncp = b.piece_join[u] >> 16;
         tot = cp[kCpMax];
         const uint32_t img = b.seg_img[s];
-        const uint32_t a = atomicAdd(&b.img_pool[img], P.rw);
+        const uint32_t a = b.no_pool ? 0xFFFFFFFFu : atomicAdd(&b.img_pool[img], P.rw);
         if (uint64_t(a) + P.rw <= b.imgs[img].entry_cap) base = a;
         else ncp = 0;  // in place
     }

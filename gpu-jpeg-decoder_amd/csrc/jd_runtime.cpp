@@ -164,6 +164,8 @@ struct jd_ctx {
     int slot = 0;  // the slot the next launch uses
     const void* last_stream = nullptr;  // caller stream of the pending launches (nullptr: the slots' own)
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
+    int64_t spare_pieces = -1;          // spare re-walk regions per image (JD_SPARE_PIECES; -1: default)
+    int64_t piece_overlap = -1;         // warm-up bits (JD_PIECE_OVERLAP_BITS; -1: default)
     jd_stats stats{};
 
     std::vector<ParsedJpeg> parsed;
@@ -289,9 +291,10 @@ uint32_t image_mode(const ImgDesc& d) {
 inline uint64_t piece_slots(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits) {
     return (ecs_bytes * 8 + piece_bits - 1) / piece_bits + nseg;
 }
-inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits) {
+inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits, int64_t spare_pieces = -1) {
     const uint64_t bits = ecs_bytes * 8, slots = piece_slots(ecs_bytes, nseg, piece_bits);
-    const uint64_t spare = (piece_bits >= bits) ? 0 : (piece_bits >= 4096 ? slots / 16 + 8 : slots);
+    uint64_t spare = (piece_bits >= bits) ? 0 : (piece_bits >= 4096 ? slots / 16 + 8 : slots);
+    if (spare_pieces >= 0) spare = uint64_t(spare_pieces);  // JD_SPARE_PIECES (tests: in-place re-walks)
     return bits / 2 + 4 + slots * (kRegionSlack + 8) + spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)));
 }
 inline uint32_t image_segments(const jd_header& h) {
@@ -555,6 +558,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     // re-scanned (k_rescan / k_chain), which costs less than every lane walking 4096 extra bits
     P.piece_overlap = (ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES)) ? kPieceOverlap
                                                                              : std::min(kPieceOverlap, 2 * adaptive);
+    if (ctx->piece_overlap >= 0) P.piece_overlap = uint32_t(ctx->piece_overlap);
     uint64_t sub = 0, entry_cursor = 0;
     P.chain_seg.reserve(seg_cursor + kPieceThreads * P.tablesets.size());
     for (size_t oi = 0; oi < order.size();) {
@@ -564,7 +568,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             d.sub_base = uint32_t(sub);
             d.sub_cap = uint32_t(piece_slots(d.len - d.ecs_off, d.nseg, P.piece_bits));
             d.entry_base = entry_cursor;
-            d.entry_cap = uint32_t(entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits));
+            d.entry_cap = uint32_t(entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces));
             entry_cursor += align_up(size_t(d.entry_cap), 4);
             sub += d.sub_cap;
             for (uint32_t k = 0; k < d.nseg; k++) P.chain_seg.push_back(d.seg_base + k);
@@ -751,6 +755,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.nchain = uint32_t(P.chain_seg.size());
         b.chain_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_chts);
         b.piece_bits = P.piece_bits;
+        b.no_pool = ctx->spare_pieces == 0 ? 1u : 0u;
         b.piece_overlap = P.piece_overlap;
         uint32_t* pc[9];
         for (int q = 0; q < 9; q++) pc[q] = reinterpret_cast<uint32_t*>(base + o_piece[q]);
@@ -979,6 +984,10 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
         const unsigned long long v = std::strtoull(e, nullptr, 0);
         if (v > 0) ctx->max_batch_entries = v;
     }
+    // test knobs: fewer spare regions (re-walks fall back to their own region, no join) and a
+    // shorter warm-up (many speculative starts fail)
+    if (const char* e = std::getenv("JD_SPARE_PIECES")) ctx->spare_pieces = std::strtoll(e, nullptr, 0);
+    if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return JD_ERR_HIP;

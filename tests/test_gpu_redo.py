@@ -1,0 +1,63 @@
+"""Re-walk paths of the fused Huffman pass (GPU), against the oracle.
+
+With a short warm-up (JD_PIECE_OVERLAP_BITS) most speculative piece starts are wrong, so k_redo
+re-walks them and k_chain_fix walks the intervals where a re-walked piece's predecessor was itself
+re-walked.  With JD_SPARE_PIECES=0 no spare region is left: every re-walk writes over its own region
+and cannot join the speculative walk (jd_kernels.hip redo_piece); with the default spare regions it
+joins at a checkpoint and the piece's blocks come from two segments (k_gather).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import jd_synth  # noqa: E402
+import jdamd  # noqa: E402
+import jdoracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+IMAGES = [  # (w, h, subsampling, restart_rows, quality)
+    (1920, 1080, "4:2:0", 0, 90),
+    (1920, 1080, "4:2:0", 1, 75),
+    (1024, 768, "4:4:4", 0, 95),
+    (1280, 720, "4:2:2", 2, 50),
+    (333, 251, "4:2:0", 0, 90),
+]
+
+
+@pytest.fixture(scope="module")
+def batch():
+    datas = [jd_synth.encode(jd_synth.synth_pixels(w, h, 5 + i), q, ss, rr)
+             for i, (w, h, ss, rr, q) in enumerate(IMAGES)]
+    refs = []
+    for d in datas:
+        st, ref = jdoracle.decode(d)
+        assert st == 0
+        refs.append(ref)
+    return datas, refs
+
+
+@pytest.mark.parametrize("spare", ["0", "default"])
+@pytest.mark.parametrize("overlap,path", [("256", "sync"), ("512", "full"), ("64", "auto")])
+def test_rewalks_vs_oracle(monkeypatch, batch, spare, overlap, path):
+    datas, refs = batch
+    monkeypatch.setenv("JD_PIECE_OVERLAP_BITS", overlap)
+    if spare != "default":
+        monkeypatch.setenv("JD_SPARE_PIECES", spare)
+    dec = jdamd.Decoder(0, path=path)
+    try:
+        outs, status = dec.decode_batch(datas)
+        joins = dec.debug_fetch("piece_join") & 0xFFFF
+    finally:
+        dec.close()
+    assert status == [0] * len(datas), status
+    for i, (o, r) in enumerate(zip(outs, refs)):
+        assert o.shape == r.shape and np.array_equal(o, r), f"image {i} differs ({IMAGES[i]})"
+    if spare == "0":  # in place: a re-walk never joins
+        assert not np.any(joins), "a re-walk joined without a spare region"
+    else:  # the short warm-up makes re-walks common: some must have joined
+        assert np.any(joins), "no re-walk joined its speculative walk"
