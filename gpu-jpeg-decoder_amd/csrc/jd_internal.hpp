@@ -111,11 +111,15 @@ struct alignas(16) ImgDesc {
 };
 static_assert(sizeof(ImgDesc) % 16 == 0, "ImgDesc must stay 16-byte aligned");
 
-// Per-block result of the Huffman kernel (sparse coefficient representation):
-//   entry_start = index of the block's first AC entry, relative to its image's ImgDesc::entry_base
-//   cnt_dc      = (number of AC entries << 26) | (DC difference & 0x3FFFFFF): the quantised DC
-//                 difference as a 26-bit two's complement value; k_idct_color predicts the DC
-// AC entry = (int16 value << 16) | zig-zag index (1..63).
+// Per-block result of the Huffman decode (sparse coefficient representation):
+//   entry_start = index of the block's first AC-entry slot (16-bit units), relative to its image's
+//                 ImgDesc::entry_base (32-bit units)
+//   cnt_dc      = slots << kCntShift | escape flag (kCntEsc) | DC difference & kDcMask: the quantised
+//                 DC difference as a 24-bit two's complement value; k_idct_color predicts the DC
+// AC entry slot (16 bits) = value << 6 | zig-zag index (1..63) for |value| <= 511; a larger value
+// (an AC size of 10 or more: rare below quality 95) takes two slots, 0x8000 | zig-zag index, then
+// the value as int16, and sets the block's escape flag.
+constexpr uint32_t kCntShift = 25, kCntEsc = 1u << 24, kDcMask = 0xFFFFFFu;
 struct BlockInfo {
     uint32_t entry_start;
     uint32_t cnt_dc;

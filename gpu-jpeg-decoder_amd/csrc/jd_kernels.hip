@@ -504,10 +504,11 @@ __device__ __forceinline__ int huff_value(uint32_t peek, uint32_t e) {
     return int(mag) - (mag < half ? int(2 * half - 1) : 0);
 }
 
-// BlockInfo.cnt_dc: AC entry count (6 bits) over a 26-bit two's-complement DC (jd_internal.hpp).
-__device__ __forceinline__ uint32_t pack_cnt_dc(uint32_t cnt, int dc) {
-    return (min(cnt, 63u) << 26) | (uint32_t(dc) & 0x3FFFFFFu);
+// BlockInfo.cnt_dc (jd_internal.hpp): AC-entry slot count (7 bits) | escape flag | 24-bit DC difference.
+__device__ __forceinline__ uint32_t pack_cnt_dc(uint32_t cnt, int dc, uint32_t esc) {
+    return (min(cnt, 127u) << kCntShift) | (esc ? kCntEsc : 0u) | (uint32_t(dc) & kDcMask);
 }
+__device__ __forceinline__ int cnt_dc_dc(uint32_t cd) { return int32_t(cd << 8) >> 8; }
 
 struct SegInfo {
     uint64_t blk0;     // first global block of the interval
@@ -629,8 +630,11 @@ constexpr uint32_t kRoundItems = (kWin * 8 + 31) / 2 + 4;
 static_assert(kRegionSlack >= 640 + kRoundItems + 2, "region slack: straddling MCU + one round past the data");
 
 constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte aligned)
+#ifndef JD_EXTRA_LDS
+#define JD_EXTRA_LDS 0  // experiment builds: extra dynamic LDS per piece workgroup (lowers occupancy)
+#endif
 size_t piece_lds_bytes(uint32_t max_slots) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * (row_words(kWin) + kRingWords) * 4;
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * (row_words(kWin) + kRingWords) * 4 + JD_EXTRA_LDS;
 }
 static_assert((kPieceThreads * row_words(kWin) * 4) % 16 == 0, "rings must start 16-byte aligned");
 
@@ -692,9 +696,17 @@ __device__ __forceinline__ uint32_t lut_fast(uint32_t tab, uint32_t peek) {
     return *reinterpret_cast<lds_u32*>(size_t((idx << 2) + tab));
 }
 
-// Block record in a piece's region: AC-entry count (<= 63) << 16 | the 16-bit DC difference (a
-// DC size is <= 15 bits, jd_internal.hpp lut_entry).
-__device__ __forceinline__ uint32_t block_rec(uint32_t cnt, int dc) { return (min(cnt, 63u) << 16) | (uint32_t(dc) & 0xFFFFu); }
+// Block record in a piece's region: escape flag << 23 | AC-entry slot count (<= 126) << 16 | the
+// 16-bit DC difference (a DC size is <= 15 bits, jd_internal.hpp lut_entry).
+__device__ __forceinline__ uint32_t block_rec(uint32_t cnt, int dc, uint32_t esc) {
+    return (esc ? (1u << 23) : 0u) | (min(cnt, 127u) << 16) | (uint32_t(dc) & 0xFFFFu);
+}
+// A 16-bit AC entry: value << 6 | zig-zag index for |value| <= 511; else an escape (0x8000 | zz)
+// followed by the value itself (jd_internal.hpp).
+__device__ __forceinline__ bool entry_big(int v) { return uint32_t(v + 511) > 1022u; }
+__device__ __forceinline__ uint32_t entry16(int v, uint32_t zz, bool big) {
+    return big ? (0x8000u | zz) : ((uint32_t(v) << 6) | zz);
+}
 
 // One piece walk.
 //   kSpec: from `start` (piece_overlap bits before the nominal start, with a guessed state) a
@@ -747,6 +759,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
     uint32_t* const reg = W.reg;
     uint32_t* const rec_top = W.reg + (W.rw - 1u);  // block record k at rec_top[-k]
+    uint16_t* const ring16 = reinterpret_cast<uint16_t*>(ring);
     uint32_t z = 0, b3 = 0, tab = tab_dc0;
     bool warm = KIND == kSpec && W.warm_to != W.start;
     bool active = active_in;
@@ -766,21 +779,22 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         thr = min(min(W.stop_at, end_thr), nxt);
     }
     uint32_t mcus = 0, emcu = kNoError, errs = 0;
-    uint32_t ent = 0, ent_blk = 0, blk = 0;
+    uint32_t ent = 0, ent_blk = 0, blk = 0, esc_blk = 0;
     int dcd = 0;
-    // Stores are deferred and issued every other loop iteration, so that one store instruction
-    // carries many lanes.  An iteration emits at most two entries (a pair entry: two AC symbols),
-    // and a block takes at least two iterations (its DC symbol never pairs), so flushing one quad
-    // and one block record every two iterations keeps at most 7 entries pending: one ring of two
-    // quads and one pending record suffice.  Entries go to the ring at slot ent & 7 (a symbol that
-    // emits nothing writes the next free slot without advancing, so its word is overwritten); a
-    // flush stores the completed quad fq straight from the ring.
+    // AC entries are 16-bit slots (an escaped value takes two).  Stores are deferred and issued
+    // every other loop iteration, so that one store instruction carries many lanes.  An iteration
+    // emits at most four slots (a pair entry: two AC symbols, each possibly escaped), and a block
+    // takes at least two iterations (its DC symbol never pairs), so flushing one quad (8 slots) and
+    // one block record every two iterations keeps at most 15 slots pending: one ring of two quads
+    // and one pending record suffice.  Slots go to the ring at ent & 15 (a symbol that emits nothing
+    // writes the next free slot without advancing, so it is overwritten); a flush stores the
+    // completed quad fq straight from the ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
     uint32_t prec = 0, pblk = 0;
     bool pend_b = false;
 #define JD_FLUSH_Q()                                                                                   \
     do {                                                                                               \
-        if (fq < (ent >> 2)) {                                                                         \
+        if (fq < (ent >> 3)) {                                                                         \
             if (!(JD_ABL & 8) || ent == 0x7FFFFFFFu)                                                   \
                 st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u))); \
             fq++;                                                                                      \
@@ -843,8 +857,13 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             uint32_t L = e & 31u;
             const bool emit = (e & ~zn & kEntEmit) != 0;  // zn < 64 (bit 6 of zn clear)
             dcd = (e & kEntDc) ? val : dcd;
-            ring[ent & 7u] = (uint32_t(val) << 16) | zn;
-            ent += emit ? 1u : 0u;
+            // the escaped value goes to the next slot unconditionally (a free slot, overwritten
+            // by the next entry unless the value needed it)
+            const bool big = entry_big(val);
+            ring16[ent & 15u] = uint16_t(entry16(val, zn, big));
+            ring16[(ent + 1u) & 15u] = uint16_t(val);
+            esc_blk |= (emit && big) ? 1u : 0u;
+            ent += emit ? (big ? 2u : 1u) : 0u;
             const uint32_t L2 = __builtin_amdgcn_ubfe(e, 20u, 4u);
             if (L2 != 0u && zn < 63u) {  // a pair entry, and the first symbol left the block open
                 const uint32_t s2 = e >> 24, sz2 = s2 & 15u;
@@ -852,13 +871,16 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 const uint32_t half = (1u << sz2) >> 1;
                 const int v2 = int(mag) - (mag < half ? int(2 * half - 1) : 0);
                 zn += s2 ? (s2 >> 4) + 1u : 64u;
-                ring[ent & 7u] = (uint32_t(v2) << 16) | zn;
-                ent += (sz2 != 0u && zn < 64u) ? 1u : 0u;
+                const bool emit2 = sz2 != 0u && zn < 64u, big2 = entry_big(v2);
+                ring16[ent & 15u] = uint16_t(entry16(v2, zn, big2));
+                ring16[(ent + 1u) & 15u] = uint16_t(v2);
+                esc_blk |= (emit2 && big2) ? 1u : 0u;
+                ent += emit2 ? (big2 ? 2u : 1u) : 0u;
                 L += L2;
             }
             R.skip(L, row);
             const bool fin = zn >= 63u;
-            prec = fin ? block_rec(ent - ent_blk, dcd) : prec;
+            prec = fin ? block_rec(ent - ent_blk, dcd, esc_blk) : prec;
             pblk = fin ? blk : pblk;
             pend_b = pend_b || fin;
             if ((it & 1u) == 0u) {
@@ -867,6 +889,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             }
             blk += fin ? 1u : 0u;
             ent_blk = fin ? ent : ent_blk;
+            esc_blk = fin ? 0u : esc_blk;
             z = fin ? 0u : zn;
             b3 += fin ? 3u : 0u;
             tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
@@ -916,7 +939,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             emcu = min(emcu, warm ? 0u : mcus);
             active = false;
         }
-        if (active && !warm && ent + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
+        if (active && !warm && (ent + 1u) / 2u + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
             m_end = R.bit();
             emcu = min(emcu, mcus);
             active = false;
@@ -929,13 +952,8 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     }
 #undef JD_FLUSH_Q
 #undef JD_FLUSH_B
-    if (ent & 3u) {  // the last, partial quad (every complete one is stored)
-        const uint32_t r = ent & 3u, qb = ent - r;
-        const uint4 q = *reinterpret_cast<const uint4*>(ring + 4u * ((qb >> 2) & 1u));
-        reg[qb] = q.x;
-        if (r >= 2u) reg[qb + 1u] = q.y;
-        if (r == 3u) reg[qb + 2u] = q.z;
-    }
+    if (ent & 7u)  // the last, partial quad (every complete one is stored; the region has room for all of it)
+        st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)));
     W.m_start = m_start;
     W.m_end = m_end;
     W.mcus = mcus;
@@ -1263,10 +1281,10 @@ __device__ __forceinline__ uint32_t gather_rows(BlockInfo* out, const uint32_t* 
 #pragma unroll
         for (int i = 0; i < kGatherLoads; i++) {
             const uint32_t k = k0 + t + 16u * i;
-            const uint32_t cnt = r[i] >> 16;
+            const uint32_t cnt = (r[i] >> 16) & 127u;
             const uint32_t incl = uint32_t(row_scan_dpp(int(cnt)));
             if (k < n && (!(JD_ABL & 32) || run == 0x7FFFFFFFu))
-                out[k] = BlockInfo{run + incl - cnt, pack_cnt_dc(cnt, int(int16_t(r[i] & 0xFFFFu)))};
+                out[k] = BlockInfo{run + incl - cnt, pack_cnt_dc(cnt, int(int16_t(r[i] & 0xFFFFu)), r[i] >> 23)};
             run += uint32_t(__shfl(int(incl), int(last), 64));
         }
     }
@@ -1294,12 +1312,12 @@ __global__ __launch_bounds__(256) void k_gather(BatchDev b) {
             const uint32_t abase = b.piece_abase[u], amcu = b.piece_amcu[u], join = b.piece_join[u] & 0xFFFFu;
             const uint32_t na = min(take, amcu);
             nA = na * S.bpm;
-            eA = abase;
+            eA = 2u * abase;  // entry indices count 16-bit slots
             topA = abase + P.rw - 1u;
             if (take > na && join) {
                 const CpRec c = b.piece_cp[size_t(u) * kCpRecords + join - 1];
                 nB = (take - na) * S.bpm;
-                eB = P.own + c.ents;
+                eB = 2u * P.own + c.ents;
                 topB = P.own + P.rw - 1u - c.mcus * S.bpm;
             }
         }
@@ -1434,7 +1452,7 @@ __device__ __forceinline__ TileLane tile_lane(const BatchDev& b, const ImgDesc& 
     t.comp = (im.block_pattern >> (2 * bb)) & 3u;
     t.start = t.have && bb == 0 && tile_mcu_starts(G, m);
     t.d = 0;
-    if (t.have) t.d = int32_t(b.blocks[im.block_base + uint64_t(G.g0 + m) * im.bpm + bb].cnt_dc << 6) >> 6;
+    if (t.have) t.d = cnt_dc_dc(b.blocks[im.block_base + uint64_t(G.g0 + m) * im.bpm + bb].cnt_dc);
     return t;
 }
 
@@ -2043,21 +2061,23 @@ __device__ __forceinline__ BlockInfo load_block_info(const BatchDev& b, const Im
     return L.have ? b.blocks[im.block_base + uint64_t(G.g0 + L.m) * TMode<M>::bpm(im) + L.bb] : BlockInfo{0u, 0u};
 }
 
-// The lane's AC entries: [first, first + cnt) of the image's entry array, read as 16-byte quads
-// from the quad holding the first one (lead = its position in that quad).  A block of a corrupt
-// stream may never have been written: never index past the image's entries.
+// The lane's AC entries: 16-bit slots [first, first + cnt) of the image's entry array, read as
+// 16-byte quads (8 slots) from the quad holding the first one (lead = its position in that quad).
+// A block of a corrupt stream may never have been written: never index past the image's entries.
 struct EntryRange {
-    const uint32_t* ep;  // 16-byte aligned
+    const uint16_t* ep;  // 16-byte aligned
     uint32_t lead;
-    int cnt, n4;         // entries, quads (cnt == 0: no quad is touched)
+    int cnt, n4;         // slots, quads (cnt == 0: no quad is touched)
+    bool esc;            // the block has an escaped (wide) value
 };
 __device__ __forceinline__ EntryRange entry_range(const BatchDev& b, const ImgDesc& im, const BlockInfo& bi, bool have) {
     EntryRange r;
-    r.cnt = have ? int(bi.cnt_dc >> 26) : 0;
-    if (uint64_t(bi.entry_start) + uint64_t(r.cnt) > im.entry_cap) r.cnt = 0;
-    r.lead = bi.entry_start & 3u;
-    r.ep = b.entries + im.entry_base + (bi.entry_start - r.lead);
-    r.n4 = r.cnt > 0 ? int(r.lead + uint32_t(r.cnt) + 3u) >> 2 : 0;
+    r.cnt = have ? int(bi.cnt_dc >> kCntShift) : 0;
+    if (uint64_t(bi.entry_start) + uint64_t(r.cnt) > 2ull * im.entry_cap) r.cnt = 0;
+    r.esc = r.cnt > 0 && (bi.cnt_dc & kCntEsc) != 0;
+    r.lead = bi.entry_start & 7u;
+    r.ep = reinterpret_cast<const uint16_t*>(b.entries + im.entry_base) + (bi.entry_start - r.lead);
+    r.n4 = r.cnt > 0 ? int(r.lead + uint32_t(r.cnt) + 7u) >> 3 : 0;
     return r;
 }
 
@@ -2065,34 +2085,47 @@ __device__ __forceinline__ EntryRange entry_range(const BatchDev& b, const ImgDe
 __device__ __forceinline__ void load_entry_quads(const EntryRange& r, uint4 (&E)[kPreQuads]) {
 #pragma unroll
     for (int u = 0; u < kPreQuads; u++)
-        E[u] = (u < r.n4) ? *reinterpret_cast<const uint4*>(r.ep + 4 * u) : make_uint4(0, 0, 0, 0);
+        E[u] = (u < r.n4) ? *reinterpret_cast<const uint4*>(r.ep + 8 * u) : make_uint4(0, 0, 0, 0);
 }
 
-// Entries of quad index qi (its 4 words in w) to the lane's staging row at their zig-zag positions:
+// Slots of quad index qi (its 4 words in v) to the lane's staging row at their zig-zag positions:
 // int16 zz of the row is at byte 2 zz, swizzled (staging_base): row base ^ (2 zz & 0x7E).
+// value = slot >> 6 (arithmetic), zz = slot & 63 (blocks without escaped values).
 __device__ __forceinline__ void scatter_quad(uint8_t* s_bytes, uint32_t base, const uint4& v, int qi,
                                              const EntryRange& r) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int i = 4 * qi + q - int(r.lead);
-        if (i >= 0 && i < r.cnt) *reinterpret_cast<int16_t*>(s_bytes + (base ^ ((w[q] << 1) & 0x7Eu))) = int16_t(w[q] >> 16);
+    for (int q = 0; q < 8; q++) {
+        const int i = 8 * qi + q - int(r.lead);
+        const uint32_t h = (q & 1) ? (w[q >> 1] >> 16) : (w[q >> 1] & 0xFFFFu);
+        if (i >= 0 && i < r.cnt)
+            *reinterpret_cast<int16_t*>(s_bytes + (base ^ ((h << 1) & 0x7Eu))) = int16_t(int(int16_t(uint16_t(h))) >> 6);
     }
 }
 
 // Sparse -> dense for the lane's block: the prefetched quads, then the rest (blocks with more
-// than 4 * kPreQuads - lead entries) four quads in flight at a time.
+// than 8 * kPreQuads - lead slots) four quads in flight at a time.  A block with an escaped value
+// (|value| > 511: rare below quality 95) walks its slots one by one instead.
 __device__ __forceinline__ void scatter_entries(uint32_t* s_buf, uint32_t base, const EntryRange& r,
                                                 const uint4 (&E)[kPreQuads]) {
     uint8_t* row = reinterpret_cast<uint8_t*>(s_buf);
 #if !(JD_ABL & 4)
+    if (__builtin_expect(r.esc, 0)) {
+        for (int i = 0; i < r.cnt; i++) {
+            const uint32_t h = r.ep[r.lead + i];
+            int v = int(int16_t(uint16_t(h))) >> 6;
+            if ((h & 0xFFC0u) == 0x8000u && i + 1 < r.cnt) v = int(int16_t(r.ep[r.lead + ++i]));
+            *reinterpret_cast<int16_t*>(row + (base ^ ((h << 1) & 0x7Eu))) = int16_t(v);
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < kPreQuads; u++) scatter_quad(row, base, E[u], u, r);
     for (int c = kPreQuads; c < r.n4; c += 4) {
         uint4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; u++)
-            v[u] = (c + u < r.n4) ? *reinterpret_cast<const uint4*>(r.ep + 4 * (c + u)) : make_uint4(0, 0, 0, 0);
+            v[u] = (c + u < r.n4) ? *reinterpret_cast<const uint4*>(r.ep + 8 * (c + u)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int u = 0; u < 4; u++) scatter_quad(row, base, v[u], c + u, r);
     }
@@ -2104,7 +2137,7 @@ __device__ __forceinline__ void scatter_entries(uint32_t* s_buf, uint32_t base, 
 // predictor.  Exact int, as the reference's int predictor: the int16 staging is bypassed.
 __device__ __forceinline__ int tile_dc_predict(const TileGeo& G, const TileLaneGeo& L, const BlockInfo& bi,
                                                const DcPred& cin, uint32_t lane) {
-    const int d = L.have ? int32_t(bi.cnt_dc << 6) >> 6 : 0;
+    const int d = L.have ? cnt_dc_dc(bi.cnt_dc) : 0;
     const bool start = L.have && L.bb == 0 && tile_mcu_starts(G, L.m);
     const uint64_t smask = __ballot(start);
     const uint32_t comp = L.comp;

@@ -874,7 +874,7 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
 
         // algorithmic bytes per kernel
         jd_stats& S = ctx->stats;
-        const double entries = double(ctr[0]);
+        const double entries = double(ctr[0]);  // 16-bit AC-entry slots
         const double blocks = pd.blocks, ecs = pd.ecs, nsubd = pd.nsub, nsegd = pd.nseg;
         const bool fancy = pd.fancy;
         const double overlap_factor = (pd.piece_bits + pd.piece_overlap) / pd.piece_bits;
@@ -883,13 +883,13 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
             pd.chunks * 12 + nsegd * 8,                        // k_index: per-chunk counters, boundaries
             2 * ecs,                                           // k_compact: read + write the ECS
             nsubd * 4 + nsegd * 16,                            // k_subplan: piece map
-            ecs * std::min(overlap_factor, 2.0) + blocks * 4 + entries * 4 + nsubd * 32,  // k_piece: bits incl.
+            ecs * std::min(overlap_factor, 2.0) + blocks * 4 + entries * 2 + nsubd * 32,  // k_piece: bits incl.
                                                                // warm-up in, records + AC entries + counts out
             nsubd * 8,                                         // k_redo: start/end check per piece
             nsubd * 20,                                        // k_chain: counts in, first MCU / count out
             blocks * 12 + nsubd * 24,                          // k_gather: records in, BlockInfo out
             blocks * 8 + pd.tiles * 48,                        // k_dc_pred: BlockInfo read, tile sums, scan
-            blocks * 8 + entries * 4 + (fancy ? blocks * 128 : pd.pixels * 3),  // k_idct_color: coefficients
+            blocks * 8 + entries * 2 + (fancy ? blocks * 128 : pd.pixels * 3),  // k_idct_color: coefficients
                                                                                  // in, RGB (fancy: planes) out
             fancy ? blocks * 128 + pd.pixels * 3 : 0.0};       // k_colour_fancy: planes in, RGB out
         for (int k = 0; k < JD_NUM_KERNELS; k++) {

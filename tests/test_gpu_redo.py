@@ -26,6 +26,7 @@ IMAGES = [  # (w, h, subsampling, restart_rows, quality)
     (1024, 768, "4:4:4", 0, 95),
     (1280, 720, "4:2:2", 2, 50),
     (333, 251, "4:2:0", 0, 90),
+    (640, 480, "4:4:4", 0, 100),  # quality 100: AC values beyond +-511 take escaped 16-bit entry slots
 ]
 
 
@@ -51,7 +52,8 @@ def test_rewalks_vs_oracle(monkeypatch, batch, spare, overlap, path):
     dec = jdamd.Decoder(0, path=path)
     try:
         outs, status = dec.decode_batch(datas)
-        joins = dec.debug_fetch("piece_join") & 0xFFFF
+        valid = dec.debug_fetch("sub_seg") != 0xFFFFFFFF  # padding slots hold stale scratch
+        joins = (dec.debug_fetch("piece_join") & 0xFFFF)[valid]
     finally:
         dec.close()
     assert status == [0] * len(datas), status
@@ -61,3 +63,23 @@ def test_rewalks_vs_oracle(monkeypatch, batch, spare, overlap, path):
         assert not np.any(joins), "a re-walk joined without a spare region"
     else:  # the short warm-up makes re-walks common: some must have joined
         assert np.any(joins), "no re-walk joined its speculative walk"
+
+
+def test_escaped_entries_vs_oracle():
+    """Quality 100 on noisy pixels: many AC values need the two-slot escape (jd_internal.hpp)."""
+    rng = np.random.default_rng(3)
+    px = rng.integers(0, 256, (256, 384, 3), dtype=np.uint8)
+    yy, xx = np.mgrid[0:256, 0:384]
+    px[:128] = np.where(((xx + yy) & 1)[:128, :, None] == 1, 255, 0).astype(np.uint8)  # high AC values
+    px[128:, :192] = np.where(((xx // 2) & 1)[128:, :192, None] == 1, 255, 0).astype(np.uint8)
+    data = jd_synth.encode(px, 100, "4:4:4")
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    dec = jdamd.Decoder(0)
+    try:
+        out = dec.decode(data)
+        esc = (dec.debug_fetch("blocks")[:, 1] >> 24) & 1
+    finally:
+        dec.close()
+    assert np.any(esc), "no block used an escaped entry"
+    assert np.array_equal(out, ref)

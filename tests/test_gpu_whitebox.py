@@ -158,13 +158,21 @@ def test_block_coefficients(sync_decoder, name):
     coef[:, 0] = dc_differences(data, coef[:, 0].astype(np.int64))
     nb = coef.shape[0]
     bad = []
+    slots = entries.view(np.uint16)  # 16-bit AC-entry slots (jd_internal.hpp BlockInfo)
     for i in range(nb):
         start, cd = int(blocks[i, 0]), int(blocks[i, 1])
-        cnt, dc = cd >> 26, ((cd & 0x3FFFFFF) ^ 0x2000000) - 0x2000000  # 6-bit count, 26-bit DC
+        cnt, dc = cd >> 25, ((cd & 0xFFFFFF) ^ 0x800000) - 0x800000  # 7-bit slot count, 24-bit DC
         got = np.zeros(64, np.int32)
         got[0] = dc
-        for e in entries[start:start + cnt]:
-            got[int(e) & 63] = _s16((int(e) >> 16) & 0xFFFF)
+        k = start
+        while k < start + cnt:
+            h = int(slots[k])
+            v = _s16(h) >> 6
+            if (h & 0xFFC0) == 0x8000:  # escape: the value in the next slot
+                k += 1
+                v = _s16(int(slots[k]))
+            got[h & 63] = v
+            k += 1
         if not np.array_equal(got, coef[i]):
             bad.append(i)
     assert not bad, f"{len(bad)} of {nb} blocks differ, first {bad[:10]}"
