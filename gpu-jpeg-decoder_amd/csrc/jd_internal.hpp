@@ -23,8 +23,7 @@ constexpr int kLutSize = 1 << kLutBits;
 #define JD_HD
 #endif
 
-// Device Huffman table (built on the host from a DHT table, uploaded once, cached by content).
-//   fast[i]: entry for the symbol whose code starts the next kLutBits stream bits (= i):
+// Symbol entry of the rare path (32 bits; jd_kernels.hip huff_slow / the piece walks' rare branch):
 //     bits 0..4   L    bits the symbol consumes, code + magnitude (0: code longer than kLutBits)
 //     bit  6      emit AC coefficient stored (size != 0)
 //     bits 8..14  adv  advance of the coefficient index z (the last position decoded, DC = 0):
@@ -34,24 +33,7 @@ constexpr int kLutSize = 1 << kLutBits;
 //     bit  15     dc   DC symbol
 //     bits 16..19 sz   magnitude bits (DC: symbol, AC: symbol & 15; a DC size above 15 is corrupt)
 //     bit  7      bad  corrupt code (slow path only)
-//   AC tables also describe the FOLLOWING symbol when the first is not EOB and both fit in the
-//   kLutBits:
-//     bits 20..23 L2   bits of the second symbol (0: no pair)
-//     bits 24..31 sym2 its run/size byte
-//   The coefficient is always EXTEND(the last sz of the L bits), so a decode step is one lookup
-//   plus bit-field extracts.  Codes longer than kLutBits take the canonical slow path:
-//   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not
-//                < lim[l-1]) — the canonical DECODE procedure of JPEG Annex F.2.2.3
-//   lim[19]    : 1 for a DC table
-//   base[l]    : valptr[l] - mincode[l]; vals[] the symbols in code order
-struct alignas(16) HuffLut {
-    uint32_t fast[kLutSize];
-    uint32_t lim[20];
-    int32_t base[20];
-    uint8_t vals[256];
-};
-static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
-constexpr int kLutWords = int(sizeof(HuffLut) / 4);
+//   The coefficient is EXTEND(the last sz of the L bits).
 constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 7;
 
 // Entry of a code of length l for symbol sym; 0 when it cannot be represented (l + sz > 31 or a
@@ -63,6 +45,42 @@ JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
     const uint32_t adv = sym == 0u ? 64u : (sym >> 4) + 1u;
     return (l + sz) | (sz ? kEntEmit : 0u) | (adv << 8) | (sz << 16);
 }
+
+// Device Huffman table (built on the host from a DHT table, uploaded once, cached by content).
+// fast[i] is the 64-bit entry {lo, hi} for the next kLutBits stream bits = i, laid out so that the
+// piece walks use its fields as instruction operands (v_bfe_i32 takes its offset from lo[4:0] and
+// its width from hi[4:0]):
+//   lo  bits 0..4   o1   32 - L1: offset in the 32-bit peek of the first symbol's magnitude
+//       bits 5..9   L1   bits of the first symbol, code + magnitude (<= 31)
+//       bit  10     DC   DC symbol
+//       bit  11     E1   the first symbol stores a coefficient (AC, size != 0)
+//       bit  12     P    a second AC symbol follows within the index (pair)
+//       bit  13     E2   the second symbol stores a coefficient
+//       bit  15     R    rare: hi holds the 32-bit entry above (0: a code longer than kLutBits);
+//                        codes longer than kLutBits, AC magnitudes of 10 bits or more (they need an
+//                        escaped slot), DC sizes above 11
+//       bits 16..31 M1   int16: the coefficient is s - (M1 ^ (s >> 31)) for s = the magnitude bits
+//                        sign-extended (v_bfe_i32 of width w1): M1 = 2^sz - 1 when the magnitude
+//                        reaches beyond the index, else w1 = 0 and M1 = -value
+//   hi  bits 0..4   w1   magnitude bits still to extract (0 when the index resolves the value)
+//       bits 5..11  adv1 advance of z by the first symbol (DC 0, AC run + 1, ZRL 16, EOB 64)
+//       bits 12..18 adv2 the same for the second symbol
+//       bits 19..22 L2   bits of the second symbol (code + magnitude, within the index)
+//       bits 23..31 v2   int9: its value (|v2| <= 255: its magnitude has at most 8 bits)
+//   Codes longer than kLutBits take the canonical slow path:
+//   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not
+//                < lim[l-1]) — the canonical DECODE procedure of JPEG Annex F.2.2.3
+//   lim[19]    : 1 for a DC table
+//   base[l]    : valptr[l] - mincode[l]; vals[] the symbols in code order
+struct alignas(16) HuffLut {
+    uint32_t fast[2 * kLutSize];  // {lo, hi} pairs
+    uint32_t lim[20];
+    int32_t base[20];
+    uint8_t vals[256];
+};
+static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
+constexpr int kLutWords = int(sizeof(HuffLut) / 4);
+constexpr uint32_t kLoDc = 1u << 10, kLoE1 = 1u << 11, kLoPair = 1u << 12, kLoE2 = 1u << 13, kLoRare = 1u << 15;
 
 // Maximum Huffman tables a table set (one workgroup of the Huffman kernel) stages into LDS.
 constexpr int kSlotsPerSet = 6;
@@ -153,9 +171,11 @@ constexpr uint32_t kPieceOverlap = JD_PIECE_OVERLAP;
 constexpr uint32_t kMinPieceBits = 512;      // adaptive floor (small batches)
 constexpr uint64_t kPieceTarget = 65536;    // pieces wanted per batch before shrinking stops
 #ifndef JD_PIECE_THREADS
-#define JD_PIECE_THREADS 256
+#define JD_PIECE_THREADS 512
 #endif
-constexpr int kPieceThreads = JD_PIECE_THREADS;  // one workgroup shares one copy of its table set in LDS
+// One workgroup shares one copy of its table set in LDS (four 8.4 KB tables for 4:2:0 + 76 B per
+// lane: two 512-lane workgroups per CU, 16 waves).
+constexpr int kPieceThreads = JD_PIECE_THREADS;
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;

@@ -617,8 +617,15 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
 #define JD_WIN_PIECE 32
 #endif
 constexpr int kWin = JD_WIN_PIECE;
-constexpr int win_loads(int win) { return win / 16 + 1; }        // 16-byte loads per window (advance + overlap)
-constexpr int row_words(int win) { return 1 + 4 * win_loads(win); }  // odd pitch (last word unused)
+// Bytes of the next window a row also holds: a round decodes the symbols whose refill word index
+// is <= kWin / 4, and the last of them reads word kWin / 4 + 1, so 8 bytes suffice.
+#ifndef JD_ROW_OVERLAP
+#define JD_ROW_OVERLAP 8
+#endif
+constexpr int kRowOverlap = JD_ROW_OVERLAP;
+static_assert(kRowOverlap == 8 || kRowOverlap == 16, "row overlap: one 8- or 16-byte load");
+constexpr int win_loads(int win) { return win / 16 + 1; }  // loads per window: win / 16 of 16 bytes + the overlap
+constexpr int row_words(int win) { return 1 + (win + kRowOverlap) / 4; }  // odd pitch (last word unused)
 static_assert(row_words(kWin) % 2 == 1, "row pitch must be odd");
 #ifndef JD_ABL  // experiment builds: 1 skip colour, 2 skip IDCT math, 4 skip the entry scatter, 8 / 16 skip the
                 // piece walk's entry / block-record stores
@@ -673,12 +680,23 @@ struct BitRow {
     }
 };
 
-#define JD_ROW_FILL(row, v, q)                        \
-    do {                                              \
-        (row)[4 * (q) + 0] = __builtin_bswap32(v.x);  \
-        (row)[4 * (q) + 1] = __builtin_bswap32(v.y);  \
-        (row)[4 * (q) + 2] = __builtin_bswap32(v.z);  \
-        (row)[4 * (q) + 3] = __builtin_bswap32(v.w);  \
+// Load q of a window at a (the last one is the overlap: 8 or 16 bytes), and its row words.
+__device__ __forceinline__ u32x4 win_load(uintptr_t a, int q, uintptr_t last) {
+    if (q == win_loads(kWin) - 1 && kRowOverlap == 8) {
+        const uintptr_t c = a + 16 * q;
+        const u32x2 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x2*>(c < last ? c : last);
+        return u32x4{v.x, v.y, 0u, 0u};
+    }
+    return load16(a + 16 * q, last);
+}
+#define JD_ROW_FILL(row, v, q)                                              \
+    do {                                                                    \
+        (row)[4 * (q) + 0] = __builtin_bswap32(v.x);                        \
+        (row)[4 * (q) + 1] = __builtin_bswap32(v.y);                        \
+        if ((q) < win_loads(kWin) - 1 || kRowOverlap == 16) {               \
+            (row)[4 * (q) + 2] = __builtin_bswap32(v.z);                    \
+            (row)[4 * (q) + 3] = __builtin_bswap32(v.w);                    \
+        }                                                                   \
     } while (0)
 
 // Decoder state per symbol: z = coefficient index of the last symbol (DC: 0), b3 = 3 x block
@@ -690,10 +708,11 @@ constexpr uint32_t kLutBytes = sizeof(HuffLut);
 typedef const __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return uint32_t(size_t((lds_u32*)p)); }
 __device__ __forceinline__ const uint32_t* lut_at(uint32_t tab) { return (const uint32_t*)(lds_u32*)size_t(tab); }
-__device__ __forceinline__ uint32_t lut_fast(uint32_t tab, uint32_t peek) {
+typedef const __attribute__((address_space(3))) u32x2 lds_u64;
+__device__ __forceinline__ u32x2 lut_fast(uint32_t tab, uint32_t peek) {
     uint32_t idx = peek >> (32 - kLutBits);
     asm("" : "+v"(idx));
-    return *reinterpret_cast<lds_u32*>(size_t((idx << 2) + tab));
+    return *reinterpret_cast<lds_u64*>(size_t((idx << 3) + tab));
 }
 
 // Block record in a piece's region: escape flag << 23 | AC-entry slot count (<= 126) << 16 | the
@@ -748,7 +767,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     uintptr_t wa = a_start & ~uintptr_t(15);
 #pragma unroll
     for (int q = 0; q < win_loads(kWin); q++) {
-        const u32x4 v = load16(wa + 16 * q, S.last);
+        const u32x4 v = win_load(wa, q, S.last);
         JD_ROW_FILL(row, v, q);
     }
     BitRow R;
@@ -783,10 +802,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     int dcd = 0;
     // AC entries are 16-bit slots (an escaped value takes two).  Stores are deferred and issued
     // every other loop iteration, so that one store instruction carries many lanes.  An iteration
-    // emits at most four slots (a pair entry: two AC symbols, each possibly escaped), and a block
-    // takes at least two iterations (its DC symbol never pairs), so flushing one quad (8 slots) and
-    // one block record every two iterations keeps at most 15 slots pending: one ring of two quads
-    // and one pending record suffice.  Slots go to the ring at ent & 15 (a symbol that emits nothing
+    // emits at most two slots (a pair of AC symbols, or one escaped value: pairs never escape), and
+    // a block takes at least two iterations (its DC symbol never pairs), so flushing one quad (8
+    // slots) and one block record every two iterations keeps fewer than 16 slots pending: one ring
+    // of two quads and one pending record suffice.  Slots go to the ring at ent & 15 (a symbol that emits nothing
     // writes the next free slot without advancing, so it is overwritten); a flush stores the
     // completed quad fq straight from the ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
@@ -809,21 +828,26 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         const uintptr_t na = wa + kWin;
         u32x4 nx[win_loads(kWin)];
 #pragma unroll
-        for (int q = 0; q < win_loads(kWin); q++) nx[q] = load16(na + 16 * q, S.last);
+        for (int q = 0; q < win_loads(kWin); q++) nx[q] = win_load(na, q, S.last);
         if (KIND == kSpec && __any(active && warm)) {  // wave-uniform
             // warm-up: follow the symbols only (the write walk's table format: pair fields carry
             // the second symbol's bits and run/size byte)
             while (active && warm && R.rp <= kWin / 4) {
                 const uint32_t peek = R.peek();
-                uint32_t e = lut_fast(tab, peek);
-                if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
-                uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
-                uint32_t L = e & 31u;
-                const uint32_t L2 = __builtin_amdgcn_ubfe(e, 20u, 4u);
-                if (L2 != 0u && zn < 63u) {
-                    const uint32_t s2 = e >> 24;
-                    zn += s2 ? (s2 >> 4) + 1u : 64u;
-                    L += L2;
+                const u32x2 E = lut_fast(tab, peek);
+                uint32_t zn, L;
+                if (E.x & kLoRare) {
+                    uint32_t e = E.y;
+                    if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
+                    zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+                    L = e & 31u;
+                } else {
+                    zn = z + __builtin_amdgcn_ubfe(E.y, 5u, 7u);
+                    L = __builtin_amdgcn_ubfe(E.x, 5u, 5u);
+                    if ((E.x & kLoPair) && zn < 63u) {
+                        zn += __builtin_amdgcn_ubfe(E.y, 12u, 7u);
+                        L += __builtin_amdgcn_ubfe(E.y, 19u, 4u);
+                    }
                 }
                 R.skip(L, row);
                 const bool fin = zn >= 63u;
@@ -848,35 +872,42 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         while (active && !warm && R.rp <= kWin / 4) {
             it++;
             const uint32_t peek = R.peek();
-            uint32_t e = lut_fast(tab, peek);
-            if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);  // 0.3 % of symbols
-            errs |= e;
-            const int val = huff_value(peek, e);
-            // EOB / ZRL / run-size (parser.cpp:114-134)
-            uint32_t zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
-            uint32_t L = e & 31u;
-            const bool emit = (e & ~zn & kEntEmit) != 0;  // zn < 64 (bit 6 of zn clear)
-            dcd = (e & kEntDc) ? val : dcd;
-            // the escaped value goes to the next slot unconditionally (a free slot, overwritten
-            // by the next entry unless the value needed it)
-            const bool big = entry_big(val);
-            ring16[ent & 15u] = uint16_t(entry16(val, zn, big));
-            ring16[(ent + 1u) & 15u] = uint16_t(val);
-            esc_blk |= (emit && big) ? 1u : 0u;
-            ent += emit ? (big ? 2u : 1u) : 0u;
-            const uint32_t L2 = __builtin_amdgcn_ubfe(e, 20u, 4u);
-            if (L2 != 0u && zn < 63u) {  // a pair entry, and the first symbol left the block open
-                const uint32_t s2 = e >> 24, sz2 = s2 & 15u;
-                const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - (L + L2), sz2);
-                const uint32_t half = (1u << sz2) >> 1;
-                const int v2 = int(mag) - (mag < half ? int(2 * half - 1) : 0);
-                zn += s2 ? (s2 >> 4) + 1u : 64u;
-                const bool emit2 = sz2 != 0u && zn < 64u, big2 = entry_big(v2);
-                ring16[ent & 15u] = uint16_t(entry16(v2, zn, big2));
-                ring16[(ent + 1u) & 15u] = uint16_t(v2);
-                esc_blk |= (emit2 && big2) ? 1u : 0u;
-                ent += emit2 ? (big2 ? 2u : 1u) : 0u;
-                L += L2;
+            const u32x2 E = lut_fast(tab, peek);
+            uint32_t zn, L;
+            if (E.x & kLoRare) {  // codes longer than the index, escaped magnitudes, corrupt codes
+                uint32_t e = E.y;
+                if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
+                errs |= e;
+                const int val = huff_value(peek, e);
+                // EOB / ZRL / run-size (parser.cpp:114-134)
+                zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+                L = e & 31u;
+                const bool emit = (e & ~zn & kEntEmit) != 0;  // zn < 64 (bit 6 of zn clear)
+                dcd = (e & kEntDc) ? val : dcd;
+                // the escaped value goes to the next slot unconditionally (a free slot, overwritten
+                // by the next entry unless the value needed it)
+                const bool big = entry_big(val);
+                ring16[ent & 15u] = uint16_t(entry16(val, zn, big));
+                ring16[(ent + 1u) & 15u] = uint16_t(val);
+                esc_blk |= (emit && big) ? 1u : 0u;
+                ent += emit ? (big ? 2u : 1u) : 0u;
+            } else {
+                // EXTEND with the table's constants: v = s - (M1 ^ (s >> 31)) for the magnitude bits
+                // s sign-extended (none left to extract when the index resolves the value: v = -M1)
+                const int s1 = __builtin_amdgcn_sbfe(int(peek), E.x, E.y);
+                const int v1 = s1 - ((int(E.x) >> 16) ^ (s1 >> 31));
+                zn = z + __builtin_amdgcn_ubfe(E.y, 5u, 7u);
+                L = __builtin_amdgcn_ubfe(E.x, 5u, 5u);
+                // a slot is written for every symbol; only a stored coefficient advances ent
+                ring16[ent & 15u] = uint16_t((uint32_t(v1) << 6) | zn);
+                ent += ((E.x & kLoE1) && zn < 64u) ? 1u : 0u;
+                dcd = (E.x & kLoDc) ? v1 : dcd;
+                if ((E.x & kLoPair) && zn < 63u) {  // a pair, and the first symbol left the block open
+                    zn += __builtin_amdgcn_ubfe(E.y, 12u, 7u);
+                    L += __builtin_amdgcn_ubfe(E.y, 19u, 4u);
+                    ring16[ent & 15u] = uint16_t((uint32_t(int(E.y) >> 23) << 6) | zn);
+                    ent += ((E.x & kLoE2) && zn < 64u) ? 1u : 0u;
+                }
             }
             R.skip(L, row);
             const bool fin = zn >= 63u;
@@ -2604,9 +2635,26 @@ __global__ void k_test_color(const int32_t* ycc, uint8_t* rgb, int n) {
 // ------------------------------------------------------------------------------------------
 size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots); }
 
+// Dynamic LDS above 64 KiB (large piece workgroups) has to be allowed per kernel once.
+static hipError_t allow_lds(size_t lds) {
+    static size_t allowed = 65536;
+    if (lds <= allowed) return hipSuccess;
+    for (const void* f : {reinterpret_cast<const void*>(&k_piece), reinterpret_cast<const void*>(&k_redo),
+                          reinterpret_cast<const void*>(&k_chain_fix)}) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+    }
+    allowed = lds;
+    return hipSuccess;
+}
+
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     if (!b.nimg) return hipSuccess;
     const size_t lds = piece_lds_bytes(b.max_slots);
+    if (k == 4 || k == 5 || k == 6) {
+        const hipError_t e = allow_lds(lds);
+        if (e != hipSuccess) return e;
+    }
     switch (k) {
         case 0:
             if (b.max_chunks) hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);

@@ -174,26 +174,56 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
     lut->lim[17] = 0xFFFFFFFFu;  // sentinel: unmatched 16-bit prefix -> corrupt
     lut->lim[19] = is_dc ? 1u : 0u;
     for (int i = 0; i < h.nvals; i++) lut->vals[i] = h.vals[i];
+    // code length and symbol of every index whose top bits are a code of <= kLutBits bits
+    uint8_t len_of[kLutSize] = {}, sym_of[kLutSize] = {};
     for (int i = 0; i < k; i++) {
         const int l = lens[i];
         if (l > kLutBits) continue;
-        const uint32_t e = lut_entry(uint32_t(l), h.vals[i], is_dc);  // 0: decoded (and rejected) by the slow path
         const int shift = kLutBits - l;
         const int first = codes[i] << shift, last = ((codes[i] + 1) << shift) - 1;
-        for (int idx = first; idx <= last; idx++) lut->fast[idx] = e;
-    }
-    if (!is_dc) {  // pair entries: the second symbol decoded from the bits left after the first
-        uint32_t one[kLutSize];
-        memcpy(one, lut->fast, sizeof(one));
-        for (uint32_t idx = 0; idx < kLutSize; idx++) {
-            const uint32_t e1 = one[idx], L1 = e1 & 31u;
-            if (e1 == 0 || ((e1 >> 8) & 127u) == 64u || L1 >= uint32_t(kLutBits)) continue;
-            const uint32_t e2 = one[(idx << L1) & (kLutSize - 1)], L2 = e2 & 31u;
-            if (e2 == 0 || L2 > uint32_t(kLutBits) - L1) continue;  // needs bits beyond the index
-            const uint32_t adv = (e2 >> 8) & 127u, sz2 = (e2 >> 16) & 15u;
-            const uint32_t sym2 = adv == 64u ? 0u : ((adv - 1u) << 4) | sz2;  // the run/size byte again
-            lut->fast[idx] = e1 | (L2 << 20) | (sym2 << 24);
+        for (int idx = first; idx <= last; idx++) {
+            len_of[idx] = uint8_t(l);
+            sym_of[idx] = h.vals[i];
         }
+    }
+    // EXTEND (utils/stream.cpp:44-52) of the sz bits of idx that follow its first `at` bits
+    auto value_at = [](uint32_t idx, uint32_t at, uint32_t sz) {
+        const uint32_t mag = (idx >> (uint32_t(kLutBits) - at - sz)) & ((1u << sz) - 1u);
+        return sz == 0 ? 0 : (mag >> (sz - 1)) ? int(mag) : int(mag) - int((1u << sz) - 1u);
+    };
+    for (uint32_t idx = 0; idx < uint32_t(kLutSize); idx++) {
+        uint32_t& lo = lut->fast[2 * idx];
+        uint32_t& hi = lut->fast[2 * idx + 1];
+        const uint32_t l1 = len_of[idx], sym1 = sym_of[idx];
+        const uint32_t e1 = l1 ? lut_entry(l1, sym1, is_dc) : 0u;  // 0: longer code (or unrepresentable)
+        const uint32_t sz1 = is_dc ? sym1 : (sym1 & 15u);
+        if (e1 == 0 || (is_dc ? sz1 > 11u : sz1 >= 10u)) {  // rare: the walks' generic branch
+            lo = kLoRare;
+            hi = e1;
+            continue;
+        }
+        const uint32_t L1 = l1 + sz1, adv1 = (e1 >> 8) & 127u;
+        uint32_t w1 = 0;
+        int32_t m1;
+        if (L1 <= uint32_t(kLutBits)) {
+            m1 = -value_at(idx, l1, sz1);
+        } else {
+            w1 = sz1;
+            m1 = int32_t((1u << sz1) - 1u);
+        }
+        lo = ((32u - L1) & 31u) | (L1 << 5) | (is_dc ? kLoDc : 0u) | ((!is_dc && sz1) ? kLoE1 : 0u) |
+             (uint32_t(m1) << 16);
+        hi = w1 | (adv1 << 5);
+        // pair: the following AC symbol, when the first is not EOB and both lie within the index
+        if (is_dc || adv1 == 64u || L1 >= uint32_t(kLutBits)) continue;
+        const uint32_t idx2 = (idx << L1) & (kLutSize - 1), l2 = len_of[idx2], sym2 = sym_of[idx2];
+        if (l2 == 0) continue;
+        const uint32_t sz2 = sym2 & 15u, L2 = l2 + sz2;
+        if (L2 > uint32_t(kLutBits) - L1) continue;  // needs bits beyond the index
+        const uint32_t adv2 = sym2 == 0u ? 64u : (sym2 >> 4) + 1u;
+        const int v2 = value_at(idx, L1 + l2, sz2);
+        lo |= kLoPair | (sz2 ? kLoE2 : 0u);
+        hi |= (adv2 << 12) | (L2 << 19) | ((uint32_t(v2) & 511u) << 23);
     }
     return true;
 }
