@@ -44,7 +44,10 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SIMDS = 1024               # 256 CUs x 4 SIMD-32
-VALU_CYCLES_PER_INST = 2   # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+# SQ_ACTIVE_INST_VALU counts quad-cycles (MI355X_MICROARCH.md); on gfx950 most 32-bit integer VALU
+# instructions (shifts, bfe, mad24, cndmask, perm, packed 16-bit, med3) issue at one wave64 per 4
+# cycles, v_add/v_and/v_add_f32 at ~2 (tools/micro/valurate.hip)
+VALU_CYCLES_PER_QUAD = 4
 BOX_CPU_SHARE = 16         # CPUs a one-GPU share of the box gets (task environment)
 
 
@@ -226,8 +229,29 @@ def valu_issue(config: str, kernel: str, avg_ms: float):
     if not k or avg_ms <= 0:
         return None
     clk = k.get("clock_ghz") or 2.4
-    frac = k["valu_insts"] * VALU_CYCLES_PER_INST / (SIMDS * clk * 1e9 * avg_ms * 1e-3)
-    return {"valu_insts_per_launch": k["valu_insts"], "clock_ghz": clk, "issue_frac": frac, "source": src}
+    busy = k.get("counters", {}).get("SQ_ACTIVE_INST_VALU") or k["valu_insts"]
+    frac = busy * VALU_CYCLES_PER_QUAD / (SIMDS * clk * 1e9 * avg_ms * 1e-3)
+    return {"valu_insts_per_launch": k["valu_insts"], "clock_ghz": clk, "busy_frac": frac,
+            "note": "VALU-busy SIMD cycles (SQ_ACTIVE_INST_VALU quad-cycles x 4) over the launch's SIMD cycles",
+            "source": src}
+
+
+def kernel_rooflines(kern: dict, config: str) -> dict:
+    """Per kernel slot: average launch time, algorithmic GB/s and its fraction of the 8 TB/s HBM
+    peak, HBM traffic per launch (committed PMC profile) and the VALU-busy fraction (committed SQ
+    profile).  The two big kernels are VALU-bound, so the last figure is the roof that applies."""
+    out = {}
+    for k, v in kern.items():
+        if not v["launches"] or v["total_ms"] <= 0:
+            continue
+        ms = v["total_ms"] / v["launches"]
+        gbs = v["bytes"] / v["launches"] / (ms * 1e-3) / 1e9
+        names = {"k_dc_pred": "k_dc_sum"}.get(k, k)
+        tr = measured_traffic(config, names)
+        vb = valu_issue(config, names, ms)
+        out[k] = {"avg_ms": round(ms, 4), "GB_s": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4),
+                  "traffic_bytes": tr[0] if tr else None, "valu_busy": round(vb["busy_frac"], 3) if vb else None}
+    return out
 
 
 def copy_peak_gbs(dev, gib: float = 4.0, reps: int = 5):
@@ -547,6 +571,7 @@ def main():
                          "valu": valu_issue(args.config, dom, avg_ms),
                          "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes,
                          "timing": f"hipEvents on the decode stream, {max(1, args.kernel_steps)} serialized batches"},
+            "kernel_rooflines": kernel_rooflines(kern, args.config),
             "kernels_ms_per_step": {k: v["total_ms"] / max(1, v["launches"]) for k, v in kern.items()},
             "kernels_ms_per_step_overlapped": {k: v["total_ms"] / max(1, v["launches"])
                                                for k, v in st_overlap["kernels"].items()},

@@ -109,7 +109,8 @@ struct alignas(16) ImgDesc {
     uint64_t block_base;              // first global block index
     uint32_t tableset;
     uint32_t chunk_base, nchunks;     // 16 KiB scan chunks of this image's ECS
-    uint32_t sub_base, sub_cap;       // this image's range in the subsequence list (upper bound)
+    uint32_t sub_base, sub_cap;       // this image's share of its table set's piece-slot range (upper
+                                      // bound of its pieces; k_subplan allocates them densely)
     uint32_t tile_mcus;               // MCU columns per IDCT/colour tile
     uint32_t tile_mrows;              // MCU rows per tile: always 1 (a tile is a run of MCUs of one
                                       // MCU row, tile_mcus * bpm <= 64; the DC prediction relies on it)
@@ -248,8 +249,12 @@ struct BatchDev {
     uint32_t* sub_seg;            // segment of each piece slot (kInvalidImage = unused)
     uint32_t nsub;                // multiple of kPieceThreads
     const uint32_t* wg_tableset;  // table set of each k_piece workgroup
+    uint32_t* ts_cursor;          // next free piece slot of each table set's range: k_subplan packs the
+                                  // pieces of the batch's images densely from its start (whole waves
+                                  // of the range's tail stay unused and exit at once)
     uint32_t max_slots;           // LUT slots staged per workgroup
     uint32_t piece_bits, piece_overlap;
+    uint32_t piece_plan;          // k_pieceplan: resident piece lanes (0: use piece_bits as is)
     uint32_t* seg_ent;            // k_subplan: first region word of each segment's pieces (image-relative)
     uint32_t* img_pool;           // k_subplan: next free region word of each image (re-walk regions)
     uint32_t no_pool;             // 1: re-walks always write over their own region (tests, JD_SPARE_PIECES=0)

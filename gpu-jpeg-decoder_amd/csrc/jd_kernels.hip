@@ -570,6 +570,63 @@ __device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts
     }
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, uint32_t(__shfl_xor(int(x), o, 64)));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += uint32_t(__shfl_xor(int(x), o, 64));
+    return x;
+}
+
+// Piece size of a large batch (one workgroup, before k_subplan): every interval of b bits is cut
+// into ceil(b / P) pieces, a lane each, and a lane walks about P + overlap bits; k_piece keeps
+// piece_plan lanes resident.  The candidates P = piece_bits * (8 + c) / 8 are scored by
+// ceil(pieces / resident) x (P + overlap) -- a partial last round of lanes takes as long as a full
+// one -- and the cheapest (the smallest P on ties) is written to counters[3] (pieces << 32 | P) for
+// k_subplan.  Counts use a float reciprocal: an estimate (k_subplan divides exactly).
+constexpr int kPlanCands = 16;
+__global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
+    __shared__ unsigned long long s_cnt[kPlanCands];
+    const uint32_t t = threadIdx.x;
+    if (t < kPlanCands) s_cnt[t] = 0;
+    __syncthreads();
+    float inv[kPlanCands];
+#pragma unroll
+    for (int c = 0; c < kPlanCands; c++) inv[c] = 8.0f / float(b.piece_bits * uint32_t(8 + c));
+    uint32_t cnt[kPlanCands] = {};
+    for (uint32_t s = t; s < b.nseg; s += blockDim.x) {
+        const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
+        const float bits = float((ce - cs) * 8u);
+#pragma unroll
+        for (int c = 0; c < kPlanCands; c++) cnt[c] += max(1u, uint32_t(ceilf(bits * inv[c])));
+    }
+#pragma unroll
+    for (int c = 0; c < kPlanCands; c++) {
+        const uint32_t w = wave_sum_u32(cnt[c]);
+        if ((t & 63u) == 0) atomicAdd(&s_cnt[c], (unsigned long long)w);
+    }
+    __syncthreads();
+    if (t == 0) {
+        double best = 1e300;
+        uint32_t pb = b.piece_bits;
+        unsigned long long np = s_cnt[0];
+        for (int c = 0; c < kPlanCands; c++) {
+            const uint32_t p = b.piece_bits * uint32_t(8 + c) / 8u;
+            const double rounds = double((s_cnt[c] + b.piece_plan - 1) / b.piece_plan);
+            const double cost = rounds * double(p + b.piece_overlap);
+            if (cost < best) {
+                best = cost;
+                pb = p;
+                np = s_cnt[c];
+            }
+        }
+        b.counters[3] = (np << 32) | pb;
+    }
+}
+
 // Per image (one wave): pieces of every interval, interval -> piece map, and each interval's
 // first region word: piece j of an interval of n pieces owns region_words(plen) words from
 // seg_ent + j * region_words(plen).  The image's spare words after them (img_pool) are handed
@@ -577,6 +634,7 @@ __device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts
 __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     const ImgDesc& im = b.imgs[blockIdx.x];
     const int lane = threadIdx.x;
+    const uint32_t piece_bits = b.piece_plan ? uint32_t(b.counters[3] & 0xFFFFFFFFull) : b.piece_bits;
     uint32_t run = 0, wrun = 0;
     for (uint32_t k0 = 0; k0 < im.nseg; k0 += 64) {
         const uint32_t k = k0 + lane;
@@ -585,13 +643,13 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
             const uint32_t s = im.seg_base + k;
             const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
             const uint32_t bits = (ce - cs) * 8;
-            n = max(1u, uint32_t((uint64_t(bits) + b.piece_bits - 1) / b.piece_bits));
+            n = max(1u, uint32_t((uint64_t(bits) + piece_bits - 1) / piece_bits));
             w = n * region_words((bits + n - 1u) / n);
         }
         const uint32_t incl = wave_incl_scan(n), wincl = wave_incl_scan(w);
         if (k < im.nseg) {
             const uint32_t s = im.seg_base + k;
-            b.seg_sub_base[s] = im.sub_base + run + incl - n;
+            b.seg_sub_base[s] = run + incl - n;  // image-relative until the image's slots are allocated
             b.seg_nsub[s] = n;
             b.seg_ent[s] = wrun + wincl - w;
         }
@@ -602,13 +660,19 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     // piece_bits) + nseg pieces, ECS bits / 2 + kRegionSlack + 4 words per piece)
     if (lane == 0) b.img_pool[blockIdx.x] = wrun;
     const uint32_t used = min(run, im.sub_cap);
+    // the image's slots: the next `used` of its table set's range (every image's share fits: the
+    // range holds the sum of their caps), so the batch's pieces are dense from the range's start
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&b.ts_cursor[im.tableset], used);
+    base = uint32_t(__shfl(int(base), 0, 64));
+    __threadfence();  // this wave's seg_sub_base / seg_nsub stores before the loads below
     for (uint32_t k = 0; k < im.nseg; k++) {
         const uint32_t s = im.seg_base + k;
-        const uint32_t base = b.seg_sub_base[s] - im.sub_base, n = b.seg_nsub[s];
+        const uint32_t off = b.seg_sub_base[s], n = b.seg_nsub[s];
+        if (lane == 0) b.seg_sub_base[s] = base + off;
         for (uint32_t u = lane; u < n; u += 64)
-            if (base + u < im.sub_cap) b.sub_seg[im.sub_base + base + u] = s;
+            if (off + u < used) b.sub_seg[base + off + u] = s;
     }
-    for (uint32_t u = used + lane; u < im.sub_cap; u += 64) b.sub_seg[im.sub_base + u] = kInvalidImage;
 }
 
 // Bytes a window round advances (the piece walks' LDS rows hold one window plus a 16-byte
@@ -744,6 +808,7 @@ struct PWalk {
     uint32_t* reg;
     uint32_t rw;
     uint32_t m_start, m_end, mcus, ents, emcu, ncp, join;
+    unsigned long long* stats;  // JD_PSTAT builds
 };
 constexpr int kSpec = 0, kRedo = 1;
 
@@ -758,6 +823,13 @@ __device__ __forceinline__ void st_ent(uint4* p, const uint4& v) {
         *p = v;
     }
 }
+
+#ifndef JD_MERGED
+#define JD_MERGED 1  // 1: warm-up and writing share one symbol loop (writes masked while warm)
+#endif
+#ifndef JD_PSTAT
+#define JD_PSTAT 0  // diagnostic builds: k_piece walk statistics summed into BatchDev::stamps[0..15]
+#endif
 
 template <int KIND>
 __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
@@ -787,7 +859,9 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     uint32_t next_cp = W.start + cp_bits, ncp = 0, join = 0;
     // an MCU end at/after end_thr leaves fewer than 8 bits: the data end (padding before RSTn/EOI)
     const uint32_t end_thr = sbits >= 8u ? sbits - 7u : 0u;
-    uint32_t thr = 0;  // the next bit at which an MCU end needs the slow branch (set when writing starts)
+    // the next bit at which an MCU end needs the slow branch: the piece start while warming up
+    // (JD_MERGED), then the next of piece end, data end, checkpoint
+    uint32_t thr = JD_MERGED ? W.warm_to : 0u;
     if (!warm) {
         uint32_t nxt = next_cp;
         if (KIND == kRedo) {
@@ -809,6 +883,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // writes the next free slot without advancing, so it is overwritten); a flush stores the
     // completed quad fq straight from the ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
+    uint32_t st_wit = 0, st_warm_wit = 0, st_lit = 0, st_lwarm = 0, st_rare = 0, st_rare_w = 0, st_rounds = 0, st_mend_w = 0, st_sym = 0;
     uint32_t prec = 0, pblk = 0;
     bool pend_b = false;
 #define JD_FLUSH_Q()                                                                                   \
@@ -829,10 +904,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         u32x4 nx[win_loads(kWin)];
 #pragma unroll
         for (int q = 0; q < win_loads(kWin); q++) nx[q] = win_load(na, q, S.last);
-        if (KIND == kSpec && __any(active && warm)) {  // wave-uniform
+        if (!JD_MERGED && KIND == kSpec && __any(active && warm)) {  // wave-uniform
             // warm-up: follow the symbols only (the write walk's table format: pair fields carry
             // the second symbol's bits and run/size byte)
+            uint32_t wit = 0;  // (JD_PSTAT)
             while (active && warm && R.rp <= kWin / 4) {
+                if (JD_PSTAT) wit++;
                 const uint32_t peek = R.peek();
                 const u32x2 E = lut_fast(tab, peek);
                 uint32_t zn, L;
@@ -867,17 +944,26 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                     }
                 }
             }
+            if (JD_PSTAT) {
+                st_warm_wit += wave_max_u32(wit);
+                st_lwarm += wit;
+            }
         }
         uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
-        while (active && !warm && R.rp <= kWin / 4) {
+        while (active && (JD_MERGED || !warm) && R.rp <= kWin / 4) {
             it++;
             const uint32_t peek = R.peek();
             const u32x2 E = lut_fast(tab, peek);
             uint32_t zn, L;
+            if (JD_PSTAT) {
+                st_rare += (E.x & kLoRare) ? 1u : 0u;
+                st_rare_w += __any(E.x & kLoRare) ? 1u : 0u;
+                st_sym += ((E.x & kLoRare) == 0 && (E.x & kLoPair)) ? 2u : 1u;
+            }
             if (E.x & kLoRare) {  // codes longer than the index, escaped magnitudes, corrupt codes
                 uint32_t e = E.y;
                 if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
-                errs |= e;
+                errs |= warm ? 0u : e;
                 const int val = huff_value(peek, e);
                 // EOB / ZRL / run-size (parser.cpp:114-134)
                 zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
@@ -890,7 +976,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 ring16[ent & 15u] = uint16_t(entry16(val, zn, big));
                 ring16[(ent + 1u) & 15u] = uint16_t(val);
                 esc_blk |= (emit && big) ? 1u : 0u;
-                ent += emit ? (big ? 2u : 1u) : 0u;
+                ent += (emit && !warm) ? (big ? 2u : 1u) : 0u;
             } else {
                 // EXTEND with the table's constants: v = s - (M1 ^ (s >> 31)) for the magnitude bits
                 // s sign-extended (none left to extract when the index resolves the value: v = -M1)
@@ -900,25 +986,25 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 L = __builtin_amdgcn_ubfe(E.x, 5u, 5u);
                 // a slot is written for every symbol; only a stored coefficient advances ent
                 ring16[ent & 15u] = uint16_t((uint32_t(v1) << 6) | zn);
-                ent += ((E.x & kLoE1) && zn < 64u) ? 1u : 0u;
+                ent += ((E.x & kLoE1) && zn < 64u && !warm) ? 1u : 0u;
                 dcd = (E.x & kLoDc) ? v1 : dcd;
                 if ((E.x & kLoPair) && zn < 63u) {  // a pair, and the first symbol left the block open
                     zn += __builtin_amdgcn_ubfe(E.y, 12u, 7u);
                     L += __builtin_amdgcn_ubfe(E.y, 19u, 4u);
                     ring16[ent & 15u] = uint16_t((uint32_t(int(E.y) >> 23) << 6) | zn);
-                    ent += ((E.x & kLoE2) && zn < 64u) ? 1u : 0u;
+                    ent += ((E.x & kLoE2) && zn < 64u && !warm) ? 1u : 0u;
                 }
             }
             R.skip(L, row);
             const bool fin = zn >= 63u;
             prec = fin ? block_rec(ent - ent_blk, dcd, esc_blk) : prec;
             pblk = fin ? blk : pblk;
-            pend_b = pend_b || fin;
+            pend_b = pend_b || (fin && !warm);
             if ((it & 1u) == 0u) {
                 JD_FLUSH_Q();
                 JD_FLUSH_B();
             }
-            blk += fin ? 1u : 0u;
+            blk += (fin && !warm) ? 1u : 0u;
             ent_blk = fin ? ent : ent_blk;
             esc_blk = fin ? 0u : esc_blk;
             z = fin ? 0u : zn;
@@ -929,9 +1015,18 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             const bool mend = b3 == bpm3;
             b3 = mend ? 0u : b3;
             tab = mend ? tab_dc0 : tab;
-            mcus += mend ? 1u : 0u;
+            mcus += (mend && !warm) ? 1u : 0u;
+            if (JD_PSTAT) st_mend_w += __any(mend && (R.bit() >= thr || (errs & kEntBad))) ? 1u : 0u;
             if (mend && (R.bit() >= thr || (errs & kEntBad))) {
                 const uint32_t consumed = R.bit();
+                if (JD_MERGED && KIND == kSpec && warm) {  // synchronised (or assumed so): the piece starts here
+                    warm = false;
+                    m_start = m_end = consumed;
+                    next_cp = consumed + cp_bits;
+                    thr = min(min(W.stop_at, end_thr), next_cp);
+                    if (consumed + 8 > sbits) active = false;
+                    continue;
+                }
                 if ((errs & kEntBad) || consumed > sbits) {  // an error in this MCU
                     emcu = min(emcu, mcus - 1u);
                     errs = 0;
@@ -975,6 +1070,11 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             emcu = min(emcu, mcus);
             active = false;
         }
+        if (JD_PSTAT) {
+            st_wit += wave_max_u32(it);
+            st_lit += it;
+            st_rounds++;
+        }
         if (__ballot(active) == 0) break;  // wave-uniform
 #pragma unroll
         for (int q = 0; q < win_loads(kWin); q++) JD_ROW_FILL(row, nx[q], q);
@@ -992,6 +1092,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     W.emcu = emcu;
     W.ncp = ncp;
     W.join = join;
+    if (JD_PSTAT && KIND == kSpec && W.stats) {
+        const uint32_t v[10] = {st_wit, st_warm_wit, wave_sum_u32(st_lit), wave_sum_u32(st_lwarm), wave_sum_u32(st_rare),
+                                wave_max_u32(st_rare_w), st_rounds, 1u, wave_max_u32(st_mend_w), wave_sum_u32(st_sym)};
+        if ((threadIdx.x & 63u) == 0)
+            for (int k = 0; k < 10; k++) atomicAdd(W.stats + k, (unsigned long long)v[k]);
+    }
 }
 
 __device__ __forceinline__ void table_slots(const TableSet& ts, const SegInfo& S, uint32_t& dcp, uint32_t& acp) {
@@ -1052,6 +1158,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     W.stop_at = piece_stop(P);
     W.reg = S.eimg + P.own;
     W.rw = P.rw;
+    W.stats = b.stamps;
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     const uint32_t none[kCpMax] = {};
     walk_piece<kSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWin),
@@ -1091,6 +1198,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
 #pragma unroll
     for (int c = 0; c < kCpMax; c++) cpb[c] = (need && uint32_t(c) < ncp) ? cp[c].bit : 0xFFFFFFFFu;
     PWalk W;
+    W.stats = nullptr;
     W.start = W.warm_to = expect;
     W.stop_at = piece_stop(P);
     W.reg = S.eimg + base;
@@ -2212,7 +2320,7 @@ __device__ __forceinline__ void zero_staging(uint32_t* s_buf, uint32_t lane) {
 //  * EXACT = true (k_idct_color_exact) decodes those tiles with the exact IDCT form.
 template <bool EXACT, int M, class Mid>
 __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDesc& im, uint32_t img, uint32_t tile,
-                                                 const TileGeo& G, const TileLaneGeo& L, int dc_pred,
+                                                 const TileGeo& G, const TileLaneGeo& L, int dc_pred, bool esc,
                                                  uint32_t* s_buf, const int* s_qz, Mid&& mid) {
     const uint32_t lane = threadIdx.x;
     using TM_ = TMode<M>;
@@ -2241,13 +2349,18 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
     const uint4* qz4 = reinterpret_cast<const uint4*>(s_qz + comp * 36);
     const int dq0 = dc_pred * int(reinterpret_cast<const uint16_t*>(s_qz)[comp * 72]);
     if (!EXACT) {  // range test before dequantising: the branch then holds no 64-value block
-        uint32_t acc = 0;
+        // When the quant steps are below 64 (qmask bit 9 clear: k >= 10), every value of a 16-bit
+        // slot (|v| <= 511) passes, so only a wave with an escaped value tests its coefficients.
+        bool in_range = !have || uint32_t(dq0 + 32768) <= 65535u;
+        if ((im.qmask & 0x200u) || __any(have && esc)) {  // wave-uniform
+            uint32_t acc = 0;
 #pragma unroll
-        for (int p = 0; p < 32; p++) {
-            const uint32_t w = rw[p];
-            acc |= w ^ (w << 1);
+            for (int p = 0; p < 32; p++) {
+                const uint32_t w = rw[p];
+                acc |= w ^ (w << 1);
+            }
+            in_range = in_range && (!have || (acc & im.qmask) == 0);
         }
-        const bool in_range = !have || ((acc & im.qmask) == 0 && uint32_t(dq0 + 32768) <= 65535u);
         if (!__all(in_range)) {  // wave-uniform
             if (lane == 0) {
                 const uint32_t k = uint32_t(atomicAdd(&b.counters[1], 1ull));
@@ -2490,7 +2603,7 @@ __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDe
         scatter_entries(s_buf, staging_base(lane), R, E);
         __syncthreads();
         JD_STAMP_AT(2);
-        idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
+        idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, R.esc, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
         JD_STAMP_AT(4);
     };
 #pragma unroll
@@ -2521,7 +2634,7 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
         load_entry_quads(R, E);
         scatter_entries(s_buf, staging_base(lane), R, E);
         __syncthreads();
-        idct_colour_tile<true, kModeGen>(b, im, tr.img, tr.tile, G, L, dc_pred, s_buf, s_qz, [] {});
+        idct_colour_tile<true, kModeGen>(b, im, tr.img, tr.tile, G, L, dc_pred, R.esc, s_buf, s_qz, [] {});
     }
 }
 
@@ -2635,6 +2748,21 @@ __global__ void k_test_color(const int32_t* ycc, uint8_t* rgb, int n) {
 // ------------------------------------------------------------------------------------------
 size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots); }
 
+uint32_t piece_lanes_resident(size_t lds) {
+    static size_t cached_lds = 0;
+    static uint32_t cached = 0;
+    if (lds == cached_lds && cached) return cached;
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    if (lds > 65536)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_piece), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_piece, kPieceThreads, lds) != hipSuccess || nb <= 0) return 0;
+    cached_lds = lds;
+    cached = uint32_t(nb) * uint32_t(cus) * uint32_t(kPieceThreads);
+    return cached;
+}
+
 // Dynamic LDS above 64 KiB (large piece workgroups) has to be allowed per kernel once.
 static hipError_t allow_lds(size_t lds) {
     static size_t allowed = 65536;
@@ -2668,6 +2796,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             // every slot not claimed by an interval (per-image slack, padding) must read invalid
             const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
             if (e != hipSuccess) return e;
+            if (b.piece_plan) hipLaunchKernelGGL(k_pieceplan, dim3(1), dim3(1024), 0, s, b);
             hipLaunchKernelGGL(k_subplan, dim3(b.nimg), dim3(64), 0, s, b);
             break;
         }

@@ -12,6 +12,9 @@ namespace jd {
 // 5 k_rescan, 6 k_chain, 7 k_piece_write (Huffman), 8 k_dc_pred, 9 k_idct_color.
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s);
 size_t huffman_lds_bytes(uint32_t max_slots);
+// Piece lanes k_piece keeps resident on the device at this dynamic LDS (workgroups per CU x CUs x
+// workgroup size); k_pieceplan fits the batch's pieces to whole rounds of them.
+uint32_t piece_lanes_resident(size_t lds);
 
 // Known-answer hooks: run exactly the device arithmetic of stage 3 on caller data.
 hipError_t launch_test_idct(const int32_t* in_zz, int32_t* out, int nblocks, int exact_only, hipStream_t s);

@@ -166,6 +166,7 @@ struct jd_ctx {
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     int64_t spare_pieces = -1;          // spare re-walk regions per image (JD_SPARE_PIECES; -1: default)
     int64_t piece_overlap = -1;         // warm-up bits (JD_PIECE_OVERLAP_BITS; -1: default)
+    bool fixed_pieces = false;          // JD_FIXED_PIECES: keep the host's piece size (no k_pieceplan)
     jd_stats stats{};
 
     std::vector<ParsedJpeg> parsed;
@@ -264,6 +265,7 @@ struct Plan {
     std::vector<TableSet> tablesets;
     std::vector<uint16_t> qtabs;
     std::vector<uint32_t> seg_img, wg_tableset;
+    std::vector<uint32_t> ts_slot0;  // first piece slot of each table set's range (k_subplan allocates from it)
     uint32_t piece_bits = kPieceBits, piece_overlap = kPieceOverlap;
     std::vector<uint32_t> chain_seg, chain_wg_tableset;  // k_chain lanes, grouped by table set
     uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0;
@@ -561,8 +563,10 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     if (ctx->piece_overlap >= 0) P.piece_overlap = uint32_t(ctx->piece_overlap);
     uint64_t sub = 0, entry_cursor = 0;
     P.chain_seg.reserve(seg_cursor + kPieceThreads * P.tablesets.size());
+    P.ts_slot0.assign(P.tablesets.size(), 0u);
     for (size_t oi = 0; oi < order.size();) {
         const int ts = pim[order[oi]].ts;
+        P.ts_slot0[ts] = uint32_t(sub);
         for (; oi < order.size() && pim[order[oi]].ts == ts; oi++) {
             ImgDesc& d = P.imgs[order[oi]];
             d.sub_base = uint32_t(sub);
@@ -705,6 +709,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_modes = put(blob, P.mode_imgs);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
         const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // entries, slow tiles, IDCT queue
+        const size_t o_tscur = put(blob, P.ts_slot0);
         const size_t upload = blob.size();
         // device-written scratch after the uploaded part (no initialisation needed)
         size_t end = upload;
@@ -751,10 +756,15 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.sub_seg = reinterpret_cast<uint32_t*>(base + o_subseg);
         b.nsub = uint32_t(nsub);
         b.wg_tableset = reinterpret_cast<const uint32_t*>(base + o_wgts);
+        b.ts_cursor = reinterpret_cast<uint32_t*>(base + o_tscur);
         b.chain_seg = reinterpret_cast<const uint32_t*>(base + o_chain);
         b.nchain = uint32_t(P.chain_seg.size());
         b.chain_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_chts);
         b.piece_bits = P.piece_bits;
+        // large batches: k_pieceplan picks the piece size (>= piece_bits) that fits the pieces to
+        // whole rounds of k_piece's resident lanes
+        b.piece_plan = (P.piece_bits == kPieceBits && !(ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES)) &&
+                        !ctx->fixed_pieces) ? piece_lanes_resident(huffman_lds_bytes(P.max_slots)) : 0u;
         b.no_pool = ctx->spare_pieces == 0 ? 1u : 0u;
         b.piece_overlap = P.piece_overlap;
         uint32_t* pc[9];
@@ -816,9 +826,9 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             for (int k = 0; k < JD_NUM_KERNELS; k++) std::fprintf(stderr, " %.3f", t_k[k]);
             std::fprintf(stderr, "\n");
         }
-        HIPCHK(ctx, ensure_pinned(pd.host, pd.host_cap, 16 + size_t(nimg) * 4));
-        HIPCHK(ctx, hipMemcpyAsync(pd.host, b.counters, 16, hipMemcpyDeviceToHost, s));
-        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(pd.host) + 16, b.status, nimg * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, ensure_pinned(pd.host, pd.host_cap, 32 + size_t(nimg) * 4));
+        HIPCHK(ctx, hipMemcpyAsync(pd.host, b.counters, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(pd.host) + 32, b.status, nimg * 4, hipMemcpyDeviceToHost, s));
         pd.timing = timing;
         pd.fancy = fancy;
         pd.blocks = double(P.total_blocks);
@@ -865,7 +875,7 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
     const uint32_t nimg = pd.nimg;
     if (nimg) {
         const unsigned long long* ctr = static_cast<const unsigned long long*>(pd.host);
-        const uint32_t* status = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pd.host) + 16);
+        const uint32_t* status = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pd.host) + 32);
         for (uint32_t i = 0; i < nimg; i++)
             if (status[i]) pd.pst[size_t(pd.item_of_img[i] - pd.lo)] = JD_ERR_CORRUPT;
         if (ctx->host_timing)
@@ -875,9 +885,14 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
         // algorithmic bytes per kernel
         jd_stats& S = ctx->stats;
         const double entries = double(ctr[0]);  // 16-bit AC-entry slots
-        const double blocks = pd.blocks, ecs = pd.ecs, nsubd = pd.nsub, nsegd = pd.nseg;
+        const double blocks = pd.blocks, ecs = pd.ecs, nsegd = pd.nseg;
+        double nsubd = pd.nsub;
         const bool fancy = pd.fancy;
-        const double overlap_factor = (pd.piece_bits + pd.piece_overlap) / pd.piece_bits;
+        // k_pieceplan's choice (counters[3] = pieces << 32 | piece bits), else the host's
+        const double piece_bits = (ctr[3] & 0xFFFFFFFFull) ? double(ctr[3] & 0xFFFFFFFFull) : pd.piece_bits;
+        if (ctr[3] >> 32) nsubd = double(ctr[3] >> 32);
+        pd.piece_bits = piece_bits;
+        const double overlap_factor = (piece_bits + pd.piece_overlap) / piece_bits;
         const double bytes[JD_NUM_KERNELS] = {
             ecs,                                               // k_scan: read the ECS once
             pd.chunks * 12 + nsegd * 8,                        // k_index: per-chunk counters, boundaries
@@ -987,6 +1002,7 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     // test knobs: fewer spare regions (re-walks fall back to their own region, no join) and a
     // shorter warm-up (many speculative starts fail)
     if (const char* e = std::getenv("JD_SPARE_PIECES")) ctx->spare_pieces = std::strtoll(e, nullptr, 0);
+    if (const char* e = std::getenv("JD_FIXED_PIECES")) ctx->fixed_pieces = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
