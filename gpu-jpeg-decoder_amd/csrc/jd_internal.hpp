@@ -51,14 +51,15 @@ JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
 // piece walks use its fields as instruction operands (v_bfe_i32 takes its offset from lo[4:0] and
 // its width from hi[4:0]):
 //   lo  bits 0..4   o1   32 - L1: offset in the 32-bit peek of the first symbol's magnitude
-//       bits 5..9   L1   bits of the first symbol, code + magnitude (<= 31)
-//       bit  10     DC   DC symbol
-//       bit  11     E1   the first symbol stores a coefficient (AC, size != 0)
-//       bit  12     P    a second AC symbol follows within the index (pair)
-//       bit  13     E2   the second symbol stores a coefficient
+//       bit  5      DC   DC symbol
+//       bit  6      E1   the first symbol stores a coefficient (AC, size != 0); bit 6 so that
+//                        lo & ~zn & 64 is its emit test (zn < 64)
+//       bit  7      E2   the second symbol stores a coefficient (tested against zn << 1)
+//       bit  8      P    a second AC symbol follows within the index (pair)
+//       bits 9..13  L1   bits of the first symbol, code + magnitude (<= 31)
 //       bit  15     R    rare: hi holds the 32-bit entry above (0: a code longer than kLutBits);
 //                        codes longer than kLutBits, AC magnitudes of 10 bits or more (they need an
-//                        escaped slot), DC sizes above 11
+//                        escaped slot), DC sizes above 11.  lo = R alone (no flags, no pair)
 //       bits 16..31 M1   int16: the coefficient is s - (M1 ^ (s >> 31)) for s = the magnitude bits
 //                        sign-extended (v_bfe_i32 of width w1): M1 = 2^sz - 1 when the magnitude
 //                        reaches beyond the index, else w1 = 0 and M1 = -value
@@ -80,7 +81,8 @@ struct alignas(16) HuffLut {
 };
 static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
 constexpr int kLutWords = int(sizeof(HuffLut) / 4);
-constexpr uint32_t kLoDc = 1u << 10, kLoE1 = 1u << 11, kLoPair = 1u << 12, kLoE2 = 1u << 13, kLoRare = 1u << 15;
+constexpr uint32_t kLoDc = 1u << 5, kLoE1 = 1u << 6, kLoE2 = 1u << 7, kLoPair = 1u << 8, kLoRare = 1u << 15;
+constexpr uint32_t kLoL1Shift = 9;
 
 // Maximum Huffman tables a table set (one workgroup of the Huffman kernel) stages into LDS.
 constexpr int kSlotsPerSet = 6;

@@ -824,9 +824,6 @@ __device__ __forceinline__ void st_ent(uint4* p, const uint4& v) {
     }
 }
 
-#ifndef JD_MERGED
-#define JD_MERGED 1  // 1: warm-up and writing share one symbol loop (writes masked while warm)
-#endif
 #ifndef JD_PSTAT
 #define JD_PSTAT 0  // diagnostic builds: k_piece walk statistics summed into BatchDev::stamps[0..15]
 #endif
@@ -859,9 +856,9 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     uint32_t next_cp = W.start + cp_bits, ncp = 0, join = 0;
     // an MCU end at/after end_thr leaves fewer than 8 bits: the data end (padding before RSTn/EOI)
     const uint32_t end_thr = sbits >= 8u ? sbits - 7u : 0u;
-    // the next bit at which an MCU end needs the slow branch: the piece start while warming up
-    // (JD_MERGED), then the next of piece end, data end, checkpoint
-    uint32_t thr = JD_MERGED ? W.warm_to : 0u;
+    // the next bit at which an MCU end needs the slow branch: the piece start while warming up,
+    // then the next of piece end, data end, checkpoint (0 after an error)
+    uint32_t thr = W.warm_to;
     if (!warm) {
         uint32_t nxt = next_cp;
         if (KIND == kRedo) {
@@ -883,7 +880,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // writes the next free slot without advancing, so it is overwritten); a flush stores the
     // completed quad fq straight from the ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
-    uint32_t st_wit = 0, st_warm_wit = 0, st_lit = 0, st_lwarm = 0, st_rare = 0, st_rare_w = 0, st_rounds = 0, st_mend_w = 0, st_sym = 0;
+    uint32_t st_wit = 0, st_lit = 0, st_rare = 0, st_rare_w = 0, st_rounds = 0, st_mend_w = 0, st_sym = 0;
     uint32_t prec = 0, pblk = 0;
     bool pend_b = false;
 #define JD_FLUSH_Q()                                                                                   \
@@ -899,76 +896,56 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         if (pend_b && (!(JD_ABL & 16) || ent == 0x7FFFFFFFu)) rec_top[-int(pblk)] = prec; \
         pend_b = false;                                                  \
     } while (0)
+    // Warm-up and writing share one symbol loop: while warm, a lane follows the symbols only (its
+    // slot count, block count and MCU count stay 0, errors are ignored) until the first MCU
+    // boundary at/after warm_to, where the piece starts.
+    uint32_t pos = W.start;                          // == R.bit(): the stream bit of the next symbol
+    uint32_t wm = warm ? 0u : 64u, wm2 = wm << 1;    // emit masks: 0 while warm
     while (true) {
         const uintptr_t na = wa + kWin;
         u32x4 nx[win_loads(kWin)];
 #pragma unroll
         for (int q = 0; q < win_loads(kWin); q++) nx[q] = win_load(na, q, S.last);
-        if (!JD_MERGED && KIND == kSpec && __any(active && warm)) {  // wave-uniform
-            // warm-up: follow the symbols only (the write walk's table format: pair fields carry
-            // the second symbol's bits and run/size byte)
-            uint32_t wit = 0;  // (JD_PSTAT)
-            while (active && warm && R.rp <= kWin / 4) {
-                if (JD_PSTAT) wit++;
-                const uint32_t peek = R.peek();
-                const u32x2 E = lut_fast(tab, peek);
-                uint32_t zn, L;
-                if (E.x & kLoRare) {
-                    uint32_t e = E.y;
-                    if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
-                    zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
-                    L = e & 31u;
-                } else {
-                    zn = z + __builtin_amdgcn_ubfe(E.y, 5u, 7u);
-                    L = __builtin_amdgcn_ubfe(E.x, 5u, 5u);
-                    if ((E.x & kLoPair) && zn < 63u) {
-                        zn += __builtin_amdgcn_ubfe(E.y, 12u, 7u);
-                        L += __builtin_amdgcn_ubfe(E.y, 19u, 4u);
-                    }
-                }
-                R.skip(L, row);
-                const bool fin = zn >= 63u;
-                z = fin ? 0u : zn;
-                b3 += fin ? 3u : 0u;
-                tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
-                if (b3 == bpm3) {  // an MCU ends here
-                    b3 = 0;
-                    tab = tab_dc0;
-                    const uint32_t consumed = R.bit();
-                    if (consumed >= W.warm_to) {  // synchronised (or assumed so): the piece starts here
-                        warm = false;
-                        m_start = m_end = consumed;
-                        next_cp = consumed + cp_bits;
-                        thr = min(min(W.stop_at, end_thr), next_cp);
-                        if (consumed + 8 > sbits) active = false;
-                    }
-                }
-            }
-            if (JD_PSTAT) {
-                st_warm_wit += wave_max_u32(wit);
-                st_lwarm += wit;
-            }
-        }
         uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
-        while (active && (JD_MERGED || !warm) && R.rp <= kWin / 4) {
+        while (active && R.rp <= kWin / 4) {
             it++;
             const uint32_t peek = R.peek();
             const u32x2 E = lut_fast(tab, peek);
-            uint32_t zn, L;
+            const uint32_t lo = E.x, hi = E.y;
             if (JD_PSTAT) {
-                st_rare += (E.x & kLoRare) ? 1u : 0u;
-                st_rare_w += __any(E.x & kLoRare) ? 1u : 0u;
-                st_sym += ((E.x & kLoRare) == 0 && (E.x & kLoPair)) ? 2u : 1u;
+                st_rare += (lo & kLoRare) ? 1u : 0u;
+                st_rare_w += __any(lo & kLoRare) ? 1u : 0u;
+                st_sym += ((lo & kLoRare) == 0 && (lo & kLoPair)) ? 2u : 1u;
             }
-            if (E.x & kLoRare) {  // codes longer than the index, escaped magnitudes, corrupt codes
-                uint32_t e = E.y;
+            // The table's entry (jd_internal.hpp HuffLut).  A rare entry (lo = kLoRare: no flags,
+            // no pair) passes through this part without effect and is decoded below.
+            // EXTEND with the table's constants: v = s - (M1 ^ (s >> 31)) for the magnitude bits s
+            // sign-extended (none left to extract when the index resolves the value: v = -M1).
+            const int s1 = __builtin_amdgcn_sbfe(int(peek), lo, hi);
+            const int v1 = s1 - ((int(lo) >> 16) ^ (s1 >> 31));
+            uint32_t zn = z + __builtin_amdgcn_ubfe(hi, 5u, 7u);
+            uint32_t L = __builtin_amdgcn_ubfe(lo, kLoL1Shift, 5u);
+            // a slot is written for every symbol; a stored coefficient (E1, zn < 64, not warm:
+            // bit 6 of lo & ~zn & wm) advances ent
+            ring16[ent & 15u] = uint16_t((uint32_t(v1) << 6) | zn);
+            ent += (lo & ~zn & wm) >> 6;
+            dcd = (lo & kLoDc) ? v1 : dcd;
+            // the second symbol of a pair, when the first left the block open (its slot goes to
+            // the next free position either way; E2 is bit 7 of lo)
+            const bool pr = (lo & kLoPair) && zn < 63u;
+            const uint32_t zn2 = zn + __builtin_amdgcn_ubfe(hi, 12u, 7u);
+            ring16[ent & 15u] = uint16_t((uint32_t(int(hi) >> 23) << 6) | zn2);
+            ent += pr ? (lo & ~(zn2 << 1) & wm2) >> 7 : 0u;
+            L += pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : 0u;
+            zn = pr ? zn2 : zn;
+            if (lo & kLoRare) {  // codes longer than the index, escaped magnitudes, corrupt codes
+                uint32_t e = hi;
                 if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
-                errs |= warm ? 0u : e;
                 const int val = huff_value(peek, e);
                 // EOB / ZRL / run-size (parser.cpp:114-134)
                 zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
                 L = e & 31u;
-                const bool emit = (e & ~zn & kEntEmit) != 0;  // zn < 64 (bit 6 of zn clear)
+                const bool emit = (e & ~zn & wm) != 0;  // kEntEmit is bit 6: zn < 64, not warm
                 dcd = (e & kEntDc) ? val : dcd;
                 // the escaped value goes to the next slot unconditionally (a free slot, overwritten
                 // by the next entry unless the value needed it)
@@ -976,26 +953,14 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 ring16[ent & 15u] = uint16_t(entry16(val, zn, big));
                 ring16[(ent + 1u) & 15u] = uint16_t(val);
                 esc_blk |= (emit && big) ? 1u : 0u;
-                ent += (emit && !warm) ? (big ? 2u : 1u) : 0u;
-            } else {
-                // EXTEND with the table's constants: v = s - (M1 ^ (s >> 31)) for the magnitude bits
-                // s sign-extended (none left to extract when the index resolves the value: v = -M1)
-                const int s1 = __builtin_amdgcn_sbfe(int(peek), E.x, E.y);
-                const int v1 = s1 - ((int(E.x) >> 16) ^ (s1 >> 31));
-                zn = z + __builtin_amdgcn_ubfe(E.y, 5u, 7u);
-                L = __builtin_amdgcn_ubfe(E.x, 5u, 5u);
-                // a slot is written for every symbol; only a stored coefficient advances ent
-                ring16[ent & 15u] = uint16_t((uint32_t(v1) << 6) | zn);
-                ent += ((E.x & kLoE1) && zn < 64u && !warm) ? 1u : 0u;
-                dcd = (E.x & kLoDc) ? v1 : dcd;
-                if ((E.x & kLoPair) && zn < 63u) {  // a pair, and the first symbol left the block open
-                    zn += __builtin_amdgcn_ubfe(E.y, 12u, 7u);
-                    L += __builtin_amdgcn_ubfe(E.y, 19u, 4u);
-                    ring16[ent & 15u] = uint16_t((uint32_t(int(E.y) >> 23) << 6) | zn);
-                    ent += ((E.x & kLoE2) && zn < 64u && !warm) ? 1u : 0u;
+                ent += emit ? (big ? 2u : 1u) : 0u;
+                if ((e & kEntBad) && !warm) {  // the next MCU end takes the branch below
+                    errs = 1u;
+                    thr = 0u;
                 }
             }
             R.skip(L, row);
+            pos += L;
             const bool fin = zn >= 63u;
             prec = fin ? block_rec(ent - ent_blk, dcd, esc_blk) : prec;
             pblk = fin ? blk : pblk;
@@ -1011,23 +976,25 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             b3 += fin ? 3u : 0u;
             tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
             // MCU end: the common case only counts; the branch is taken at the next threshold
-            // (piece end, data end, checkpoint) or after an error
+            // (piece start while warm, piece end, data end, checkpoint) or after an error
             const bool mend = b3 == bpm3;
             b3 = mend ? 0u : b3;
             tab = mend ? tab_dc0 : tab;
             mcus += (mend && !warm) ? 1u : 0u;
-            if (JD_PSTAT) st_mend_w += __any(mend && (R.bit() >= thr || (errs & kEntBad))) ? 1u : 0u;
-            if (mend && (R.bit() >= thr || (errs & kEntBad))) {
-                const uint32_t consumed = R.bit();
-                if (JD_MERGED && KIND == kSpec && warm) {  // synchronised (or assumed so): the piece starts here
+            if (JD_PSTAT) st_mend_w += __any(mend && pos >= thr) ? 1u : 0u;
+            if (mend && pos >= thr) {
+                const uint32_t consumed = pos;
+                if (KIND == kSpec && warm) {  // synchronised (or assumed so): the piece starts here
                     warm = false;
+                    wm = 64u;
+                    wm2 = 128u;
                     m_start = m_end = consumed;
                     next_cp = consumed + cp_bits;
                     thr = min(min(W.stop_at, end_thr), next_cp);
                     if (consumed + 8 > sbits) active = false;
                     continue;
                 }
-                if ((errs & kEntBad) || consumed > sbits) {  // an error in this MCU
+                if (errs || consumed > sbits) {  // an error in this MCU
                     emcu = min(emcu, mcus - 1u);
                     errs = 0;
                 }
@@ -1093,7 +1060,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     W.ncp = ncp;
     W.join = join;
     if (JD_PSTAT && KIND == kSpec && W.stats) {
-        const uint32_t v[10] = {st_wit, st_warm_wit, wave_sum_u32(st_lit), wave_sum_u32(st_lwarm), wave_sum_u32(st_rare),
+        const uint32_t v[10] = {st_wit, 0u, wave_sum_u32(st_lit), 0u, wave_sum_u32(st_rare),
                                 wave_max_u32(st_rare_w), st_rounds, 1u, wave_max_u32(st_mend_w), wave_sum_u32(st_sym)};
         if ((threadIdx.x & 63u) == 0)
             for (int k = 0; k < 10; k++) atomicAdd(W.stats + k, (unsigned long long)v[k]);

@@ -211,7 +211,7 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
             w1 = sz1;
             m1 = int32_t((1u << sz1) - 1u);
         }
-        lo = ((32u - L1) & 31u) | (L1 << 5) | (is_dc ? kLoDc : 0u) | ((!is_dc && sz1) ? kLoE1 : 0u) |
+        lo = ((32u - L1) & 31u) | (L1 << kLoL1Shift) | (is_dc ? kLoDc : 0u) | ((!is_dc && sz1) ? kLoE1 : 0u) |
              (uint32_t(m1) << 16);
         hi = w1 | (adv1 << 5);
         // pair: the following AC symbol, when the first is not EOB and both lie within the index
