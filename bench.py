@@ -218,7 +218,8 @@ def measured_traffic(config: str, kernel: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC traffic profile of this
     config (profiles/<round>_traffic.json, tools/profile_summary.py), or None."""
     k, src = newest_profile("*_traffic.json", config, kernel)
-    return (k["hbm_bytes"], src) if k else None
+    # per timing slot: a slot may dispatch several instances per batch (one per sampling layout)
+    return (k.get("hbm_bytes_per_batch", k["hbm_bytes"]), src) if k else None
 
 
 def valu_issue(config: str, kernel: str, avg_ms: float):
@@ -229,9 +230,10 @@ def valu_issue(config: str, kernel: str, avg_ms: float):
     if not k or avg_ms <= 0:
         return None
     clk = k.get("clock_ghz") or 2.4
-    busy = k.get("counters", {}).get("SQ_ACTIVE_INST_VALU") or k["valu_insts"]
+    n = k.get("dispatches_per_batch", 1.0)  # instances per timing slot (one per sampling layout)
+    busy = (k.get("counters", {}).get("SQ_ACTIVE_INST_VALU") or k["valu_insts"]) * n
     frac = busy * VALU_CYCLES_PER_QUAD / (SIMDS * clk * 1e9 * avg_ms * 1e-3)
-    return {"valu_insts_per_launch": k["valu_insts"], "clock_ghz": clk, "busy_frac": frac,
+    return {"valu_insts_per_launch": k["valu_insts"] * n, "dispatches_per_batch": n, "clock_ghz": clk, "busy_frac": frac,
             "note": "VALU-busy SIMD cycles (SQ_ACTIVE_INST_VALU quad-cycles x 4) over the launch's SIMD cycles",
             "source": src}
 

@@ -12,7 +12,7 @@ Per config:
   profiles/TAG_sq_<cfg>.json           SQ counters per kernel (C2, C5): instruction counts, wave-cycle
                                        split, clock held (GRBM_GUI_ACTIVE / 8 XCDs / dispatch time)
 Kernel names drop their template arguments (k_idct_color<1> -> k_idct_color; per-launch averages
-over the instances that ran).  bench.py reads traffic and valu_insts/clock_ghz from these files.
+over the instances that ran, with the dispatches per batch beside them).  bench.py reads traffic and valu_insts/clock_ghz from these files.
 """
 import collections
 import csv
@@ -40,7 +40,14 @@ def counters(d):
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             if r["Counter_Name"] in ("GRBM_GUI_ACTIVE",):
                 vals[k]["_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
-    return {k: {n: sum(v) / len(v) for n, v in c.items()} for k, c in vals.items()}
+    out = {k: {n: sum(v) / len(v) for n, v in c.items()} for k, c in vals.items()}
+    # dispatches of each kernel name per batch (k_scan runs once per batch): a timing slot such as
+    # k_idct_color launches one instance per sampling layout present, so per-slot figures are the
+    # per-dispatch averages times this
+    nb = max(len(v) for v in vals.get("k_scan", {"": [1]}).values()) if vals else 1
+    for k, c in vals.items():
+        out[k]["_per_batch"] = max(len(v) for n, v in c.items() if not n.startswith("_")) / nb
+    return out
 
 
 for c in cfgs:
@@ -60,7 +67,9 @@ for c in cfgs:
         for k in sorted(set(fe) | set(wr)):
             f = fe.get(k, {}).get("FETCH_SIZE", 0.0) * 1024.0
             w = wr.get(k, {}).get("WRITE_SIZE", 0.0) * 1024.0
-            out["kernels"][k] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes": 2 * f + w}
+            n = (fe.get(k) or wr.get(k))["_per_batch"]
+            out["kernels"][k] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes": 2 * f + w,
+                                 "dispatches_per_batch": n, "hbm_bytes_per_batch": (2 * f + w) * n}
         json.dump(out, open(os.path.join(prof, f"{tag}_{c}_traffic.json"), "w"), indent=1)
     sq = counters(os.path.join(run, f"{c}_sq"))
     if sq:
@@ -71,7 +80,7 @@ for c in cfgs:
                  "lds_insts": m.get("SQ_INSTS_LDS"), "vmem_rd_insts": m.get("SQ_INSTS_VMEM_RD"),
                  "vmem_wr_insts": m.get("SQ_INSTS_VMEM_WR"), "waves": m.get("SQ_WAVES"),
                  "lds_bank_conflict_frac": (m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"])
-                 if m.get("SQ_LDS_IDX_ACTIVE") else None}
+                 if m.get("SQ_LDS_IDX_ACTIVE") else None, "dispatches_per_batch": m["_per_batch"]}
             wc = m.get("SQ_WAVE_CYCLES")
             if wc:
                 e["wave_cycles_split"] = {"active": m.get("SQ_ACTIVE_INST_ANY", 0) / wc,
