@@ -1806,6 +1806,40 @@ constexpr uint32_t pk16(int lo, int hi) { return (uint32_t(lo) & 0xFFFFu) | (uin
 __device__ __forceinline__ int dot2(uint32_t a, uint32_t k, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, k), c, false);
 }
+// The same as one VOP3P v_dot2_i32_i16 with its own accumulator operand: the builtin compiles to the
+// tied-accumulator v_dot2c form, which costs a v_mov per product to seed the accumulator (64 per
+// block).  k: the constant pair, in an SGPR (the one scalar operand VOP3P allows); the accumulator
+// is the inline constant 0 (dot2_0) or a VGPR (dot2_v).
+#ifndef JD_DOT2_ASM
+#define JD_DOT2_ASM 1
+#endif
+#ifndef JD_PACK_PERM
+#define JD_PACK_PERM 1
+#endif
+#ifndef JD_ZERO_ASM
+#define JD_ZERO_ASM 0  // 1: one hoisted zero quad (asm), 2: lane bound only; both measured slower
+#endif
+#ifndef JD_HALVES
+#define JD_HALVES 1
+#endif
+__device__ __forceinline__ int dot2_0(uint32_t a, uint32_t k) {
+#if JD_DOT2_ASM
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "s"(k));
+    return r;
+#else
+    return dot2(a, k, 0);
+#endif
+}
+__device__ __forceinline__ int dot2_v(uint32_t a, uint32_t k, int c) {
+#if JD_DOT2_ASM
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
+    return r;
+#else
+    return dot2(a, k, c);
+#endif
+}
 // (natural n_lo, natural n_hi) as one int16 pair from the zig-zag pair words dw
 __device__ __forceinline__ uint32_t nat_pair(const uint32_t (&dw)[32], int n_lo, int n_hi) {
     const int zl = kZzOfNat.v[n_lo], zh = kZzOfNat.v[n_hi];
@@ -1813,17 +1847,17 @@ __device__ __forceinline__ uint32_t nat_pair(const uint32_t (&dw)[32], int n_lo,
                          (uint32_t(5 + 2 * (zh & 1)) << 24);
     return __builtin_amdgcn_perm(dw[zh >> 1], dw[zl >> 1], sel);
 }
-__device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, int* out) {
+__device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, int* out, int c128) {
     const uint32_t P0 = nat_pair(dw, 8 * r + 0, 8 * r + 4), P1 = nat_pair(dw, 8 * r + 1, 8 * r + 7);
     const uint32_t P2 = nat_pair(dw, 8 * r + 5, 8 * r + 3), P3 = nat_pair(dw, 8 * r + 2, 8 * r + 6);
-    int x8 = dot2(P0, pk16(2048, 2048), 128);
-    int y0 = dot2(P0, pk16(2048, -2048), 128);
-    int x4 = dot2(P1, pk16(kC1, kC7), 0);
-    int x5 = dot2(P1, pk16(kC7, -kC1), 0);
-    int x6 = dot2(P2, pk16(kC5, kC3), 0);
-    int x7 = dot2(P2, pk16(kC3, -kC5), 0);
-    int x2 = dot2(P3, pk16(kC6, -kC2), 0);
-    int x3 = dot2(P3, pk16(kC2, kC6), 0);
+    int x8 = dot2_v(P0, pk16(2048, 2048), c128);
+    int y0 = dot2_v(P0, pk16(2048, -2048), c128);
+    int x4 = dot2_0(P1, pk16(kC1, kC7));
+    int x5 = dot2_0(P1, pk16(kC7, -kC1));
+    int x6 = dot2_0(P2, pk16(kC5, kC3));
+    int x7 = dot2_0(P2, pk16(kC3, -kC5));
+    int x2 = dot2_0(P3, pk16(kC6, -kC2));
+    int x3 = dot2_0(P3, pk16(kC2, kC6));
     const int y1 = x4 + x6;
     x4 -= x6;
     x6 = x5 + x7;
@@ -1844,8 +1878,10 @@ __device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, i
     out[7] = (x7 - y1) >> 8;
 }
 __device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], int (&blk)[64]) {
+    int c128;
+    asm("v_mov_b32 %0, 0x80" : "=v"(c128));  // one VGPR holding the row pass's rounding term
 #pragma unroll
-    for (int r = 0; r < 8; r++) idct_row_dot2(dw, r, blk + 8 * r);
+    for (int r = 0; r < 8; r++) idct_row_dot2(dw, r, blk + 8 * r, c128);
 #pragma unroll
     for (int c = 0; c < 8; c++) idct_col_fast(blk + c);
 }
@@ -2086,6 +2122,71 @@ __device__ __forceinline__ void row_rgb_packed(const uint4& Yq, const uint32_t (
     w[5] = __builtin_amdgcn_perm(B[3], RG[3], 0x05030204u);                                            // b6 r7 g7 b7
 }
 
+// The 4:2:0 tail step: 4 pixels of two rows that share their two chroma samples (both chroma
+// planes subsampled 2x2).  A 4:2:0 tile of 10 MCUs has 160 8-pixel row-pair groups, two and a half
+// lane-steps: the last half step is done as 64 4-pixel halves, so no lane idles (k_idct_color).
+__device__ __forceinline__ void rgb4_packed(const uint2& Yq, const uint32_t (&TR)[2], const uint32_t (&TG)[2],
+                                            const uint32_t (&TB)[2], uint32_t (&w)[3]) {
+    const uint32_t Y[2] = {Yq.x, Yq.y};
+    uint32_t RG[2], B[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const uint32_t r = pk_add_sat_u8(Y[u], TR[u]), g = pk_add_sat_u8(Y[u], TG[u]);
+        B[u] = pk_add_sat_u8(Y[u], TB[u]);
+        RG[u] = __builtin_amdgcn_perm(g, r, 0x05010400u);
+    }
+    w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x02040100u);                                            // r0 g0 b0 r1
+    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0503u), 0x05040100u);  // g1 b1 r2 g2
+    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x05030204u);                                            // b2 r3 g3 b3
+}
+__device__ __forceinline__ void fix_g4_exact(const uint2& Yq, const int (&cb)[2], const int (&cr)[2], uint32_t exmask,
+                                             uint32_t (&w)[3]) {
+    const uint32_t Y[2] = {Yq.x, Yq.y};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int u = j >> 1;
+        if ((exmask >> u) & 1u) {
+            const int y = (j & 1) ? int32_t(Y[u]) >> 16 : int(int16_t(Y[u] & 0xFFFFu));
+            const int g = color_g_exact(y, cb[u], cr[u]);
+            const int byte = 3 * j + 1;
+            w[byte >> 2] = (w[byte >> 2] & ~(0xFFu << (8 * (byte & 3)))) | (uint32_t(g) << (8 * (byte & 3)));
+        }
+    }
+}
+// n <= 4 pixels (12 bytes when n == 4) of a row
+__device__ __forceinline__ void store12(uint8_t* dst, const uint32_t (&w)[3], uint32_t n) {
+    if (n == 4 && (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+        auto d1 = gptr(reinterpret_cast<uint32_t*>(dst));
+        d1[0] = w[0];
+        d1[1] = w[1];
+        d1[2] = w[2];
+    } else {
+        auto d = gptr(dst);
+#pragma unroll
+        for (int k = 0; k < 12; k++)
+            if (uint32_t(k) < 3 * n) d[k] = uint8_t(w[k / 4] >> (8 * (k % 4)));
+    }
+}
+__device__ __forceinline__ void colour4x2(const int16_t* s_pl, uint32_t yoff, uint32_t ypitch, uint32_t cboff,
+                                          uint32_t croff, uint32_t (&w0)[3], uint32_t (&w1)[3]) {
+    const uint32_t cbw = *reinterpret_cast<const uint32_t*>(s_pl + cboff);
+    const uint32_t crw = *reinterpret_cast<const uint32_t*>(s_pl + croff);
+    const int cb[2] = {int(int16_t(cbw & 0xFFFFu)), int32_t(cbw) >> 16};
+    const int cr[2] = {int(int16_t(crw & 0xFFFFu)), int32_t(crw) >> 16};
+    const ChromaTerms t0 = chroma_terms(cb[0], cr[0]), t1 = chroma_terms(cb[1], cr[1]);
+    const uint32_t TR[2] = {pair16(t0.r, t0.r), pair16(t1.r, t1.r)};
+    const uint32_t TG[2] = {pair16(t0.g, t0.g), pair16(t1.g, t1.g)};
+    const uint32_t TB[2] = {pair16(t0.b, t0.b), pair16(t1.b, t1.b)};
+    const uint32_t ex = (t0.exact ? 1u : 0u) | (t1.exact ? 2u : 0u);
+    const uint2 Y0 = *reinterpret_cast<const uint2*>(s_pl + yoff), Y1 = *reinterpret_cast<const uint2*>(s_pl + yoff + ypitch);
+    rgb4_packed(Y0, TR, TG, TB, w0);
+    rgb4_packed(Y1, TR, TG, TB, w1);
+    if (__any(ex != 0u)) {
+        fix_g4_exact(Y0, cb, cr, ex, w0);
+        fix_g4_exact(Y1, cb, cr, ex, w1);
+    }
+}
+
 // One wave per tile of tile_mcus x tile_mrows MCUs (host-chosen, <= 64 blocks):
 //  1. lane j owns block j: its LDS row (pitch 65 words) is filled with the block's DC and AC
 //     entries, dequantised in zig-zag order (parser.cpp:111,130) and placed at natural positions
@@ -2271,12 +2372,25 @@ __device__ __forceinline__ void stage_quant(const BatchDev& b, const ImgDesc& im
     }
 }
 
+// One zero quad materialised once (the compiler would re-create it with four v_mov per store) and
+// the lane known to be < kIdctThreads (only the last store is predicated).
 __device__ __forceinline__ void zero_staging(uint32_t* s_buf, uint32_t lane) {
+#if JD_ZERO_ASM == 1
+    __builtin_assume(lane < kIdctThreads);
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const uint4 zq = make_uint4(z, z, z, z);
+#else
+#if JD_ZERO_ASM == 2
+    __builtin_assume(lane < kIdctThreads);
+#endif
+    const uint4 zq = make_uint4(0, 0, 0, 0);
+#endif
     uint4* z4 = reinterpret_cast<uint4*>(s_buf);
 #pragma unroll
     for (uint32_t k = 0; k < (kIdctBufWords / 4 + kIdctThreads - 1) / kIdctThreads; k++) {
         const uint32_t i = lane + k * kIdctThreads;
-        if (i < kIdctBufWords / 4) z4[i] = make_uint4(0, 0, 0, 0);
+        if (i < kIdctBufWords / 4) z4[i] = zq;
     }
 }
 
@@ -2379,11 +2493,11 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
                            size_t(((r0 + mr) * vc + tyb) * 8) * (im.mcux * hc * 8) + ((m0 + mi) * hc + txb) * 8;
 #pragma unroll
             for (int r = 0; r < 8; r++) {
-                uint4 q;
-                q.x = (uint32_t(blk[8 * r + 0]) & 0xFFFFu) | (uint32_t(blk[8 * r + 1]) << 16);
-                q.y = (uint32_t(blk[8 * r + 2]) & 0xFFFFu) | (uint32_t(blk[8 * r + 3]) << 16);
-                q.z = (uint32_t(blk[8 * r + 4]) & 0xFFFFu) | (uint32_t(blk[8 * r + 5]) << 16);
-                q.w = (uint32_t(blk[8 * r + 6]) & 0xFFFFu) | (uint32_t(blk[8 * r + 7]) << 16);
+                uint4 q;  // one v_perm per int16 pair
+                q.x = pair16(blk[8 * r + 0], blk[8 * r + 1]);
+                q.y = pair16(blk[8 * r + 2], blk[8 * r + 3]);
+                q.z = pair16(blk[8 * r + 4], blk[8 * r + 5]);
+                q.w = pair16(blk[8 * r + 6], blk[8 * r + 7]);
                 *gptr(reinterpret_cast<u32x4*>(dst + size_t(r) * (im.mcux * hc * 8))) = u32x4{q.x, q.y, q.z, q.w};
             }
         }
@@ -2414,11 +2528,18 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         int16_t* dst = s_pl + base + ((mr * TM_::v(im, comp) + tyb) * 8) * pitch + (mi * hc + txb) * 8;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            uint4 q;
+            uint4 q;  // one v_perm per int16 pair
+#if JD_PACK_PERM
+            q.x = pair16(blk[8 * r + 0], blk[8 * r + 1]);
+            q.y = pair16(blk[8 * r + 2], blk[8 * r + 3]);
+            q.z = pair16(blk[8 * r + 4], blk[8 * r + 5]);
+            q.w = pair16(blk[8 * r + 6], blk[8 * r + 7]);
+#else
             q.x = (uint32_t(blk[8 * r + 0]) & 0xFFFFu) | (uint32_t(blk[8 * r + 1]) << 16);
             q.y = (uint32_t(blk[8 * r + 2]) & 0xFFFFu) | (uint32_t(blk[8 * r + 3]) << 16);
             q.z = (uint32_t(blk[8 * r + 4]) & 0xFFFFu) | (uint32_t(blk[8 * r + 5]) << 16);
             q.w = (uint32_t(blk[8 * r + 6]) & 0xFFFFu) | (uint32_t(blk[8 * r + 7]) << 16);
+#endif
             *reinterpret_cast<uint4*>(dst + r * pitch) = q;
         }
     }
@@ -2442,7 +2563,13 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
 #if JD_ABL & 1
     if (lane < 1000) return true;
 #endif
-    for (; gy < ngy; gy += step_y + (gc + step_c >= gpr ? 1u : 0u), gc = gc + step_c >= gpr ? gc + step_c - gpr : gc + step_c) {
+    // 4:2:0 (row pairs, chroma subsampled 2x horizontally): when the last lane-step would be at most
+    // half full, it is done as 4-pixel halves of the remaining groups (colour4x2) instead
+    const uint32_t ngroups = gpr * ngy, nfull = ngroups / kIdctThreads, nrem = ngroups - nfull * kIdctThreads;
+    const bool halves = JD_HALVES && pair && cmode == 1u && nrem != 0u && 2u * nrem <= kIdctThreads;  // wave-uniform
+    const uint32_t nsteps = halves ? nfull : ~0u;
+    for (uint32_t st = 0; gy < ngy && st < nsteps;
+         st++, gy += step_y + (gc + step_c >= gpr ? 1u : 0u), gc = gc + step_c >= gpr ? gc + step_c - gpr : gc + step_c) {
         const uint32_t py = gy * rows, gx = gc << 3;
         const uint32_t y = y_tile + py, x = x_tile + gx;
         if (y >= H || x >= W) continue;
@@ -2503,6 +2630,19 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         {
             store24(out + (size_t(y) * W + x) * 3, w0, min(8u, W - x));
             if (pair && y + 1 < H) store24(out + (size_t(y + 1) * W + x) * 3, w1, min(8u, W - x));
+        }
+    }
+    if (halves && lane < 2u * nrem) {
+        const uint32_t g = nfull * kIdctThreads + (lane >> 1);
+        const uint32_t hy = div_small(g, magic16(gpr)), hc = g - hy * gpr;
+        const uint32_t py = hy * 2u, gx = (hc << 3) + ((lane & 1u) << 2);
+        const uint32_t y = y_tile + py, x = x_tile + gx;
+        if (y < H && x < W) {
+            uint32_t w0[3], w1[3];
+            colour4x2(s_pl, pbase[0] + py * ppitch[0] + gx, ppitch[0], pbase[1] + (py >> 1) * ppitch[1] + (gx >> 1),
+                      pbase[2] + (py >> 1) * ppitch[2] + (gx >> 1), w0, w1);
+            store12(out + (size_t(y) * W + x) * 3, w0, min(4u, W - x));
+            if (y + 1 < H) store12(out + (size_t(y + 1) * W + x) * 3, w1, min(4u, W - x));
         }
     }
     return true;

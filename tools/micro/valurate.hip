@@ -37,7 +37,17 @@
     X(28, "v_sat_pk_u8_i16 %0, %0")                                              \
     X(29, "v_xad_u32 %0, %0, %1, %2")                                            \
     X(30, "v_cmp_gt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc")            \
-    X(31, "v_min3_i32 %0, %0, %1, %2")
+    X(31, "v_min3_i32 %0, %0, %1, %2")                                          \
+    X(32, "v_dot2_i32_i16 %0, %1, %2, %0")                                       \
+    X(33, "v_mov_b32 %0, %1\n v_dot2c_i32_i16 %0, %1, %2")                       \
+    X(34, "v_ashrrev_i32 %0, %1, %0")                                            \
+    X(35, "v_mul_i32_i24 %0, %0, %1")                                            \
+    X(36, "v_mad_i32_i24 %0, %0, %1, %2")                                        \
+    X(37, "v_sub_u32 %0, %0, %1")                                                \
+    X(38, "v_mul_hi_u32 %0, %0, %1")                                             \
+    X(39, "v_floor_f32 %0, %0")                                                  \
+    X(40, "v_mul_f32 %0, %0, %1")                                                \
+    X(41, "v_mov_b32 %0, %1")
 
 #define KCASE(N, S) else if (KIND == N) { _Pragma("unroll") for (int j = 0; j < 8; j++) asm volatile(S : "+v"(x[j]) : "v"(c), "v"(e) : "vcc"); }
 
