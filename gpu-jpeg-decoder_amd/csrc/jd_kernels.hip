@@ -6,14 +6,15 @@
 //   k_index        one wave per image: chunk offsets in the un-stuffed stream, restart-interval
 //                  (segment) boundaries, RSTn order / count checks
 //   k_compact      16 KiB per workgroup: drops the stuffed 00 after every FF (byte compaction)
+//   k_pieceplan    one workgroup: the piece size for the batch (whole rounds of resident lanes)
 //   k_subplan      one wave per image: pieces (<= piece_bits un-stuffed bits) of every interval
 //   k_piece        one lane per piece: a speculative, self-synchronising Huffman walk (warm-up
 //                  from before the piece, then block records + sparse AC entries into the piece's
 //                  own region, checkpoints); k_redo re-walks the pieces whose speculative start
 //                  was wrong (joining the speculative walk at a checkpoint); k_chain / k_chain_fix
 //                  verify the chain of pieces and prefix-sum each piece's first MCU
-//   k_gather       one wave per piece: block records -> BlockInfo (DC difference, entry range) at
-//                  the blocks' global positions
+//   k_gather       64 pieces per wave (one row of 16 lanes per piece): block records -> BlockInfo
+//                  (DC difference, entry range) at the blocks' global positions
 //   k_dc_sum / k_dc_scan   DC predictors at every IDCT tile's first block
 //   k_idct_color   one wave per tile (a run of <= 64 blocks of one MCU row): DC prediction,
 //                  dequantisation, integer IDCT in registers, replicate chroma upsampling and
