@@ -93,6 +93,7 @@ struct TableSet {
     uint8_t dc_slot[4];
     uint8_t ac_slot[4];
     int32_t nslots;
+    int32_t set_lut0;  // first of this set's nslots LUTs in BatchDev::set_luts (k_redo reads them there)
 };
 
 // Per image of a batch (device array, one entry per decodable image).
@@ -239,6 +240,7 @@ struct BatchDev {
     uint32_t nimg;
     const HuffLut* luts;
     const TableSet* tablesets;
+    const HuffLut* set_luts;  // every table set's LUTs, contiguous per set (global-memory lookups)
     const uint16_t* qtabs;        // 64 x uint16 per quant table, zig-zag order
     // segments (restart intervals)
     const uint32_t* seg_img;      // image of each segment

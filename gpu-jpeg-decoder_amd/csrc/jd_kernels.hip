@@ -32,6 +32,18 @@
 
 namespace jd {
 
+// Wave priority of the latency-bound kernels.  Two batches are in flight: batch k's
+// re-walks (k_redo: a few lanes with long serial walks) and short kernels share the CUs with batch
+// k+1's k_piece or batch k-1's k_idct_color, whose 16-20 waves per CU would otherwise take most
+// issue slots and stretch k_redo from 0.4 to 2.5 ms on the critical path.  s_setprio raises the
+// issue priority of their waves over the two big kernels' waves on the same SIMD.
+#ifndef JD_PRIO
+#define JD_PRIO 2  // 0: off, 1: k_redo / k_chain / k_chain_fix, 2: every kernel but k_piece / k_idct_color
+#endif
+#define JD_PRIO_CRIT() do { if (JD_PRIO >= 1) __builtin_amdgcn_s_setprio(3); } while (0)
+#define JD_PRIO_SHORT() do { if (JD_PRIO >= 2) __builtin_amdgcn_s_setprio(2); } while (0)
+
+
 // zig-zag index -> natural (row-major) position: inverse of src/idct.cpp:8-16.
 // constexpr: fully unrolled loops index it at compile time (register naming, no lookups)
 constexpr uint8_t kNatOfZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
@@ -128,6 +140,7 @@ __device__ __forceinline__ uint32_t scan_masks(uint32_t x, uint32_t& ff, uint32_
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
+    JD_PRIO_SHORT();
     __shared__ uint32_t s_wsum[2][kScanThreads / 64];
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t c = blockIdx.x;
@@ -247,6 +260,7 @@ __device__ __forceinline__ uint32_t fill_before(uintptr_t file, uint32_t lo, uin
 }
 
 __global__ __launch_bounds__(64) void k_index(BatchDev b) {
+    JD_PRIO_SHORT();
     const uint32_t ii = blockIdx.x;
     const ImgDesc& im = b.imgs[ii];
     const uintptr_t file = uintptr_t(im.jpeg);
@@ -349,6 +363,7 @@ __device__ __forceinline__ void store_run(uint32_t* s_out, uint32_t off, const u
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
+    JD_PRIO_SHORT();
     __shared__ uint32_t s_out[kScanChunk / 4 + 4];
     __shared__ uint32_t s_wsum[kScanThreads / 64];
     const ImgDesc& im = b.imgs[blockIdx.y];
@@ -590,6 +605,7 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
 // k_subplan.  Counts use a float reciprocal: an estimate (k_subplan divides exactly).
 constexpr int kPlanCands = 16;
 __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
+    JD_PRIO_SHORT();
     __shared__ unsigned long long s_cnt[kPlanCands];
     const uint32_t t = threadIdx.x;
     if (t < kPlanCands) s_cnt[t] = 0;
@@ -633,6 +649,7 @@ __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
 // seg_ent + j * region_words(plen).  The image's spare words after them (img_pool) are handed
 // out to re-walks (k_redo, k_chain_fix).
 __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
+    JD_PRIO_SHORT();
     const ImgDesc& im = b.imgs[blockIdx.x];
     const int lane = threadIdx.x;
     const uint32_t piece_bits = b.piece_plan ? uint32_t(b.counters[3] & 0xFFFFFFFFull) : b.piece_bits;
@@ -705,6 +722,12 @@ constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte alig
 #ifndef JD_EXTRA_LDS
 #define JD_EXTRA_LDS 0  // experiment builds: extra dynamic LDS per piece workgroup (lowers occupancy)
 #endif
+// k_redo: 64-lane workgroups with the tables in global memory, so that they fit beside the other
+// batch's k_piece / k_idct_color waves instead of waiting for a whole CU's LDS.
+constexpr int kRedoThreads = 64;
+static_assert(kPieceThreads % kRedoThreads == 0, "a redo workgroup lies inside one piece workgroup");
+constexpr size_t kRedoLds = size_t(kRedoThreads) * (row_words(kWin) + kRingWords) * 4;
+static_assert((kRedoThreads * row_words(kWin) * 4) % 16 == 0, "redo rings must start 16-byte aligned");
 size_t piece_lds_bytes(uint32_t max_slots) {
     return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * (row_words(kWin) + kRingWords) * 4 + JD_EXTRA_LDS;
 }
@@ -780,6 +803,27 @@ __device__ __forceinline__ u32x2 lut_fast(uint32_t tab, uint32_t peek) {
     return *reinterpret_cast<lds_u64*>(size_t((idx << 3) + tab));
 }
 
+// Where a walk's tables live: LDS (k_piece, k_chain_fix: tab is an LDS byte address) or global
+// memory (k_redo: tab is the 64-bit address of the table in BatchDev::set_luts, so its workgroups
+// need LDS only for the lanes' rows and rings).
+template <bool GL>
+struct TabSpace {
+    typedef uint32_t T;
+    static __device__ __forceinline__ T base(const uint32_t* p) { return lds_addr(p); }
+    static __device__ __forceinline__ u32x2 fast(T tab, uint32_t peek) { return lut_fast(tab, peek); }
+    static __device__ __forceinline__ const uint32_t* at(T tab) { return lut_at(tab); }
+};
+template <>
+struct TabSpace<true> {
+    typedef uint64_t T;
+    static __device__ __forceinline__ T base(const uint32_t* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)); }
+    static __device__ __forceinline__ u32x2 fast(T tab, uint32_t peek) {
+        const uint64_t idx = peek >> (32 - kLutBits);
+        return *reinterpret_cast<const __attribute__((address_space(1))) u32x2*>((idx << 3) + tab);
+    }
+    static __device__ __forceinline__ const uint32_t* at(T tab) { return reinterpret_cast<const uint32_t*>(tab); }
+};
+
 // Block record in a piece's region: escape flag << 23 | AC-entry slot count (<= 126) << 16 | the
 // 16-bit DC difference (a DC size is <= 15 bits, jd_internal.hpp lut_entry).
 __device__ __forceinline__ uint32_t block_rec(uint32_t cnt, int dc, uint32_t esc) {
@@ -829,7 +873,7 @@ __device__ __forceinline__ void st_ent(uint4* p, const uint4& v) {
 #define JD_PSTAT 0  // diagnostic builds: k_piece walk statistics summed into BatchDev::stamps[0..15]
 #endif
 
-template <int KIND>
+template <int KIND, bool GL = false>
 __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
                                            uint32_t* row, uint32_t* ring, bool active_in, PWalk& W, CpRec* cp,
                                            uint32_t cp_bits, const uint32_t (&cpb)[kCpMax]) {
@@ -844,12 +888,15 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
     const uint32_t sbits = S.bits;
     const uint32_t bpm3 = 3u * S.bpm;
-    const uint32_t lbase = lds_addr(s_lutw);
-    const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
+    typedef TabSpace<GL> TS;
+    typedef typename TS::T TabT;
+    const TabT lbase = TS::base(s_lutw);
+    const TabT tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
     uint32_t* const reg = W.reg;
     uint32_t* const rec_top = W.reg + (W.rw - 1u);  // block record k at rec_top[-k]
     uint16_t* const ring16 = reinterpret_cast<uint16_t*>(ring);
-    uint32_t z = 0, b3 = 0, tab = tab_dc0;
+    uint32_t z = 0, b3 = 0;
+    TabT tab = tab_dc0;
     bool warm = KIND == kSpec && W.warm_to != W.start;
     bool active = active_in;
     uint32_t m_start = warm ? kNoPiece : W.start, m_end = W.start;
@@ -911,7 +958,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         while (active && R.rp <= kWin / 4) {
             it++;
             const uint32_t peek = R.peek();
-            const u32x2 E = lut_fast(tab, peek);
+            const u32x2 E = TS::fast(tab, peek);
             const uint32_t lo = E.x, hi = E.y;
             if (JD_PSTAT) {
                 st_rare += (lo & kLoRare) ? 1u : 0u;
@@ -941,7 +988,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             zn = pr ? zn2 : zn;
             if (lo & kLoRare) {  // codes longer than the index, escaped magnitudes, corrupt codes
                 uint32_t e = hi;
-                if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
+                if ((e & 31u) == 0) e = huff_slow(TS::at(tab), peek);
                 const int val = huff_value(peek, e);
                 // EOB / ZRL / run-size (parser.cpp:114-134)
                 zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
@@ -1148,6 +1195,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
 // spare region of the image when one is left (joining the speculative walk at a checkpoint),
 // else over its own region (no join: that overwrites what the checkpoints describe).
 // Returns the piece's new end.
+template <bool GL>
 __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceGeo& P, uint32_t s, uint32_t u,
                                uint32_t expect, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp, uint32_t* row,
                                uint32_t* ring, bool need) {
@@ -1171,7 +1219,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
     W.stop_at = piece_stop(P);
     W.reg = S.eimg + base;
     W.rw = P.rw;
-    walk_piece<kRedo>(S, s_lutw, dcp, acp, row, ring, need, W, cp, 0xFFFFFFFFu, cpb);
+    walk_piece<kRedo, GL>(S, s_lutw, dcp, acp, row, ring, need, W, cp, 0xFFFFFFFFu, cpb);
     if (!need) return 0;
     uint32_t end = W.m_end, mcus = W.mcus, ents = W.ents, emcu = W.emcu;
     if (W.join) {
@@ -1196,11 +1244,11 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
 // predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images).
 // Starting from that end is exact when the predecessor is right; a predecessor re-walked in this
 // round keeps its end when it joins its speculative walk, and otherwise k_chain notices.
-__global__ __launch_bounds__(kPieceThreads) void k_redo(BatchDev b) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    const uint32_t u = blockIdx.x * kPieceThreads + threadIdx.x;
+__global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
+    JD_PRIO_CRIT();
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];  // the lanes' rows and rings only
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
+    const uint32_t u = blockIdx.x * kRedoThreads + threadIdx.x;
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
     uint32_t expect = 0;
     bool need = false;
@@ -1209,9 +1257,8 @@ __global__ __launch_bounds__(kPieceThreads) void k_redo(BatchDev b) {
         need = b.piece_bit[u] != expect;
     }
     if (!__syncthreads_or(need)) return;  // workgroup-uniform
-    const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
-    stage_luts(b, ts, s_lut, kPieceThreads);
-    __syncthreads();
+    // the piece workgroup (kPieceThreads lanes, one table set) this one is part of
+    const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
     SegInfo S;
     PieceGeo P{0u, 1u, 0u, 0u, 0u};
     if (need) {
@@ -1222,9 +1269,9 @@ __global__ __launch_bounds__(kPieceThreads) void k_redo(BatchDev b) {
     }
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    redo_piece(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp,
-               s_rows + threadIdx.x * row_words(kWin), s_rows + kPieceThreads * row_words(kWin) + threadIdx.x * kRingWords,
-               need);
+    redo_piece<true>(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
+                     s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
+                     need);
 }
 
 // The MCUs piece j contributes, given its first MCU m0 (the interval has nmcu_seg): a piece before
@@ -1247,6 +1294,7 @@ __device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_
 // some start still disagrees after k_redo (a double failure, rare) is flagged for k_chain_fix,
 // which walks it serially with re-walks.
 __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
+    JD_PRIO_CRIT();
     const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     if (s >= b.nseg) return;  // wave-uniform
@@ -1307,6 +1355,7 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
 // order, re-walk every piece whose start disagrees with its predecessor's end (the workgroup
 // stages its tables only when some lane needs them), and take the counts serially.
 __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
+    JD_PRIO_CRIT();
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
@@ -1346,7 +1395,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
         uint32_t pend = b.piece_end[u];
         if (b.piece_bit[u] != expect) {  // the start had not synchronised: re-walk from the truth
             const PieceGeo P = piece_geo(b, S, s, u);
-            pend = redo_piece(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, row, ring, true);
+            pend = redo_piece<false>(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, row, ring, true);
         }
         const uint32_t pm = b.piece_nmcu[u], em = b.piece_emcu[u];
         const bool last = j + 1 == n || (final_seg && mcu_run + pm >= nmcu_seg);
@@ -1398,6 +1447,7 @@ __device__ __forceinline__ uint32_t gather_rows(BlockInfo* out, const uint32_t* 
     return run - ebase;
 }
 __global__ __launch_bounds__(256) void k_gather(BatchDev b) {
+    JD_PRIO_SHORT();
     __shared__ uint32_t s_ents;
     if (threadIdx.x == 0) s_ents = 0;
     __syncthreads();
@@ -1567,6 +1617,7 @@ __device__ __forceinline__ TileLane tile_lane(const BatchDev& b, const ImgDesc& 
 // (all of them when it has none) and whether it has one.
 constexpr uint32_t kDcTilesPerWave = 4;  // k_dc_sum: the tiles' BlockInfo loads are in flight together
 __global__ __launch_bounds__(256) void k_dc_sum(BatchDev b) {
+    JD_PRIO_SHORT();
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t nt = im.tiles_x * im.tiles_y, lane = threadIdx.x & 63u;
     const uint32_t tile0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kDcTilesPerWave;
@@ -1591,6 +1642,7 @@ __global__ __launch_bounds__(256) void k_dc_sum(BatchDev b) {
 // Wave per image: segmented exclusive scan over its tiles in raster order, in place: tile_dc
 // becomes the predictor of each component at the tile's first block.
 __global__ __launch_bounds__(64) void k_dc_scan(BatchDev b) {
+    JD_PRIO_SHORT();
     const ImgDesc& im = b.imgs[blockIdx.x];
     const uint32_t lane = threadIdx.x, nt = im.tiles_x * im.tiles_y;
     int c0 = 0, c1 = 0, c2 = 0;
@@ -2912,7 +2964,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             if (b.nsub) hipLaunchKernelGGL(k_piece, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
             break;
         case 5:
-            if (b.nsub) hipLaunchKernelGGL(k_redo, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            if (b.nsub) hipLaunchKernelGGL(k_redo, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
             break;
         case 6:
             if (!b.nseg) break;

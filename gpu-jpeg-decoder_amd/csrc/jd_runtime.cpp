@@ -699,8 +699,16 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         std::vector<uint8_t> blob;
         const size_t nseg = P.seg_img.size();
         const size_t nsub = P.nsub;
+        // every table set's LUTs once more, contiguous per set: k_redo looks them up in global
+        // memory (so its small workgroups need no LDS for tables)
+        std::vector<HuffLut> set_luts;
+        for (TableSet& t : P.tablesets) {
+            t.set_lut0 = int32_t(set_luts.size());
+            for (int k = 0; k < t.nslots; k++) set_luts.push_back(ctx->lut_host[size_t(t.lut[k])]);
+        }
         const size_t o_imgs = put(blob, P.imgs);
         const size_t o_ts = put(blob, P.tablesets);
+        const size_t o_setluts = put(blob, set_luts);
         const size_t o_q = put(blob, P.qtabs);
         const size_t o_segimg = put(blob, P.seg_img);
         const size_t o_wgts = put(blob, P.wg_tableset);
@@ -744,6 +752,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.nimg = nimg;
         b.luts = static_cast<const HuffLut*>(ctx->lut_dev.p);
         b.tablesets = reinterpret_cast<const TableSet*>(base + o_ts);
+        b.set_luts = reinterpret_cast<const HuffLut*>(base + o_setluts);
         b.qtabs = reinterpret_cast<const uint16_t*>(base + o_q);
         b.seg_img = reinterpret_cast<const uint32_t*>(base + o_segimg);
         b.seg_cstart = reinterpret_cast<uint32_t*>(base + o_cstart);
