@@ -1354,17 +1354,19 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
 // One lane per interval flagged by k_chain (workgroups grouped by table set): walk its pieces in
 // order, re-walk every piece whose start disagrees with its predecessor's end (the workgroup
 // stages its tables only when some lane needs them), and take the counts serially.
-__global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
+// 64-lane workgroups with the tables in global memory, as k_redo: almost every workgroup exits at
+// once, and with the 73 KB of LDS a piece workgroup takes, each of them had to wait for a CU's
+// LDS under the other batch's k_idct_color (1.1 ms instead of 0.02 in a kernel trace).
+__global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
     JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    const uint32_t li = blockIdx.x * kPieceThreads + threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];  // the lanes' rows and rings only
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
+    const uint32_t li = blockIdx.x * kRedoThreads + threadIdx.x;
     uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
     if (s != kInvalidImage && !b.seg_fix[s]) s = kInvalidImage;
     const bool need = s != kInvalidImage;
     if (!__syncthreads_or(need)) return;  // workgroup-uniform: the common case
-    const TableSet& ts = b.tablesets[b.chain_wg_tableset[blockIdx.x]];
+    const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
     SegInfo S;
     uint32_t base = 0, n = 0;
     if (need) {
@@ -1374,13 +1376,12 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
     } else {
         seg_invalid(b, S);
     }
-    stage_luts(b, ts, s_lut, kPieceThreads);
-    __syncthreads();
     if (!need) return;
+    const uint32_t* const luts = reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0);
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
     uint32_t* const row = s_rows + threadIdx.x * row_words(kWin);
-    uint32_t* const ring = s_rows + kPieceThreads * row_words(kWin) + threadIdx.x * kRingWords;
+    uint32_t* const ring = s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords;
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const bool final_seg = seg_is_final(b, s);  // trailing bytes after its last MCU are ignored
     bool bad = false, done = false;
@@ -1395,7 +1396,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_chain_fix(BatchDev b) {
         uint32_t pend = b.piece_end[u];
         if (b.piece_bit[u] != expect) {  // the start had not synchronised: re-walk from the truth
             const PieceGeo P = piece_geo(b, S, s, u);
-            pend = redo_piece<false>(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, row, ring, true);
+            pend = redo_piece<true>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, true);
         }
         const uint32_t pm = b.piece_nmcu[u], em = b.piece_emcu[u];
         const bool last = j + 1 == n || (final_seg && mcu_run + pm >= nmcu_seg);
@@ -2969,7 +2970,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
         case 6:
             if (!b.nseg) break;
             hipLaunchKernelGGL(k_chain, dim3((b.nseg + 3) / 4), dim3(256), 0, s, b);
-            if (b.nchain) hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            if (b.nchain) hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
             break;
         case 7:
             if (b.nsub) hipLaunchKernelGGL(k_gather, dim3((b.nsub + 255) / 256), dim3(256), 0, s, b);  // 64 pieces per wave
