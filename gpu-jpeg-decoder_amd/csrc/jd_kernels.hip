@@ -38,7 +38,8 @@ namespace jd {
 // issue slots and stretch k_redo from 0.4 to 2.5 ms on the critical path.  s_setprio raises the
 // issue priority of their waves over the two big kernels' waves on the same SIMD.
 #ifndef JD_PRIO
-#define JD_PRIO 2  // 0: off, 1: k_redo / k_chain / k_chain_fix, 2: every kernel but k_piece / k_idct_color
+#define JD_PRIO 1  // 0: off, 1: k_redo / k_chain / k_chain_fix, 2: every kernel but k_piece / k_idct_color
+                   // (2 made k_dc_sum 40 % slower)
 #endif
 #define JD_PRIO_CRIT() do { if (JD_PRIO >= 1) __builtin_amdgcn_s_setprio(3); } while (0)
 #define JD_PRIO_SHORT() do { if (JD_PRIO >= 2) __builtin_amdgcn_s_setprio(2); } while (0)
@@ -1963,18 +1964,23 @@ struct ChromaTerms {
 // R and B as one 24-bit multiply-add and a shift each: floor(1402 cr / 1000) + 128 =
 // (91881 cr + 128 * 2^16) >> 16 and floor(1772 cb / 1000) + 128 = (58065 cb + 128 * 2^15 + 32) >> 15
 // for every cr, cb in [-256, 255] (magic constants found by exhaustive search; the products stay
-// below 2^31).  G's quotient from float(n) / 587000 (|n| < 2^28, error < 5e-5), its remainder exact
-// in integers.  Equal to the integer definitions above for every (cb, cr) in [-256, 255]^2
+// below 2^31).  G's quotient by a multiply-high on n offset to [0, 2^29) (below), its remainder
+// exact in integers.  Equal to the integer definitions above for every (cb, cr) in [-256, 255]^2
 // (tests/test_oracle.py::test_chroma_terms_exhaustive, and the GPU's all-2^27 test_color_exhaustive).
 __device__ __forceinline__ ChromaTerms chroma_terms(int cb, int cr) {
     ChromaTerms t;
     t.r = (__mul24(cr, 91881) + (128 << 16)) >> 16;
     t.b = (__mul24(cb, 58065) + (128 << 15) + 32) >> 15;
-    const int n = __mul24(cb, 202008) + __mul24(cr, 419198);
-    const int q = int(floorf(float(n) * (1.0f / 587000.0f)));
-    const int rem = n - __mul24(q, 587000);
-    t.exact = n != 0 && (rem < 64 || rem > 587000 - 64);
-    t.g = n == 0 ? 128 : 127 - q;
+    // n' = n + 271 * 587000 is in [0, 2^29): floor(n' / 587000) = mulhi(n', M) >> 19 with
+    // M = ceil(2^51 / 587000) for every n' of the domain (checked exhaustively), two integer
+    // instructions instead of the float convert / multiply / floor / convert
+    constexpr int kOff = 271 * 587000;
+    const uint32_t np = uint32_t(__mul24(cb, 202008) + __mul24(cr, 419198) + kOff);
+    const uint32_t qp = __umulhi(np, 3836115526u) >> 19;  // q + 271
+    const int rem = int(np) - __mul24(int(qp), 587000);
+    const bool nz = np != uint32_t(kOff);
+    t.exact = nz && (rem < 64 || rem > 587000 - 64);
+    t.g = nz ? 127 + 271 - int(qp) : 128;
     return t;
 }
 __device__ __forceinline__ uint32_t clamp_u8(int v) { return uint32_t(min(max(v, 0), 255)); }  // v_med3_i32

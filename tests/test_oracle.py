@@ -151,8 +151,9 @@ def test_idct_shortcuts_equal_branch_free():
 def test_chroma_terms_exhaustive():
     """k_idct_color's chroma terms (jd_kernels.hip chroma_terms): R and B as one 24-bit
     multiply-add and a shift, (91881 cr + 128 * 2^16) >> 16 and (58065 cb + 128 * 2^15 + 32) >> 15;
-    G's quotient as floor(float(n) * (1 / 587000.0f)) with an exact integer remainder.  Equal to the
-    integer definitions for every (cb, cr) in [-256, 255]^2 (IEEE float32 emulated in numpy)."""
+    G's quotient as a multiply-high of n + 271 * 587000 by ceil(2^51 / 587000), shifted right 19
+    (and, as before, floor(float(n) * (1 / 587000.0f))), with an exact integer remainder.  Equal to
+    the integer definitions for every (cb, cr) in [-256, 255]^2 (IEEE float32 emulated in numpy)."""
     cb, cr = np.meshgrid(np.arange(-256, 256, dtype=np.int64), np.arange(-256, 256, dtype=np.int64), indexing="ij")
     cb, cr = cb.ravel(), cr.ravel()
     f32 = np.float32
@@ -167,6 +168,10 @@ def test_chroma_terms_exhaustive():
     q_f = np.floor(n.astype(f32) * f32(1.0 / 587000.0)).astype(np.int64)
     rem_f = n - q_f * 587000
     assert (tr_i == tr_m).all() and (tb_i == tb_m).all() and (q_i == q_f).all()
+    npr = n + 271 * 587000
+    assert npr.min() >= 0 and npr.max() < 2**29
+    q_h = ((npr * 3836115526) >> 51) - 271  # __umulhi(n', M) >> 19
+    assert 3836115526 == -(-(2**51) // 587000) < 2**32 and (q_h == q_i).all()
     ex_i = (n != 0) & ((rem_i < 64) | (rem_i > 587000 - 64))
     ex_f = (n != 0) & ((rem_f < 64) | (rem_f > 587000 - 64))
     assert (ex_i == ex_f).all()
