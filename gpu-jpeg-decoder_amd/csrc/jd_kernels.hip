@@ -729,9 +729,14 @@ constexpr int kRedoThreads = 64;
 static_assert(kPieceThreads % kRedoThreads == 0, "a redo workgroup lies inside one piece workgroup");
 constexpr size_t kRedoLds = size_t(kRedoThreads) * (row_words(kWin) + kRingWords) * 4;
 static_assert((kRedoThreads * row_words(kWin) * 4) % 16 == 0, "redo rings must start 16-byte aligned");
-size_t piece_lds_bytes(uint32_t max_slots) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(kPieceThreads) * (row_words(kWin) + kRingWords) * 4 + JD_EXTRA_LDS;
+size_t piece_lds_bytes(uint32_t max_slots, int nt) {
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(nt) * (row_words(kWin) + kRingWords) * 4 + JD_EXTRA_LDS;
 }
+// Batches with fewer piece lanes than this run k_piece in 64-lane workgroups.
+#ifndef JD_SMALL_PIECE_LANES
+#define JD_SMALL_PIECE_LANES 16384
+#endif
+constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
 static_assert((kPieceThreads * row_words(kWin) * 4) % 16 == 0, "rings must start 16-byte aligned");
 
 // Stream reader over a lane's LDS row of big-endian words.  A and B are the words under the read
@@ -1144,15 +1149,19 @@ __device__ __forceinline__ uint32_t piece_stop(const PieceGeo& P) {
 
 // Lane per piece slot: the speculative walk (warm-up, then the writing walk into the piece's own
 // region).  Piece 0 of an interval starts at bit 0 in the true state.
-__global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
+// NT = kPieceThreads, or 64 for batches with few pieces (one small image: a few 512-lane
+// workgroups would leave all but a few CUs idle; 64-lane ones spread the same lanes over 8x as
+// many CUs, each staging its own table copy).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    const TableSet& ts = b.tablesets[b.wg_tableset[blockIdx.x]];
-    stage_luts(b, ts, s_lut, kPieceThreads);
+    const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * NT) / kPieceThreads]];
+    stage_luts(b, ts, s_lut, NT);
     __syncthreads();
 
-    const uint32_t u = blockIdx.x * kPieceThreads + threadIdx.x;
+    const uint32_t u = blockIdx.x * NT + threadIdx.x;
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
     const bool valid = s != kInvalidImage;
     SegInfo S;
@@ -1178,7 +1187,7 @@ __global__ __launch_bounds__(kPieceThreads) void k_piece(BatchDev b) {
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     const uint32_t none[kCpMax] = {};
     walk_piece<kSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWin),
-                      s_rows + kPieceThreads * row_words(kWin) + threadIdx.x * kRingWords, valid, W, cp,
+                      s_rows + NT * row_words(kWin) + threadIdx.x * kRingWords, valid, W, cp,
                       max(1u, P.plen / kCpMax), none);
     if (!valid) return;
     b.piece_bit[u] = (P.j == 0) ? 0u : W.m_start;
@@ -2913,7 +2922,7 @@ __global__ void k_test_color(const int32_t* ycc, uint8_t* rgb, int n) {
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots); }
+size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots, kPieceThreads); }
 
 uint32_t piece_lanes_resident(size_t lds) {
     static size_t cached_lds = 0;
@@ -2923,8 +2932,8 @@ uint32_t piece_lanes_resident(size_t lds) {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return 0;
     if (lds > 65536)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_piece), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_piece, kPieceThreads, lds) != hipSuccess || nb <= 0) return 0;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_piece<kPieceThreads>), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_piece<kPieceThreads>, kPieceThreads, lds) != hipSuccess || nb <= 0) return 0;
     cached_lds = lds;
     cached = uint32_t(nb) * uint32_t(cus) * uint32_t(kPieceThreads);
     return cached;
@@ -2934,8 +2943,7 @@ uint32_t piece_lanes_resident(size_t lds) {
 static hipError_t allow_lds(size_t lds) {
     static size_t allowed = 65536;
     if (lds <= allowed) return hipSuccess;
-    for (const void* f : {reinterpret_cast<const void*>(&k_piece), reinterpret_cast<const void*>(&k_redo),
-                          reinterpret_cast<const void*>(&k_chain_fix)}) {
+    for (const void* f : {reinterpret_cast<const void*>(&k_piece<kPieceThreads>), reinterpret_cast<const void*>(&k_piece<64>)}) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
@@ -2945,7 +2953,7 @@ static hipError_t allow_lds(size_t lds) {
 
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     if (!b.nimg) return hipSuccess;
-    const size_t lds = piece_lds_bytes(b.max_slots);
+    const size_t lds = piece_lds_bytes(b.max_slots, kPieceThreads);
     if (k == 4 || k == 5 || k == 6) {
         const hipError_t e = allow_lds(lds);
         if (e != hipSuccess) return e;
@@ -2968,7 +2976,10 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             break;
         }
         case 4:
-            if (b.nsub) hipLaunchKernelGGL(k_piece, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            if (b.nsub >= kSmallPieceLanes)
+                hipLaunchKernelGGL(k_piece<kPieceThreads>, dim3(b.nsub / kPieceThreads), dim3(kPieceThreads), lds, s, b);
+            else if (b.nsub)
+                hipLaunchKernelGGL(k_piece<64>, dim3(b.nsub / 64), dim3(64), piece_lds_bytes(b.max_slots, 64), s, b);
             break;
         case 5:
             if (b.nsub) hipLaunchKernelGGL(k_redo, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
