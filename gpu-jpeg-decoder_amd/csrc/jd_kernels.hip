@@ -1316,25 +1316,40 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     // The scan's last interval ends at EOI, and what follows its last MCU is ignored: the piece
     // whose MCUs reach the interval's count is the last one that matters, and the pieces after it
     // (decoding trailing bytes) are dropped.
+    // Four consecutive pieces per lane, 256 per wave-iteration: an interval without DRI can have
+    // a thousand pieces, and each iteration is a round of dependent global loads.
+    constexpr uint32_t kPer = 4, kStep = 64 * kPer;
     uint32_t jl = n - 1;
     if (final_seg) {
         uint32_t run = 0;
-        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
-            const uint32_t j = j0 + lane;
-            const uint32_t pm = j < n ? b.piece_nmcu[base + j] : 0u;
-            const uint32_t inc = run + uint32_t(wave_scan_dpp(int(pm)));
-            const uint64_t hit = __ballot(j < n && inc >= nmcu_seg);
+        for (uint32_t j0 = 0; j0 < n; j0 += kStep) {
+            const uint32_t jb = j0 + kPer * lane;
+            uint32_t c[kPer];
+#pragma unroll
+            for (uint32_t t = 0; t < kPer; t++) c[t] = jb + t < n ? b.piece_nmcu[base + jb + t] : 0u;
+#pragma unroll
+            for (uint32_t t = 1; t < kPer; t++) c[t] += c[t - 1];  // inclusive within the lane
+            const uint32_t before = run + uint32_t(wave_scan_dpp(int(c[kPer - 1]))) - c[kPer - 1];
+            uint32_t tf = kPer;  // the lane's first piece whose running count reaches the interval's
+#pragma unroll
+            for (int t = kPer - 1; t >= 0; t--)
+                if (jb + t < n && before + c[t] >= nmcu_seg) tf = uint32_t(t);
+            const uint64_t hit = __ballot(tf < kPer);
             if (hit) {  // wave-uniform
-                jl = j0 + uint32_t(__builtin_ctzll(hit));
+                const int L = __builtin_ctzll(hit);
+                jl = j0 + kPer * uint32_t(L) + uint32_t(__shfl(int(tf), L, 64));
                 break;
             }
-            run = __shfl(inc, 63, 64);
+            run = uint32_t(__shfl(int(before + c[kPer - 1]), 63, 64));
         }
     }
     bool need = false;
-    for (uint32_t j0 = 0; j0 <= jl; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        if (j <= jl) need |= b.piece_bit[base + j] != (j ? b.piece_end[base + j - 1] : 0u);
+    for (uint32_t j0 = 0; j0 <= jl; j0 += kStep) {
+#pragma unroll
+        for (uint32_t t = 0; t < kPer; t++) {
+            const uint32_t j = j0 + kPer * lane + t;
+            if (j <= jl) need |= b.piece_bit[base + j] != (j ? b.piece_end[base + j - 1] : 0u);
+        }
     }
     if (__any(need)) {  // wave-uniform
         if (lane == 0) b.seg_fix[s] = 1u;
@@ -1343,20 +1358,33 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     if (lane == 0) b.seg_fix[s] = 0u;
     uint32_t mcu_run = 0;
     bool bad = false;
-    for (uint32_t j0 = 0; j0 < n; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        const bool in = j <= jl;  // pieces past jl: no MCUs
-        const uint32_t pm = in ? b.piece_nmcu[base + j] : 0u;
-        const uint32_t pin = (in && j != jl) ? pm : 0u;
-        const uint32_t im = uint32_t(wave_scan_dpp(int(pin)));
-        const uint32_t m0 = mcu_run + im - pin;
-        uint32_t take = 0;
-        if (in) take = piece_take(pm, b.piece_emcu[base + j], m0, nmcu_seg, j == jl, final_seg, bad);
-        if (j < n) {
-            b.piece_mcu0[base + j] = min(m0, nmcu_seg);
-            b.piece_nmcu[base + j] = (m0 <= nmcu_seg) ? min(take, nmcu_seg - m0) : 0u;
+    for (uint32_t j0 = 0; j0 < n; j0 += kStep) {
+        const uint32_t jb = j0 + kPer * lane;
+        uint32_t pm[kPer], pin[kPer], em[kPer], ex[kPer];
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < kPer; t++) {
+            const uint32_t j = jb + t;
+            const bool in = j <= jl;  // pieces past jl: no MCUs
+            pm[t] = in ? b.piece_nmcu[base + j] : 0u;
+            em[t] = in ? b.piece_emcu[base + j] : kNoError;
+            pin[t] = (in && j != jl) ? pm[t] : 0u;
+            ex[t] = tot;  // exclusive within the lane
+            tot += pin[t];
         }
-        mcu_run += __shfl(int(im), 63, 64);
+        const uint32_t before = mcu_run + uint32_t(wave_scan_dpp(int(tot))) - tot;
+#pragma unroll
+        for (uint32_t t = 0; t < kPer; t++) {
+            const uint32_t j = jb + t;
+            const uint32_t m0 = before + ex[t];
+            uint32_t take = 0;
+            if (j <= jl) take = piece_take(pm[t], em[t], m0, nmcu_seg, j == jl, final_seg, bad);
+            if (j < n) {
+                b.piece_mcu0[base + j] = min(m0, nmcu_seg);
+                b.piece_nmcu[base + j] = (m0 <= nmcu_seg) ? min(take, nmcu_seg - m0) : 0u;
+            }
+        }
+        mcu_run = uint32_t(__shfl(int(before + tot), 63, 64));
     }
     if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
 }
