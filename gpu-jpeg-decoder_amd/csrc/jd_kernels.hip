@@ -1303,22 +1303,16 @@ __device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_
 // ended, and give each piece its first MCU and its MCU count by prefix sums.  An interval where
 // some start still disagrees after k_redo (a double failure, rare) is flagged for k_chain_fix,
 // which walks it serially with re-walks.
-__global__ __launch_bounds__(256) void k_chain(BatchDev b) {
-    JD_PRIO_CRIT();
-    const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u;
-    if (s >= b.nseg) return;  // wave-uniform
-    SegInfo S;
-    seg_info(b, s, S);
-    const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
-    const uint32_t nmcu_seg = S.nblk / S.bpm;
-    const bool final_seg = seg_is_final(b, s);
+// One wave per interval s of n pieces (k_chain), kPer consecutive pieces per lane: an interval
+// without DRI can have a thousand pieces, and each wave-iteration is a round of dependent global
+// loads (kPer = 4 there; 1 for the short intervals of DRI streams).
+template <uint32_t kPer>
+__device__ __forceinline__ void chain_interval(const BatchDev& b, uint32_t s, uint32_t lane, const SegInfo& S,
+                                               uint32_t base, uint32_t n, uint32_t nmcu_seg, bool final_seg) {
     // The scan's last interval ends at EOI, and what follows its last MCU is ignored: the piece
     // whose MCUs reach the interval's count is the last one that matters, and the pieces after it
     // (decoding trailing bytes) are dropped.
-    // Four consecutive pieces per lane, 256 per wave-iteration: an interval without DRI can have
-    // a thousand pieces, and each iteration is a round of dependent global loads.
-    constexpr uint32_t kPer = 4, kStep = 64 * kPer;
+    constexpr uint32_t kStep = 64 * kPer;
     uint32_t jl = n - 1;
     if (final_seg) {
         uint32_t run = 0;
@@ -1387,6 +1381,22 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
         mcu_run = uint32_t(__shfl(int(before + tot), 63, 64));
     }
     if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+}
+
+__global__ __launch_bounds__(256) void k_chain(BatchDev b) {
+    JD_PRIO_CRIT();
+    const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (s >= b.nseg) return;  // wave-uniform
+    SegInfo S;
+    seg_info(b, s, S);
+    const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
+    const uint32_t nmcu_seg = S.nblk / S.bpm;
+    const bool final_seg = seg_is_final(b, s);
+    if (n > 64)
+        chain_interval<4>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+    else
+        chain_interval<1>(b, s, lane, S, base, n, nmcu_seg, final_seg);
 }
 
 // One lane per interval flagged by k_chain (workgroups grouped by table set): walk its pieces in
