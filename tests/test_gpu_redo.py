@@ -4,7 +4,9 @@ With a short warm-up (JD_PIECE_OVERLAP_BITS) most speculative piece starts are w
 re-walks them and k_chain_fix walks the intervals where a re-walked piece's predecessor was itself
 re-walked.  With JD_SPARE_PIECES=0 no spare region is left: every re-walk writes over its own region
 and cannot join the speculative walk (jd_kernels.hip redo_piece); with the default spare regions it
-joins at a checkpoint and the piece's blocks come from two segments (k_gather).
+joins at a checkpoint and the piece's blocks come from two segments (k_gather).  The re-walks read
+the Huffman tables from global memory (each table set's LUTs in BatchDev::set_luts); the grayscale
+image adds a second table set.
 """
 import os
 import sys
@@ -27,12 +29,14 @@ IMAGES = [  # (w, h, subsampling, restart_rows, quality)
     (1280, 720, "4:2:2", 2, 50),
     (333, 251, "4:2:0", 0, 90),
     (640, 480, "4:4:4", 0, 100),  # quality 100: AC values beyond +-511 take escaped 16-bit entry slots
+    (1280, 720, "gray", 0, 85),   # a second table set (one component): k_redo / k_chain_fix read
+                                  # their tables at a nonzero offset of BatchDev::set_luts
 ]
 
 
 @pytest.fixture(scope="module")
 def batch():
-    datas = [jd_synth.encode(jd_synth.synth_pixels(w, h, 5 + i), q, ss, rr)
+    datas = [jd_synth.encode(jd_synth.synth_pixels(w, h, 5 + i, ss == "gray"), q, "4:4:4" if ss == "gray" else ss, rr)
              for i, (w, h, ss, rr, q) in enumerate(IMAGES)]
     refs = []
     for d in datas:
