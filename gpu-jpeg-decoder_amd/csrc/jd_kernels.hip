@@ -1924,6 +1924,9 @@ __device__ __forceinline__ int dot2(uint32_t a, uint32_t k, int c) {
 #ifndef JD_HALVES
 #define JD_HALVES 1
 #endif
+#ifndef JD_QUAD_SKIP
+#define JD_QUAD_SKIP 1
+#endif
 __device__ __forceinline__ int dot2_0(uint32_t a, uint32_t k) {
 #if JD_DOT2_ASM
     int r;
@@ -2433,8 +2436,10 @@ __device__ __forceinline__ void scatter_entries(uint32_t* s_buf, uint32_t base, 
         }
         return;
     }
+    // quads no lane of the wave has are skipped (wave-uniform): their slots would all be masked
 #pragma unroll
-    for (int u = 0; u < kPreQuads; u++) scatter_quad(row, base, E[u], u, r);
+    for (int u = 0; u < kPreQuads; u++)
+        if (!JD_QUAD_SKIP || u == 0 || __any(u < r.n4)) scatter_quad(row, base, E[u], u, r);
     for (int c = kPreQuads; c < r.n4; c += 4) {
         uint4 v[4];
 #pragma unroll
