@@ -382,8 +382,8 @@ def cpu_baseline(hosts, hdrs, target_s: float = 5.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=40)  # ~0.3 s on C2: the two-batch pipeline's ramp is amortised
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override images per rank")
     ap.add_argument("--quality", type=int, default=90)
