@@ -12,9 +12,15 @@ collective on the data path; one all-gather of per-rank counters at the end (RCC
 
 Rank 0 prints one JSON line (contract in the task statement) with, besides the contract keys:
   roofline      the dominant kernel's algorithmic bytes / its hipEvent-measured average launch time
-                against the 8 TB/s HBM peak, the same against an in-run copy-kernel peak, its HBM
-                traffic and VALU issue fraction from the committed PMC profiles (profiles/)
-  e2e_h2d       the same batch with the JPEG bytes handed over in host memory (PCIe-inclusive)
+                against the 8 TB/s HBM peak, the same against an in-run copy-kernel peak (the
+                library's 16-byte-per-lane copy, jd_test_copy_peak), its HBM traffic and VALU issue
+                fraction from the committed PMC profiles (profiles/); `bound` names the roof that
+                binds it ("valu" when the committed SQ profile shows VALU busy > 0.7, else "hbm")
+  e2e_h2d       the same batch with the JPEG bytes handed over in host memory (PCIe-inclusive,
+                pipelined: host staging of batch k+1 overlaps the GPU's batch k), next to an in-run
+                pinned H2D rate of the same byte count
+  per_rank      every rank's step time, host phase times (parse, plan, input staging, wait) and its
+                concurrent e2e_h2d leg, from the one all-gather (shows whether the host feed binds)
   cpu_baseline  the reference's own CPU decoder (oracle/_ref/ref_bench, built from its sources) on
                 the BASELINE config-1 image, and the oracle (the CPU restatement, which also decodes
                 4:2:0 / RST) on a bounded sample of this workload, 1 core and all cores, with the
@@ -196,6 +202,29 @@ def gather_matrix(local, world: int):
     return local.cpu().numpy()[None]
 
 
+RANK_FIELDS = ["elapsed_s", "pixels", "images", "ecs_bytes", "jpeg_bytes", "ecs_bytes_per_step",
+               "images_per_step", "ms_per_step", "parse_ms", "plan_ms", "stage_ms", "wait_ms", "e2e_ms",
+               "h2d_GB_s"]
+
+
+def rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, steps, host_ms_step, e2e_ms, h2d_gbs):
+    """This rank's counter vector for the one all-gather (order: RANK_FIELDS; column 0 = elapsed
+    is max-reduced, 1-4 summed)."""
+    return [elapsed, pixels * steps, n * steps, ecs * steps, jpeg_bytes * steps, ecs, n,
+            elapsed / max(1, steps) * 1e3, host_ms_step.get("parse", 0.0), host_ms_step.get("plan", 0.0),
+            host_ms_step.get("stage_inputs", 0.0), host_ms_step.get("wait", 0.0), e2e_ms, h2d_gbs]
+
+
+def per_rank_table(allc, steps):
+    """Per-rank diagnostics from the gathered matrix: step time, host phases per step (parse, plan,
+    input staging, time blocked waiting for the GPU), the concurrent e2e_h2d leg and pinned H2D rate."""
+    keys = RANK_FIELDS[7:]
+    out = {k: [round(float(x), 4) for x in allc[:, RANK_FIELDS.index(k)]] for k in keys}
+    host = allc[:, 8] + allc[:, 9]
+    out["host_parse_plan_over_step"] = [round(float(h / m), 4) if m > 0 else None for h, m in zip(host, allc[:, 7])]
+    return out
+
+
 def gather_counters(local, world: int):
     """(max over ranks of counter 0 = elapsed, sums of the other counters)."""
     allc = gather_matrix(local, world)
@@ -223,9 +252,10 @@ def measured_traffic(config: str, kernel: str):
 
 
 def valu_issue(config: str, kernel: str, avg_ms: float):
-    """VALU issue fraction of `kernel` from the newest committed SQ profile of this config
-    (profiles/<round>_sq_<config>.json): VALU wave-instructions per launch x 2 cycles over the
-    SIMD-cycles of the launch at the clock the profiled run held (GRBM_GUI_ACTIVE / 8 XCDs / time)."""
+    """VALU busy fraction of `kernel` from the newest committed SQ profile of this config
+    (profiles/<round>_sq_<config>.json): SQ_ACTIVE_INST_VALU quad-cycles per launch x 4 cycles
+    (VALU_CYCLES_PER_QUAD) over the SIMD-cycles of the launch at the clock the profiled run held
+    (GRBM_GUI_ACTIVE / 8 XCDs / time)."""
     k, src = newest_profile("*_sq_*.json", config, kernel)
     if not k or avg_ms <= 0:
         return None
@@ -256,26 +286,38 @@ def kernel_rooflines(kern: dict, config: str) -> dict:
     return out
 
 
-def copy_peak_gbs(dev, gib: float = 4.0, reps: int = 5):
-    """In-run HBM peak: a device-to-device copy of `gib` GiB (read + write bytes / time)."""
+def copy_peak_gbs(dec, dev, gib: float = 4.0, reps: int = 10):
+    """In-run HBM peak: the library's 16-byte-per-lane copy kernel (jd_test_copy_peak, the guide's
+    "float4 copy" of MI355X_MICROARCH.md) over `gib` GiB, read + write bytes / time (hipEvents on the
+    decoder's stream)."""
     import torch
 
-    n = int(gib * (1 << 30))
+    n = int(gib * (1 << 30)) // 16 * 16
     a = torch.empty(n, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
     a.fill_(1)
-    b.copy_(a)
     torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize(dev)
-    gbs = 2.0 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    gbs = dec.copy_peak(a.data_ptr(), b.data_ptr(), n, reps)
     del a, b
     torch.cuda.empty_cache()
     return gbs
+
+
+def pinned_h2d_gbs(nbytes: int, dev, reps: int = 3):
+    """In-run pinned host -> device copy rate for `nbytes` (the PCIe leg of e2e_h2d)."""
+    import torch
+
+    src = torch.empty(int(nbytes), dtype=torch.uint8).pin_memory()
+    dst = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(reps):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter() - t
+    del src, dst
+    return nbytes * reps / t / 1e9
 
 
 def cpu_model():
@@ -345,6 +387,12 @@ def cpu_baseline(hosts, hdrs, target_s: float = 5.0):
     res["port_1core"] = {"MPix_s": px1 / s1 / 1e6, "images": n1, "seconds": s1}
     res["port_all_cores"] = {"MPix_s": pxall / sall / 1e6, "images": nall, "seconds": sall, "threads": cores}
     res["value"] = res["port_all_cores"]["MPix_s"]
+    # every CPU this process may use: the box's rules cap one GPU's job at BOX_CPU_SHARE threads, so
+    # this is the measured per-thread rate at `cores` threads scaled linearly (an upper bound: no
+    # memory-bandwidth or SMT saturation is modelled), not a measurement
+    allowed = len(os.sched_getaffinity(0))
+    res["port_all_allowed_projected"] = {"MPix_s": res["value"] / cores * allowed, "cpus": allowed,
+                                         "note": f"linear extrapolation of the {cores}-thread rate"}
 
     c1 = jd_synth.encode(jd_synth.synth_pixels(512, 512, 0), 90, "4:4:4", 0, 0)
     c1a = np.frombuffer(c1, np.uint8).copy()
@@ -369,7 +417,8 @@ def cpu_baseline(hosts, hdrs, target_s: float = 5.0):
             cal = res["port_c1_1core_MPix_s"] / res["reference_c1"]["MPix_s_1core"]
             res["calibration_port_over_reference"] = cal
             res["reference_equivalent"] = {"MPix_s_1core": px1 / s1 / 1e6 / cal,
-                                           "MPix_s_all_cores": res["value"] / cal}
+                                           "MPix_s_all_cores": res["value"] / cal,
+                                           "MPix_s_all_allowed_projected": res["value"] / cal / cores * allowed}
             sample_desc += f"; reference: config-1 image x{reps} on 1 process, x{max(2, reps // 2)} on {cores}"
         else:
             res["reference_c1"] = None
@@ -389,7 +438,7 @@ def main():
     ap.add_argument("--quality", type=int, default=90)
     ap.add_argument("--cpu-sample", type=int, default=1, help="1: time the CPU baselines, 0: skip")
     ap.add_argument("--verify", type=int, default=1, help="check images {0, n/2, n-1} bit-exact vs the oracle")
-    ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the H2D-inclusive run (0: skip)")
+    ap.add_argument("--e2e-steps", type=int, default=8, help="steps of the H2D-inclusive run (0: skip)")
     ap.add_argument("--copy-peak", type=int, default=1, help="measure an in-run HBM copy peak")
     ap.add_argument("--kernel-steps", type=int, default=3,
                     help="serialized (non-overlapped) steps after the timed region for per-kernel times")
@@ -439,7 +488,6 @@ def main():
     # two output buffers: consecutive pipelined batches (in flight together on the decoder's two
     # slot streams) write different memory, as distinct batches of a real stream would
     rgb_bufs = [torch.empty(otot, dtype=torch.uint8, device=dev) for _ in range(2)]
-    rgb_dev = rgb_bufs[0]
     flat = np.zeros(tot, np.uint8)
     for h, o in zip(hosts, in_offs):
         flat[o:o + h.nbytes] = h
@@ -477,6 +525,7 @@ def main():
             verified.append(i)
 
     dec.reset_stats()
+    torch.cuda.reset_peak_memory_stats(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -491,6 +540,7 @@ def main():
     if args.verify and any(r.status for b in batches for r in b[1]):  # the last timed batches' statuses
         raise SystemExit("decode failed inside the timed region")
     st_overlap = dec.stats()
+    host_ms_step = {k: v / args.steps for k, v in st_overlap["host_ms"].items()}
     # per-kernel times for the roofline from serialized batches (outside the timed region): in the
     # timed loop consecutive batches overlap on the slot streams, so a kernel's hipEvent span there
     # includes the other batch's kernels
@@ -499,27 +549,44 @@ def main():
         dec.decode_prepared(batches[k & 1], pipelined=False)
     st = dec.stats()
 
-    # PCIe-inclusive rate (not `value`): the JPEG bytes handed over in host memory, RGB to HBM
+    # PCIe-inclusive rate (not `value`): the JPEG bytes handed over in host memory, RGB to HBM;
+    # pipelined like the timed loop (the host stages batch k+1 while the GPU decodes batch k), run
+    # by every rank at once so a multi-GPU run shows the shared host's feed rate
     e2e = None
+    e2e_ms = h2d_gbs = 0.0
     if args.e2e_steps:
-        host_batch = dec.make_batch(hosts, [None] * n, [rgb_dev.data_ptr() + o for o in out_offs])
-        dec.decode_prepared(host_batch)
+        host_batches = [dec.make_batch(hosts, [None] * n, [rb.data_ptr() + o for o in out_offs]) for rb in rgb_bufs]
+        for k in range(2):
+            dec.decode_prepared(host_batches[k], pipelined=True)
+        dec.wait()
+        dec.reset_stats()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize(dev)
         te = time.perf_counter()
-        for _ in range(args.e2e_steps):
-            dec.decode_prepared(host_batch)
+        for k in range(args.e2e_steps):
+            dec.decode_prepared(host_batches[k & 1], pipelined=True)
+        dec.wait()
         torch.cuda.synchronize(dev)
         te = time.perf_counter() - te
-        if any(r.status for r in host_batch[1]):
+        if any(r.status for b in host_batches for r in b[1]):
             raise SystemExit("decode failed in the H2D-inclusive run")
-        e2e = {"MPix_s": pixels * args.e2e_steps / te / 1e6, "ms_per_step": te / args.e2e_steps * 1e3,
-               "steps": args.e2e_steps, "note": "per rank; JPEG bytes from pageable host memory through the "
-               "library's pinned staging + H2D copy, RGB left in HBM"}
+        se = dec.stats()
+        e2e_ms = te / args.e2e_steps * 1e3
+        h2d_gbs = pinned_h2d_gbs(int(jpeg_bytes), dev)
+        bound_ms = jpeg_bytes / (h2d_gbs * 1e9) * 1e3
+        e2e = {"MPix_s": pixels * args.e2e_steps / te / 1e6, "ms_per_step": e2e_ms,
+               "steps": args.e2e_steps, "pinned_h2d_GB_s": h2d_gbs, "h2d_bound_ms_per_step": bound_ms,
+               "frac_of_h2d_bound": bound_ms / e2e_ms,
+               "host_ms_per_step": {k: v / args.e2e_steps for k, v in se["host_ms"].items()},
+               "note": "per rank; JPEG bytes from pageable host memory, copied by the library's host workers "
+                       "into per-slot pinned staging and uploaded on the slot's stream while the other slot "
+                       "decodes (jd_decode_batch_async); RGB left in HBM"}
 
-    # one all-gather of per-rank counters (RCCL over xGMI when N > 1)
-    local = torch.tensor([elapsed, pixels * args.steps, n * args.steps, ecs * args.steps,
-                          jpeg_bytes * args.steps, ecs, n], dtype=torch.float64,
-                         device=dev if d["backend"] == "nccl" else "cpu")
+    # one all-gather of per-rank counters (RCCL over xGMI when N > 1): totals for the line, and
+    # every rank's step time and host feed (so an 8-GPU run shows whether the host binds)
+    local = torch.tensor(rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, args.steps, host_ms_step, e2e_ms, h2d_gbs),
+                         dtype=torch.float64, device=dev if d["backend"] == "nccl" else "cpu")
     allc = gather_matrix(local, world)
     t_max = float(allc[:, 0].max())
     tot_px, tot_img, tot_ecs, tot_bytes = (float(allc[:, k].sum()) for k in range(1, 5))
@@ -532,7 +599,8 @@ def main():
         per_launch_bytes = kd["bytes"] / max(1, kd["launches"])
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic = measured_traffic(args.config, dom)
-        copy_gbs = copy_peak_gbs(dev) if (args.copy_peak and world == 1) else None
+        copy_gbs = copy_peak_gbs(dec, dev) if (args.copy_peak and world == 1) else None
+        vb = valu_issue(args.config, dom, avg_ms)
         cpu = cpu_baseline(hosts, hdrs) if (args.cpu_sample and world == 1) else None
         px_rank = float(sum(h.width * h.height for h in hdrs))
         res = {
@@ -564,13 +632,13 @@ def main():
             "images_per_s": tot_img / t_max,
             "jpeg_MB_per_s": tot_bytes / t_max / 1e6,
             "ecs_MB_per_s": tot_ecs / t_max / 1e6,
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "valu" if vb and vb["busy_frac"] > 0.7 else "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,
                          "measured_copy_peak": copy_gbs,
                          "frac_of_measured_peak": achieved / copy_gbs if copy_gbs else None,
-                         "valu": valu_issue(args.config, dom, avg_ms),
+                         "valu": vb,
                          "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes,
                          "timing": f"hipEvents on the decode stream, {max(1, args.kernel_steps)} serialized batches"},
             "kernel_rooflines": kernel_rooflines(kern, args.config),
@@ -579,6 +647,11 @@ def main():
                                                for k, v in st_overlap["kernels"].items()},
             "path_roofline_frac": ((ecs + 3 * pixels) / (t_max / args.steps) / 1e9) / HBM_PEAK_GBS,
             "e2e_h2d": e2e,
+            "per_rank": per_rank_table(allc, args.steps),
+            "device_memory": {"decoder_pools_peak_GB": dec.device_bytes()[1] / 1e9,
+                              "torch_peak_GB": torch.cuda.max_memory_allocated(dev) / 1e9,
+                              "note": "rank 0: the library's grow-only pools (two in-flight slots) and the "
+                                      "bench's own input/output buffers"},
             "cpu_baseline": cpu,
             "verified_bit_exact": verified,
             "gen_s": t_gen,

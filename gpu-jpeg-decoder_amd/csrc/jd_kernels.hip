@@ -25,6 +25,7 @@
 // Arithmetic follows the reference CPU decoder bit for bit (cpp-decoder/src/idct.cpp,
 // utils/color.cpp); the restatement used as checker lives in oracle/ (tests only).
 #include <hip/hip_runtime.h>
+#include <mutex>
 
 #include "jd_kernels.hpp"
 
@@ -2962,35 +2963,67 @@ __global__ void k_test_color(const int32_t* ycc, uint8_t* rgb, int n) {
     rgb[3 * i + 2] = uint8_t(B);
 }
 
+// HBM copy peak (bench.py's in-run roofline reference, MI355X_MICROARCH.md "float4 copy"): each
+// lane moves four 16-byte vectors, all four loads issued before the stores, consecutive lanes on
+// consecutive vectors (every wave instruction covers 1 KiB).
+constexpr int kCopyThreads = 256, kCopyPer = 4;
+typedef uint32_t copy_v4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(kCopyThreads) void k_copy16(const copy_v4* __restrict__ src, copy_v4* __restrict__ dst,
+                                                         size_t n16) {
+    const size_t base = size_t(blockIdx.x) * (kCopyThreads * kCopyPer) + threadIdx.x;
+    copy_v4 v[kCopyPer];
+    if (base + (kCopyPer - 1) * kCopyThreads < n16) {
+#pragma unroll
+        for (int k = 0; k < kCopyPer; k++) v[k] = src[base + k * kCopyThreads];
+#pragma unroll
+        for (int k = 0; k < kCopyPer; k++) dst[base + k * kCopyThreads] = v[k];
+        return;
+    }
+    for (int k = 0; k < kCopyPer; k++)
+        if (base + k * kCopyThreads < n16) dst[base + k * kCopyThreads] = src[base + k * kCopyThreads];
+}
+
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
 size_t huffman_lds_bytes(uint32_t max_slots) { return piece_lds_bytes(max_slots, kPieceThreads); }
 
 uint32_t piece_lanes_resident(size_t lds) {
-    static size_t cached_lds = 0;
-    static uint32_t cached = 0;
-    if (lds == cached_lds && cached) return cached;
+    // cached per device (a process may drive several GPUs, one context each)
+    constexpr int kMaxDev = 64;
+    static std::mutex m;
+    static size_t cached_lds[kMaxDev] = {};
+    static uint32_t cached[kMaxDev] = {};
     int dev = 0, cus = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+    std::lock_guard<std::mutex> l(m);
+    if (dev < kMaxDev && lds == cached_lds[dev] && cached[dev]) return cached[dev];
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     if (lds > 65536)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_piece<kPieceThreads>), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_piece<kPieceThreads>, kPieceThreads, lds) != hipSuccess || nb <= 0) return 0;
-    cached_lds = lds;
-    cached = uint32_t(nb) * uint32_t(cus) * uint32_t(kPieceThreads);
-    return cached;
+    const uint32_t lanes = uint32_t(nb) * uint32_t(cus) * uint32_t(kPieceThreads);
+    if (dev < kMaxDev) {
+        cached_lds[dev] = lds;
+        cached[dev] = lanes;
+    }
+    return lanes;
 }
 
 // Dynamic LDS above 64 KiB (large piece workgroups) has to be allowed per kernel once.
 static hipError_t allow_lds(size_t lds) {
-    static size_t allowed = 65536;
-    if (lds <= allowed) return hipSuccess;
+    constexpr int kMaxDev = 64;  // per device, as piece_lanes_resident
+    static std::mutex m;
+    static size_t allowed[kMaxDev] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+    std::lock_guard<std::mutex> l(m);
+    if (lds <= std::max<size_t>(65536, allowed[dev])) return hipSuccess;
     for (const void* f : {reinterpret_cast<const void*>(&k_piece<kPieceThreads>), reinterpret_cast<const void*>(&k_piece<64>)}) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
-    allowed = lds;
+    allowed[dev] = lds;
     return hipSuccess;
 }
 
@@ -3069,6 +3102,14 @@ hipError_t launch_test_idct(const int32_t* in_zz, int32_t* out, int n, int exact
 
 hipError_t launch_test_color(const int32_t* ycc, uint8_t* rgb, int n, hipStream_t s) {
     hipLaunchKernelGGL(k_test_color, dim3((n + 255) / 256), dim3(256), 0, s, ycc, rgb, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy16(const void* src, void* dst, size_t bytes, hipStream_t s) {
+    const size_t n16 = bytes / 16;
+    const size_t per = size_t(kCopyThreads) * kCopyPer;
+    hipLaunchKernelGGL(k_copy16, dim3(uint32_t((n16 + per - 1) / per)), dim3(kCopyThreads), 0, s,
+                       static_cast<const copy_v4*>(src), static_cast<copy_v4*>(dst), n16);
     return hipGetLastError();
 }
 

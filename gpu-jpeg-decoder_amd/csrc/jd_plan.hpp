@@ -1,0 +1,59 @@
+// jd_plan.hpp — the host plan's pure functions (no HIP): geometry of a parsed image, its
+// AC-entry reservation and its device descriptor.  jd_runtime.cpp's build_plan calls them; the
+// sanitizer harness (tools/jd_fuzz_host.cpp, ASan + UBSan) drives them on mutated files.
+#pragma once
+
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "jd.h"
+#include "jd_internal.hpp"
+#include "jd_parse.hpp"
+
+namespace jd {
+
+// Sampling layout of an image for k_idct_color's specialised instances (jd_kernels.hip TMode):
+// 1 = 4:2:0 (Y 2x2), 2 = 4:2:2 (Y 2x1), 3 = 4:4:4, each with one Cb and one Cr block per MCU in
+// frame order; 0 = anything else (generic instance).
+uint32_t image_mode(const ImgDesc& d);
+
+// AC-entry region words of one image: its pieces' regions (jd_internal.hpp
+// region_words: at most ECS bits / 2 + kRegionSlack + 8 per piece slot) and spare regions for the
+// re-walks of pieces whose speculative start was wrong (~0.6 % of full-size pieces; with short
+// pieces, up to every piece).
+inline uint64_t piece_slots(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits) {
+    return (ecs_bytes * 8 + piece_bits - 1) / piece_bits + nseg;
+}
+inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits, int64_t spare_pieces = -1) {
+    const uint64_t bits = ecs_bytes * 8, slots = piece_slots(ecs_bytes, nseg, piece_bits);
+    uint64_t spare = (piece_bits >= bits) ? 0 : (piece_bits >= 4096 ? slots / 16 + 8 : slots);
+    if (spare_pieces >= 0) spare = uint64_t(spare_pieces);  // JD_SPARE_PIECES (tests: in-place re-walks)
+    return bits / 2 + 4 + slots * (kRegionSlack + 8) + spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)));
+}
+inline uint32_t image_segments(const jd_header& h) {
+    const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
+    return h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
+}
+
+// An image's AC-entry offsets are image-relative 32-bit values in 16-bit slot units
+// (BlockInfo::entry_start, k_gather's running offset): its reservation at the shortest pieces must
+// stay below 2^31 words, else the plan rejects it with JD_ERR_CAPACITY.
+constexpr uint64_t kMaxImageEntryWords = 0x7FFFFF00ull;
+inline bool image_fits(uint64_t ecs_bytes, const jd_header& h) {
+    return entry_words(ecs_bytes, image_segments(h), kMinPieceBits) <= kMaxImageEntryWords;
+}
+
+// Per image of the plan: what the sequential pass decides (table set, quant slots, bases).
+struct PlanImg {
+    int item, ts;
+    uint16_t qslot[3];
+    uint64_t block_base, entry_base, comp;
+    uint32_t seg_base, nseg, chunk_base, nchunks;
+};
+
+// Fills d (everything but the piece ranges) for item it; pure function of the header + bases.
+void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uint64_t out_addr, const PlanImg& pi,
+               ImgDesc& d);
+
+}  // namespace jd

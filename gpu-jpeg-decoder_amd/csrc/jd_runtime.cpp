@@ -6,6 +6,7 @@
 // no allocation.  Replaces the reference's per-image extract()/allocate()/clean() cycle
 // (cuda-decoder/benchmark_thoughput/benchmark.cu:49-93) which cudaMalloc'ed every image.
 #include <hip/hip_runtime_api.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdio.h>
 #include <chrono>
 #include <cstdlib>
@@ -28,6 +29,7 @@
 #include "jd_internal.hpp"
 #include "jd_kernels.hpp"
 #include "jd_parse.hpp"
+#include "jd_plan.hpp"
 #include "jd_test.h"
 
 using namespace jd;
@@ -39,12 +41,18 @@ struct DevBuf {
     size_t cap = 0;
 };
 
-struct PinBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-};
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// roctx range over a host phase (parse / plan / launch / collect), visible in rocprofv3
+// --marker-trace next to the kernels; the analogue of the reference's NVTX ranges
+// (cuda-decoder/benchmark/benchmark.cu:41,70).
+struct Range {
+    explicit Range(const char* what) { roctxRangePushA(what); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range&) = delete;
+    Range& operator=(const Range&) = delete;
+};
 
 struct CachedLut {
     HuffSpec spec;
@@ -133,6 +141,9 @@ struct Pending {
     size_t host_cap = 0;
     void* plan_host = nullptr;                  // pinned staging of this slot's plan blob
     size_t plan_cap = 0;
+    void* in_host = nullptr;                    // pinned staging of this slot's host-memory JPEG inputs
+    size_t in_cap = 0;
+    DevBuf d_input;                             // device copy of those inputs
     hipEvent_t done = nullptr;
     hipEvent_t ev[JD_NUM_KERNELS][2] = {};
     bool timing = false, fancy = false;
@@ -156,9 +167,9 @@ struct jd_ctx {
     DevBuf lut_dev;
     size_t lut_dev_count = 0;
 
-    // pools shared by the slots (host inputs / outputs: collected before reuse)
-    DevBuf input, output;
-    PinBuf input_host;
+    // output pool shared by the slots (host outputs: collected before reuse); host inputs are
+    // staged per slot (Pending::in_host / d_input), so host-input batches pipeline too
+    DevBuf output;
 
     Pending pend[2];
     int slot = 0;  // the slot the next launch uses
@@ -175,6 +186,8 @@ struct jd_ctx {
     // last batch (jd_debug_fetch)
     BatchDev last{};
     uint64_t last_blocks = 0, last_entries = 0;
+    std::vector<uint64_t> last_entry_base;  // per image (jd_debug_fetch 20)
+    uint64_t dev_bytes = 0, dev_peak = 0;   // device pool bytes held now / at most (jd_device_bytes)
 };
 
 namespace {
@@ -190,30 +203,52 @@ jd_status hip_fail(jd_ctx* ctx, hipError_t e, const char* what) {
         if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);  \
     } while (0)
 
-hipError_t ensure_dev(DevBuf& b, size_t bytes) {
+// Waits for everything this context has in flight: the pending batches (their done events, on
+// the slot streams or a caller stream) and the context stream.  Unlike hipDeviceSynchronize it
+// does not stall the caller's unrelated streams.
+hipError_t quiesce(jd_ctx* ctx) {
+    hipError_t r = hipSuccess;
+    for (Pending& pd : ctx->pend)
+        if (pd.active) {
+            const hipError_t e = hipEventSynchronize(pd.done);
+            if (e != hipSuccess) r = e;
+        }
+    if (ctx->stream) {
+        const hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) r = e;
+    }
+    return r;
+}
+
+// Makes the context stream wait for the pending batches (jd.h: calls on one context are ordered).
+hipError_t order_after_pending(jd_ctx* ctx) {
+    for (Pending& pd : ctx->pend)
+        if (pd.active) {
+            const hipError_t e = hipStreamWaitEvent(ctx->stream, pd.done, 0);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+hipError_t ensure_dev(jd_ctx* ctx, DevBuf& b, size_t bytes) {
     if (bytes <= b.cap) return hipSuccess;
     const size_t n = std::max(bytes, b.cap + b.cap / 2);
     if (b.p) {
-        (void)hipDeviceSynchronize();  // a launched batch may still use it (jd_decode_batch_async)
+        (void)quiesce(ctx);  // a launched batch may still use it (jd_decode_batch_async)
         (void)hipFree(b.p);
+        ctx->dev_bytes -= b.cap;
     }
     b.p = nullptr;
     b.cap = 0;
     hipError_t e = hipMalloc(&b.p, n);
-    if (e == hipSuccess) b.cap = n;
+    if (e == hipSuccess) {
+        b.cap = n;
+        ctx->dev_bytes += n;
+        ctx->dev_peak = std::max(ctx->dev_peak, ctx->dev_bytes);
+    }
     return e;
 }
 
-hipError_t ensure_pin(PinBuf& b, size_t bytes) {
-    if (bytes <= b.cap) return hipSuccess;
-    const size_t n = std::max(bytes, b.cap + b.cap / 2);
-    if (b.p) (void)hipHostFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-    hipError_t e = hipHostMalloc(&b.p, n, hipHostMallocDefault);
-    if (e == hipSuccess) b.cap = n;
-    return e;
-}
 
 int lut_id(jd_ctx* ctx, const HuffSpec& s, bool is_dc, uint64_t h) {
     auto range = ctx->lut_by_hash.equal_range(h);
@@ -234,7 +269,7 @@ int lut_id(jd_ctx* ctx, const HuffSpec& s, bool is_dc, uint64_t h) {
 
 jd_status sync_luts(jd_ctx* ctx) {
     if (ctx->lut_dev_count == ctx->lut_host.size()) return JD_OK;
-    HIPCHK(ctx, ensure_dev(ctx->lut_dev, ctx->lut_host.size() * sizeof(HuffLut)));
+    HIPCHK(ctx, ensure_dev(ctx, ctx->lut_dev, ctx->lut_host.size() * sizeof(HuffLut)));
     HIPCHK(ctx, hipMemcpyAsync(ctx->lut_dev.p, ctx->lut_host.data(), ctx->lut_host.size() * sizeof(HuffLut),
                                hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -243,6 +278,7 @@ jd_status sync_luts(jd_ctx* ctx) {
 }
 
 void parse_all(jd_ctx* ctx, const jd_item* items, int n) {
+    Range r("jd_parse");
     ctx->parsed.resize(size_t(n));
     ctx->pst.resize(size_t(n));
     constexpr int kPer = 16;  // images per work item
@@ -275,35 +311,6 @@ struct Plan {
     uint32_t mode_off[4] = {0, 0, 0, 0}, mode_cnt[4] = {0, 0, 0, 0}, mode_max_tiles[4] = {0, 0, 0, 0};
 };
 
-// Sampling layout of an image for k_idct_color's specialised instances (jd_kernels.hip TMode):
-// 1 = 4:2:0 (Y 2x2), 2 = 4:2:2 (Y 2x1), 3 = 4:4:4, each with one Cb and one Cr block per MCU in
-// frame order; 0 = anything else (generic instance).
-uint32_t image_mode(const ImgDesc& d) {
-    if (d.ncomp != 3 || d.h[1] != 1 || d.v[1] != 1 || d.h[2] != 1 || d.v[2] != 1) return 0;
-    if (d.h[0] == 2 && d.v[0] == 2) return 1;
-    if (d.h[0] == 2 && d.v[0] == 1) return 2;
-    if (d.h[0] == 1 && d.v[0] == 1) return 3;
-    return 0;
-}
-
-// AC-entry region words of one image: its pieces' regions (jd_internal.hpp
-// region_words: at most ECS bits / 2 + kRegionSlack + 8 per piece slot) and spare regions for the
-// re-walks of pieces whose speculative start was wrong (~0.6 % of full-size pieces; with short
-// pieces, up to every piece).
-inline uint64_t piece_slots(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits) {
-    return (ecs_bytes * 8 + piece_bits - 1) / piece_bits + nseg;
-}
-inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits, int64_t spare_pieces = -1) {
-    const uint64_t bits = ecs_bytes * 8, slots = piece_slots(ecs_bytes, nseg, piece_bits);
-    uint64_t spare = (piece_bits >= bits) ? 0 : (piece_bits >= 4096 ? slots / 16 + 8 : slots);
-    if (spare_pieces >= 0) spare = uint64_t(spare_pieces);  // JD_SPARE_PIECES (tests: in-place re-walks)
-    return bits / 2 + 4 + slots * (kRegionSlack + 8) + spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)));
-}
-inline uint32_t image_segments(const jd_header& h) {
-    const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
-    return h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
-}
-
 // Largest item prefix [lo, hi) whose sparse-coefficient words stay within the context's
 // max_batch_entries (default kMaxBatchEntries; entry indices are image-relative, this only bounds
 // the pool, 4 B per word; estimated at full-size pieces).  JD_MAX_BATCH_ENTRIES overrides it
@@ -321,78 +328,6 @@ int batch_split(jd_ctx* ctx, int lo, int n, const jd_item* items) {
         cap += w;
     }
     return hi;
-}
-
-// Per image of the plan: what the sequential pass decides (table set, quant slots, bases).
-struct PlanImg {
-    int item, ts;
-    uint16_t qslot[3];
-    uint64_t block_base, entry_base, comp;
-    uint32_t seg_base, nseg, chunk_base, nchunks;
-};
-
-// Fills d (everything but the piece ranges) for item it; pure function of the header + bases.
-void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uint64_t out_addr, const PlanImg& pi,
-               ImgDesc& d) {
-    const jd_header& h = pj.hdr;
-    memset(&d, 0, sizeof(d));
-    d.jpeg = dev_addr;
-    d.rgb = out_addr;
-    d.len = uint32_t(item.len);
-    d.ecs_off = uint32_t(h.ecs_offset);
-    d.width = uint32_t(h.width);
-    d.height = uint32_t(h.height);
-    d.mcux = uint32_t(h.mcux);
-    d.mcuy = uint32_t(h.mcuy);
-    d.ncomp = uint32_t(h.ncomp);
-    d.hmax = uint32_t(h.hmax);
-    d.vmax = uint32_t(h.vmax);
-    d.bpm = uint32_t(h.blocks_per_mcu);
-    uint32_t pat = 0, b = 0;
-    for (int c = 0; c < h.ncomp; c++) {
-        d.h[c] = uint8_t(h.h[c]);
-        d.v[c] = uint8_t(h.v[c]);
-        d.comp_block0[c] = uint8_t(b);
-        for (int j = 0; j < h.h[c] * h.v[c]; j++, b++) pat |= uint32_t(c) << (2 * b);
-        d.qslot[c] = pi.qslot[c];
-    }
-    {  // k_idct_color's fast-IDCT range test: |c| <= 2^(k-1) keeps |c * step| < 2^15 (int16)
-        uint32_t qmax = 1;
-        for (int c = 0; c < h.ncomp; c++)
-            for (int k = 0; k < 64; k++) qmax = std::max<uint32_t>(qmax, pj.q[h.tq[c]][k]);
-        uint32_t k = 1;
-        while (k < 16 && (uint64_t(1) << k) * qmax < 32768) k++;  // largest k: 2^(k-1) * qmax < 2^15
-        const uint32_t lo = (0xFFFFu << k) & 0xFFFFu;
-        d.qmask = lo | (lo << 16);
-    }
-    d.block_pattern = pat;
-    d.restart_interval = uint32_t(h.restart_interval);
-    d.nseg = pi.nseg;
-    d.seg_base = pi.seg_base;
-    d.block_base = pi.block_base;
-    d.tableset = uint32_t(pi.ts);
-    {  // IDCT/colour tiles: one wave, one lane per block: the most blocks <= 64 over 1 or 2 MCU rows
-        uint32_t lw = 0, lh = 0;
-        while ((8u << lw) < 8u * d.hmax) lw++;
-        while ((8u << lh) < 8u * d.vmax) lh++;
-        d.lg_mw = 3 + lw;
-        d.lg_mh = 3 + lh;
-        // a run of consecutive MCUs of one MCU row (k_idct_color's DC prediction scans it in order)
-        d.tile_mcus = std::max(1u, uint32_t(kTileMaxBlocks) / d.bpm);
-        d.tile_mrows = 1;
-        d.tiles_x = (d.mcux + d.tile_mcus - 1) / d.tile_mcus;
-        d.tiles_y = (d.mcuy + d.tile_mrows - 1) / d.tile_mrows;
-        for (int c = 0; c < h.ncomp; c++) {
-            uint32_t sx = 0, sy = 0;
-            while ((uint32_t(h.h[c]) << sx) < d.hmax) sx++;
-            while ((uint32_t(h.v[c]) << sy) < d.vmax) sy++;
-            d.shx[c] = uint8_t(sx);
-            d.shy[c] = uint8_t(sy);
-        }
-    }
-    d.nchunks = pi.nchunks;  // scan chunks over [align16(file + ecs_off), file + len)
-    d.chunk_base = pi.chunk_base;
-    d.comp = pi.comp;  // offset for now; rebased onto the pool in launch_batch
 }
 
 jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const std::vector<uint64_t>& dev_addr,
@@ -414,8 +349,8 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         if (ctx->pst[it] != JD_OK) continue;
         const ParsedJpeg& pj = ctx->parsed[it];
         const jd_header& h = pj.hdr;
-        if (entry_words(items[it].len - h.ecs_offset, image_segments(h), kMinPieceBits) > 0xFFFFFF00ull) {
-            ctx->pst[it] = JD_ERR_CAPACITY;  // image-relative entry indices are 32-bit
+        if (!image_fits(items[it].len - h.ecs_offset, h)) {  // jd_plan.hpp kMaxImageEntryWords
+            ctx->pst[it] = JD_ERR_CAPACITY;
             continue;
         }
         bool same_tables = prev && prev->hdr.ncomp == h.ncomp;
@@ -638,20 +573,33 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         if (!rgb_on_device) out_bytes += align_up(size_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3, 256);
     }
     if (in_bytes) {
-        HIPCHK(ctx, ensure_dev(ctx->input, in_bytes));
-        HIPCHK(ctx, ensure_pin(ctx->input_host, in_bytes));
+        // Host-memory inputs: copied into this slot's pinned staging by the host workers in
+        // parallel (pieces of at most 1 MiB), then one H2D on the slot's stream, which overlaps
+        // the other slot's kernels.  The slot is idle here (collected above).
+        Range r("jd_stage_inputs");
+        const auto ts0 = std::chrono::steady_clock::now();
+        HIPCHK(ctx, ensure_dev(ctx, pd.d_input, in_bytes));
+        HIPCHK(ctx, ensure_pinned(pd.in_host, pd.in_cap, in_bytes));
+        struct Piece { const uint8_t* src; size_t off, n; };
+        std::vector<Piece> pieces;
+        constexpr size_t kStagePiece = size_t(1) << 20;
         size_t off = 0;
         for (int i = lo; i < hi; i++) {
             if (ctx->pst[i] != JD_OK || items[i].jpeg_dev) continue;
-            memcpy(static_cast<uint8_t*>(ctx->input_host.p) + off, items[i].jpeg, items[i].len);
-            dev_addr[i] = reinterpret_cast<uint64_t>(ctx->input.p) + off;
+            for (size_t k = 0; k < items[i].len; k += kStagePiece)
+                pieces.push_back({items[i].jpeg + k, off + k, std::min(kStagePiece, items[i].len - k)});
+            dev_addr[i] = reinterpret_cast<uint64_t>(pd.d_input.p) + off;
             off += align_up(items[i].len + 64, 256);
         }
-        HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, ctx->input_host.p, in_bytes, hipMemcpyHostToDevice, s));
+        uint8_t* const stage = static_cast<uint8_t*>(pd.in_host);
+        ctx->pool->run(int(pieces.size()), [&](int k) { memcpy(stage + pieces[size_t(k)].off, pieces[size_t(k)].src, pieces[size_t(k)].n); });
+        HIPCHK(ctx, hipMemcpyAsync(pd.d_input.p, pd.in_host, in_bytes, hipMemcpyHostToDevice, s));
+        ctx->stats.host_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+        ctx->stats.h2d_bytes += double(in_bytes);
     }
     for (int i = lo; i < hi; i++)
         if (ctx->pst[i] == JD_OK && items[i].jpeg_dev) dev_addr[i] = reinterpret_cast<uint64_t>(items[i].jpeg_dev);
-    if (out_bytes) HIPCHK(ctx, ensure_dev(ctx->output, out_bytes));
+    if (out_bytes) HIPCHK(ctx, ensure_dev(ctx, ctx->output, out_bytes));
     {
         size_t off = 0;
         for (int i = lo; i < hi; i++) {
@@ -666,6 +614,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     }
 
     // 2. plan
+    std::unique_ptr<Range> rng(new Range("jd_plan"));
     const auto tp0 = std::chrono::steady_clock::now();
     auto tms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count(); };
     Plan P;
@@ -676,7 +625,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     if (st != JD_OK) return st;
     const uint32_t nimg = uint32_t(P.imgs.size());
     if (nimg) {
-        HIPCHK(ctx, ensure_dev(pd.d_comp, std::max<size_t>(16, P.comp_bytes)));
+        HIPCHK(ctx, ensure_dev(ctx, pd.d_comp, std::max<size_t>(16, P.comp_bytes)));
         for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(pd.d_comp.p);
         const bool fancy = (ctx->flags & JD_FLAG_FANCY_UPSAMPLING) != 0;
         uint32_t max_fancy_wgs = 0;
@@ -692,7 +641,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
                 const uint64_t groups = uint64_t((d.width + 7) / 8) * d.height;
                 max_fancy_wgs = std::max<uint32_t>(max_fancy_wgs, uint32_t((groups + 255) / 256));
             }
-            HIPCHK(ctx, ensure_dev(pd.d_planes, std::max<size_t>(16, tot)));
+            HIPCHK(ctx, ensure_dev(ctx, pd.d_planes, std::max<size_t>(16, tot)));
             for (size_t i = 0; i < P.imgs.size(); i++)
                 P.imgs[i].planes = reinterpret_cast<uint64_t>(pd.d_planes.p) + poff[i];
         }
@@ -737,13 +686,13 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_fix = reserve(end, nseg * 4);
         const size_t o_tdc = reserve(end, size_t(P.total_tiles) * sizeof(DcPred));
         const size_t o_slow = reserve(end, size_t(P.total_tiles) * 8);
-        HIPCHK(ctx, ensure_dev(pd.d_plan, end));
+        HIPCHK(ctx, ensure_dev(ctx, pd.d_plan, end));
         HIPCHK(ctx, ensure_pinned(pd.plan_host, pd.plan_cap, upload));
         memcpy(pd.plan_host, blob.data(), upload);
         HIPCHK(ctx, hipMemcpyAsync(pd.d_plan.p, pd.plan_host, upload, hipMemcpyHostToDevice, s));
-        HIPCHK(ctx, ensure_dev(pd.d_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
-        HIPCHK(ctx, ensure_dev(pd.d_blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
-        HIPCHK(ctx, ensure_dev(pd.d_entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
+        HIPCHK(ctx, ensure_dev(ctx, pd.d_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
+        HIPCHK(ctx, ensure_dev(ctx, pd.d_blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
+        HIPCHK(ctx, ensure_dev(ctx, pd.d_entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
 
         uint8_t* base = static_cast<uint8_t*>(pd.d_plan.p);
         BatchDev b;
@@ -811,7 +760,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             b.mode_max_tiles[m] = P.mode_max_tiles[m];
         }
         if (std::getenv("JD_STAMPS")) {  // diagnostic builds (JD_STAMP): per-tile phase stamps
-            HIPCHK(ctx, ensure_dev(pd.d_stamps, size_t(P.total_tiles) * 64));
+            HIPCHK(ctx, ensure_dev(ctx, pd.d_stamps, size_t(P.total_tiles) * 64));
             HIPCHK(ctx, hipMemsetAsync(pd.d_stamps.p, 0, size_t(P.total_tiles) * 64, s));
             b.stamps = static_cast<unsigned long long*>(pd.d_stamps.p);
         }
@@ -821,8 +770,11 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         ctx->last = b;
         ctx->last_blocks = P.total_blocks;
         ctx->last_entries = P.total_entry_cap;
+        ctx->last_entry_base.resize(P.imgs.size());
+        for (size_t i = 0; i < P.imgs.size(); i++) ctx->last_entry_base[i] = P.imgs[i].entry_base;
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
         const double t_upload = tms();
+        rng.reset(new Range("jd_launch"));
         double t_k[JD_NUM_KERNELS];
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
             if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][0], s));
@@ -851,6 +803,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         pd.piece_overlap = double(P.piece_overlap);
         pd.t_plan = t_plan;
         pd.t_upload = t_upload - t_plan;
+        ctx->stats.host_ms[1] += t_upload;  // plan + plan upload
     }
     pd.nimg = nimg;
     pd.item_of_img = P.item_of_img;
@@ -879,8 +832,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
 jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
     if (!pd.active) return JD_OK;
     pd.active = false;
+    Range r("jd_collect");
     const auto tw0 = std::chrono::steady_clock::now();
     HIPCHK(ctx, hipEventSynchronize(pd.done));
+    ctx->stats.host_ms[3] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
     const uint32_t nimg = pd.nimg;
     if (nimg) {
         const unsigned long long* ctr = static_cast<const unsigned long long*>(pd.host);
@@ -1034,13 +989,14 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
 jd_status jd_ctx_destroy(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&ctx->lut_dev, &ctx->input, &ctx->output})
+    (void)quiesce(ctx);
+    for (DevBuf* b : {&ctx->lut_dev, &ctx->output})
         if (b->p) (void)hipFree(b->p);
-    if (ctx->input_host.p) (void)hipHostFree(ctx->input_host.p);
     for (Pending& pd : ctx->pend) {
-        for (DevBuf* b : {&pd.d_plan, &pd.d_brk, &pd.d_blocks, &pd.d_entries, &pd.d_comp, &pd.d_planes, &pd.d_stamps})
+        for (DevBuf* b : {&pd.d_plan, &pd.d_brk, &pd.d_blocks, &pd.d_entries, &pd.d_comp, &pd.d_planes, &pd.d_stamps,
+                          &pd.d_input})
             if (b->p) (void)hipFree(b->p);
+        if (pd.in_host) (void)hipHostFree(pd.in_host);
         if (pd.stream) (void)hipStreamDestroy(pd.stream);
         if (pd.host) (void)hipHostFree(pd.host);
         if (pd.plan_host) (void)hipHostFree(pd.plan_host);
@@ -1079,20 +1035,18 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
         if (st != JD_OK) return st;
         ctx->last_stream = hip_stream;
     }
-    // The host input staging buffer and the output pool are reused per launch: with host inputs
-    // or host outputs, collect first, and collect every sub-batch before launching the next.
-    bool host_inputs = false;
-    for (int i = 0; i < n && !host_inputs; i++) host_inputs = !items[i].jpeg_dev;
-    if (host_inputs || !rgb_on_device) {
+    // The output pool is shared by the slots: with host outputs, collect first, and collect every
+    // sub-batch before launching the next.  Host inputs are staged per slot and pipeline.
+    if (!rgb_on_device) {
         const jd_status st = finish_all(ctx);
         if (st != JD_OK) return st;
         async = false;
     }
     const auto t0 = std::chrono::steady_clock::now();
     parse_all(ctx, items, n);
-    if (ctx->host_timing)
-        std::fprintf(stderr, "host parse %.3f ms\n",
-                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    const double t_parse = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->stats.host_ms[0] += t_parse;
+    if (ctx->host_timing) std::fprintf(stderr, "host parse %.3f ms\n", t_parse);
     for (int lo = 0; lo < n;) {
         const int hi = batch_split(ctx, lo, n, items);
         hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->pend[ctx->slot].stream;
@@ -1204,6 +1158,7 @@ jd_status jd_device_free(jd_ctx* ctx, void* dptr) {
 
 jd_status jd_memcpy_h2d(jd_ctx* ctx, void* dst, const void* src, size_t n) {
     if (!ctx || (n && (!dst || !src))) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, order_after_pending(ctx));  // an in-flight batch may still read dst
     HIPCHK(ctx, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return JD_OK;
@@ -1211,6 +1166,7 @@ jd_status jd_memcpy_h2d(jd_ctx* ctx, void* dst, const void* src, size_t n) {
 
 jd_status jd_memcpy_d2h(jd_ctx* ctx, void* dst, const void* src, size_t n) {
     if (!ctx || (n && (!dst || !src))) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, order_after_pending(ctx));  // an in-flight batch may still write src
     HIPCHK(ctx, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return JD_OK;
@@ -1262,11 +1218,15 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
         case 17: src = b.piece_amcu; n = size_t(b.nsub) * 4; break;
         case 18: src = b.piece_join; n = size_t(b.nsub) * 4; break;
         case 19: src = b.seg_ent; n = size_t(b.nseg) * 4; break;
+        case 20:  // per image of the last batch: ImgDesc::entry_base (u64, 32-bit words), host copy
+            *nbytes = ctx->last_entry_base.size() * 8;
+            if (dst) memcpy(dst, ctx->last_entry_base.data(), std::min(*nbytes, cap));
+            return JD_OK;
         default: return JD_ERR_INVALID_ARG;
     }
     *nbytes = n;
     if (dst && src && n) {
-        HIPCHK(ctx, hipDeviceSynchronize());  // the last batch ran on a slot's stream
+        HIPCHK(ctx, quiesce(ctx));  // the last batch ran on a slot's stream
         HIPCHK(ctx, hipMemcpy(dst, src, std::min(n, cap), hipMemcpyDeviceToHost));
     }
     return JD_OK;
@@ -1290,6 +1250,34 @@ jd_status jd_test_color(jd_ctx* ctx, const int32_t* ycc_dev, uint8_t* rgb_dev, i
     if (!ctx || !ycc_dev || !rgb_dev || n < 0) return JD_ERR_INVALID_ARG;
     HIPCHK(ctx, launch_test_color(ycc_dev, rgb_dev, n, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return JD_OK;
+}
+
+jd_status jd_device_bytes(jd_ctx* ctx, uint64_t* current, uint64_t* peak) {
+    if (!ctx) return JD_ERR_INVALID_ARG;
+    if (current) *current = ctx->dev_bytes;
+    if (peak) *peak = ctx->dev_peak;
+    return JD_OK;
+}
+
+jd_status jd_test_copy_peak(jd_ctx* ctx, const void* src, void* dst, size_t bytes, int reps, double* gbs) {
+    if (!ctx || !src || !dst || !gbs || reps <= 0 || bytes == 0 || bytes % 16) return JD_ERR_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    HIPCHK(ctx, order_after_pending(ctx));
+    hipEvent_t e0, e1;
+    HIPCHK(ctx, hipEventCreate(&e0));
+    HIPCHK(ctx, hipEventCreate(&e1));
+    hipError_t e = launch_copy16(src, dst, bytes, ctx->stream);  // warm-up
+    if (e == hipSuccess) e = hipEventRecord(e0, ctx->stream);
+    for (int r = 0; r < reps && e == hipSuccess; r++) e = launch_copy16(src, dst, bytes, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(e1, ctx->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (e != hipSuccess) return hip_fail(ctx, e, "jd_test_copy_peak");
+    *gbs = ms > 0 ? 2.0 * double(bytes) * reps / (double(ms) * 1e-3) / 1e9 : 0.0;
     return JD_OK;
 }
 

@@ -33,7 +33,7 @@ JD_FLAG_FORCE_LANES = 4
 JD_FLAG_FANCY_UPSAMPLING = 8
 JD_FLAG_FULL_PIECES = 16
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES, "full": JD_FLAG_FULL_PIECES}
-JD_ABI_VERSION = 4
+JD_ABI_VERSION = 5
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece", "k_redo", "k_chain",
                 "k_gather", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
@@ -72,7 +72,8 @@ class _Stats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_int * JD_NUM_KERNELS), ("total_ms", ctypes.c_double * JD_NUM_KERNELS),
                 ("bytes", ctypes.c_double * JD_NUM_KERNELS), ("batches", ctypes.c_double),
                 ("images", ctypes.c_double), ("pixels", ctypes.c_double), ("ecs_bytes", ctypes.c_double),
-                ("blocks", ctypes.c_double), ("segments", ctypes.c_double), ("subsequences", ctypes.c_double)]
+                ("blocks", ctypes.c_double), ("segments", ctypes.c_double), ("subsequences", ctypes.c_double),
+                ("host_ms", ctypes.c_double * 4), ("h2d_bytes", ctypes.c_double)]
 
 
 # Every symbol include/jd.h and include/jd_test.h declare (checked by tests/test_abi.py).
@@ -81,6 +82,7 @@ EXPORTED_SYMBOLS = [
     "jd_decode_batch_async", "jd_decode_wait", "jd_write_array", "jd_write_ppm", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
     "jd_memcpy_h2d", "jd_memcpy_d2h", "jd_synchronize", "jd_get_stats", "jd_reset_stats",
     "jd_kernel_name", "jd_test_idct", "jd_test_idct_exact", "jd_test_color", "jd_debug_fetch", "jd_ctx_last_error",
+    "jd_test_copy_peak", "jd_device_bytes",
 ]
 
 _lib = None
@@ -125,6 +127,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         "jd_test_color": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
         "jd_debug_fetch": (c_int, [c_void_p, c_int, c_void_p, c_size_t, ctypes.POINTER(c_size_t)]),
         "jd_ctx_last_error": (ctypes.c_char_p, [c_void_p]),
+        "jd_device_bytes": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+        "jd_test_copy_peak": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -365,7 +369,16 @@ class Decoder:
                         for k in range(JD_NUM_KERNELS)},
             "batches": s.batches, "images": s.images, "pixels": s.pixels, "ecs_bytes": s.ecs_bytes,
             "blocks": s.blocks, "segments": s.segments, "subsequences": s.subsequences,
+            "host_ms": {"parse": s.host_ms[0], "plan": s.host_ms[1], "stage_inputs": s.host_ms[2],
+                        "wait": s.host_ms[3]},
+            "h2d_bytes": s.h2d_bytes,
         }
+
+    def device_bytes(self):
+        """(bytes the context's device pools hold now, their high-water mark)."""
+        cur, peak = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.jd_device_bytes(self.ctx, ctypes.byref(cur), ctypes.byref(peak))
+        return cur.value, peak.value
 
     def last_error(self) -> str:
         return (self.lib.jd_ctx_last_error(self.ctx) or b"").decode()
@@ -379,7 +392,8 @@ class Decoder:
                     "sub_seg": (9, np.uint32, 1), "status": (10, np.uint32, 1), "entries": (11, np.uint32, 1),
                     "piece_mcu0": (12, np.uint32, 1), "piece_abase": (13, np.uint32, 1),
                     "piece_cp": (14, np.uint32, 36), "stamps": (15, np.uint64, 8), "piece_emcu": (16, np.uint32, 1),
-                    "piece_amcu": (17, np.uint32, 1), "piece_join": (18, np.uint32, 1), "seg_ent": (19, np.uint32, 1)}
+                    "piece_amcu": (17, np.uint32, 1), "piece_join": (18, np.uint32, 1), "seg_ent": (19, np.uint32, 1),
+                    "entry_base": (20, np.uint64, 1)}
 
     def debug_fetch(self, name: str) -> np.ndarray:
         """Internal array of the most recent batch (white-box tests and debugging)."""
@@ -409,6 +423,15 @@ class Decoder:
         din.free()
         dout.free()
         return out
+
+    def copy_peak(self, src_ptr: int, dst_ptr: int, nbytes: int, reps: int = 5) -> float:
+        """HBM copy peak in GB/s (read + write bytes): the library's 16-byte-per-lane copy kernel
+        over caller device buffers (jd_test_copy_peak)."""
+        g = ctypes.c_double()
+        st = self.lib.jd_test_copy_peak(self.ctx, src_ptr, dst_ptr, nbytes, reps, ctypes.byref(g))
+        if st != JD_OK:
+            raise JDError(st, "jd_test_copy_peak " + self.last_error())
+        return g.value
 
     def test_color(self, ycc: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(ycc, dtype=np.int32).reshape(-1, 3)

@@ -11,8 +11,10 @@
  * Output format: interleaved uint8 RGB, H*W*3 bytes, row-major (the reference writes the same
  * values as three int planes in a text `.array` file — jd_write_array reproduces that file).
  *
- * Threading: a jd_ctx belongs to one host thread and one HIP device; calls on one context are
- * ordered on its stream.  jd_parse and jd_write_array are reentrant and context-free.
+ * Threading: a jd_ctx belongs to one host thread and one HIP device.  Calls on one context are
+ * ordered: the memcpy helpers and jd_synchronize run after every batch the context has launched
+ * (pending jd_decode_batch_async work included, on whichever stream it runs).  jd_parse and
+ * jd_write_array are reentrant and context-free.
  */
 #ifndef JD_H
 #define JD_H
@@ -24,7 +26,7 @@
 extern "C" {
 #endif
 
-#define JD_ABI_VERSION 4
+#define JD_ABI_VERSION 5
 
 typedef enum jd_status {
     JD_OK = 0,
@@ -43,12 +45,15 @@ typedef struct jd_ctx jd_ctx;
 
 /* jd_opts.flags */
 #define JD_FLAG_TIMING 1u /* record hipEvents around every kernel launch (jd_get_stats) */
-/* Entropy-decode piece size (default: 8192-bit pieces).  Results are identical for every
- * setting; the flags exist so tests can stress the two extremes of the piece-parallel decode. */
-#define JD_FLAG_FORCE_SYNC 2u  /* 1024-bit pieces: many speculative starts, exercises re-scans */
+/* Entropy-decode piece size.  Default: pieces of at least 16384 bits (kPieceBits) with a 4096-bit
+ * warm-up; for large batches the device-side planner (k_pieceplan) grows them up to ~2x so the
+ * pieces fill whole rounds of resident lanes.  Results are identical for every setting; the flags
+ * exist so tests can stress the two extremes of the piece-parallel decode. */
+#define JD_FLAG_FORCE_SYNC 2u  /* 1024-bit pieces: many speculative starts, exercises re-walks */
 #define JD_FLAG_FORCE_LANES 4u /* one piece per restart interval (the whole scan if no DRI) */
-/* Small batches (under ~64 K pieces of 8192 bits) use shorter pieces by default, down to 512 bits
- * with a 2x-piece warm-up; this flag keeps 8192-bit pieces / 4096-bit warm-up for every batch. */
+/* Small batches (under ~64 K pieces of 16384 bits) use shorter pieces by default, down to 512 bits
+ * with a 2x-piece warm-up; this flag keeps 16384-bit pieces / 4096-bit warm-up for every batch
+ * (k_pieceplan may still grow them for large batches). */
 #define JD_FLAG_FULL_PIECES 16u
 /* Chroma upsampling: replicate (default; the semantics pinned in DESIGN.md §2) or, with this flag,
  * libjpeg's triangular "fancy" filter for 2x1, 2x2 and 1x2 ratios (closer to libjpeg-turbo /
@@ -122,12 +127,15 @@ jd_status jd_decode_file(jd_ctx* ctx, const char* path, uint8_t* rgb, size_t rgb
 jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
                           int rgb_on_device, void* hip_stream);
 
-/* Pipelined form of jd_decode_batch for inputs and outputs already in device memory (jpeg_dev
- * and rgb device pointers; other items make it behave as jd_decode_batch): returns once the
- * batch is launched, after collecting the batch launched before it, so the host parses and plans
- * batch k+1 while the GPU decodes batch k.  results[] (and the caller's buffers) must stay valid
- * until the batch is collected: by the next jd_decode_batch_async / jd_decode_batch call on the
- * context, or by jd_decode_wait. */
+/* Pipelined form of jd_decode_batch with device outputs (rgb are device pointers): returns once
+ * the batch is launched, after collecting the batch launched before it, so the host parses and
+ * plans batch k+1 (and stages its host inputs) while the GPU decodes batch k.  Inputs may be
+ * device-resident (jpeg_dev) or host memory (jpeg_dev NULL): host inputs are copied into the
+ * launching slot's pinned staging by the context's host workers before the call returns, and
+ * uploaded by an H2D on that slot's stream, which overlaps the other slot's kernels.
+ * results[], the rgb buffers and the jpeg_dev buffers must stay valid until the batch is
+ * collected: by the next jd_decode_batch_async / jd_decode_batch call on the context, or by
+ * jd_decode_wait; host jpeg buffers only until the call returns. */
 jd_status jd_decode_batch_async(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
                                 void* hip_stream);
 /* Collects every launched batch (fills their results). */
@@ -164,10 +172,17 @@ typedef struct jd_stats {
     double total_ms[JD_NUM_KERNELS]; /* hipEvent time, summed over launches                     */
     double bytes[JD_NUM_KERNELS];    /* algorithmic bytes moved, summed          */
     double batches, images, pixels, ecs_bytes, blocks, segments, subsequences;
+    /* host wall time (ms, summed): 0 header parse, 1 plan + plan upload, 2 staging of host-memory
+     * inputs (parallel memcpy into pinned memory + H2D issue), 3 waiting for batches to finish */
+    double host_ms[4];
+    double h2d_bytes; /* host-memory input bytes uploaded */
 } jd_stats;
 jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out);
 jd_status jd_reset_stats(jd_ctx* ctx);
 const char* jd_kernel_name(int k);
+/* Device memory the context's pools hold now and at most since creation (bytes; pools are
+ * grow-only: the piece regions of the largest batch dominate). */
+jd_status jd_device_bytes(jd_ctx* ctx, uint64_t* current, uint64_t* peak);
 
 #ifdef __cplusplus
 }

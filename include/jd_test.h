@@ -24,12 +24,19 @@ jd_status jd_test_idct_exact(jd_ctx* ctx, const int32_t* in_dev, int32_t* out_de
 /* ycc: n x (Y, Cb, Cr) IDCT outputs in [-256,255]; rgb: n x 3 bytes */
 jd_status jd_test_color(jd_ctx* ctx, const int32_t* ycc_dev, uint8_t* rgb_dev, int n);
 
+/* HBM copy peak: copies `bytes` (a multiple of 16) from src_dev to dst_dev `reps` times with a
+ * 16-byte-per-lane kernel and returns the read + write rate in GB/s (hipEvents on the context
+ * stream; the roofline reference of bench.py). */
+jd_status jd_test_copy_peak(jd_ctx* ctx, const void* src_dev, void* dst_dev, size_t bytes, int reps, double* gbs);
+
 /* Copies an internal array of the most recent batch to the host (debugging / white-box tests).
  * what: 0 blocks (8 B each), 1 seg_cstart, 2 seg_cend, 3 seg_sub_base, 4 seg_nsub (u32 each),
  *       5 piece_bit, 6 piece_end, 7 piece_nmcu, 8 piece_nent, 9 sub_seg (u32 per piece slot),
  *       10 status (u32 per image), 11 entries (u32), 12 piece_mcu0, 13 piece_ent0 (u32 per piece
  *       slot), 14 piece_cp (9 x 16 B per piece slot: 8 scan checkpoints {bit, MCUs, entries,
- *       error} and the totals {end, MCUs, entries, error | checkpoints << 8}).
+ *       error} and the totals {end, MCUs, entries, error | checkpoints << 8}), 15 stamps,
+ *       16 piece_emcu, 17 piece_amcu, 18 piece_join (u32 per piece slot), 19 seg_ent (u32 per
+ *       segment), 20 entry_base (u64 per image: first 32-bit word of its AC-entry region).
  *       *nbytes receives the array size; at most cap bytes are copied. */
 jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* host_dst, size_t cap, size_t* nbytes);
 

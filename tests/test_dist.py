@@ -45,7 +45,12 @@ def _worker(rank, world, port, batch, q):
     local = torch.tensor([elapsed, 64 * 48 * batch, batch, 100.0 * (rank + 1), 7.0], dtype=torch.float64)
     t_max, sums = bench.gather_counters(local, world)
     mat = bench.gather_matrix(torch.tensor([float(rank), float(len(seeds_c5))], dtype=torch.float64), world)
-    q.put((rank, d, threads, info, seeds_c2, seeds_c5, digests, t_max, sums, mat.tolist()))
+    # the bench's real per-rank vector: rank 1 is host-bound (slow parse + plan, slow e2e leg)
+    host = {"parse": 0.5 + 2.0 * rank, "plan": 0.25 + rank, "stage_inputs": 1.0, "wait": 0.1}
+    vec = bench.rank_vector(2.0 + rank, 64 * 48, batch, 1000.0, 1500.0, 10, host, 20.0 + 5 * rank, 50.0 - rank)
+    full = bench.gather_matrix(torch.tensor(vec, dtype=torch.float64), world)
+    table = bench.per_rank_table(full, 10)
+    q.put((rank, d, threads, info, seeds_c2, seeds_c5, digests, t_max, sums, mat.tolist(), table, full.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,7 +68,7 @@ def test_bench_rank_setup_sharding_and_counter_gather_gloo():
         p.join(60)
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
-    for rank, d, threads, info, _, _, _, t_max, sums, mat in out:
+    for rank, d, threads, info, _, _, _, t_max, sums, mat, table, full in out:
         assert d["world_seen"] == world and d["rank"] == rank and d["backend"] == "gloo"
         assert d["device_index"] == rank  # one device per local rank (no GPU here: index only)
         assert 1 <= threads <= bench_share() and info["rank_cpus"] >= 1
@@ -73,6 +78,13 @@ def test_bench_rank_setup_sharding_and_counter_gather_gloo():
         assert sums[2] == 300.0
         assert sums[3] == 14.0
         assert [r[0] for r in mat] == [0.0, 1.0] and sum(r[1] for r in mat) == world * batch
+        # per-rank diagnostics: every rank's row, in rank order
+        assert table["ms_per_step"] == [200.0, 300.0]
+        assert table["parse_ms"] == [0.5, 2.5] and table["plan_ms"] == [0.25, 1.25]
+        assert table["stage_ms"] == [1.0, 1.0] and table["wait_ms"] == [0.1, 0.1]
+        assert table["e2e_ms"] == [20.0, 25.0] and table["h2d_GB_s"] == [50.0, 49.0]
+        assert table["host_parse_plan_over_step"] == [round(0.75 / 200.0, 4), round(3.75 / 300.0, 4)]
+        assert max(r[0] for r in full) == 3.0 and sum(r[1] for r in full) == 2 * 64 * 48 * 10
     d0, d1 = set(out[0][6]), set(out[1][6])
     assert len(d0) == batch and len(d1) == batch and not (d0 & d1), "ranks must decode disjoint images"
     c2 = [set(o[4]) for o in out]
