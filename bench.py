@@ -444,6 +444,9 @@ def main():
                     help="serialized (non-overlapped) steps after the timed region for per-kernel times")
     ap.add_argument("--path", default="auto", choices=["auto", "sync", "lanes", "full"],
                     help="entropy-decode path (auto: lanes for images with restart intervals)")
+    ap.add_argument("--fancy", action="store_true",
+                    help="libjpeg's triangular chroma upsampling (JD_FLAG_FANCY_UPSAMPLING; an option beyond the "
+                         "reference, parity unpinned) instead of replication")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one blocking jd_decode_batch per step instead of jd_decode_batch_async (which "
                          "parses and plans step k+1 on the host while the GPU decodes step k)")
@@ -495,7 +498,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     threads, thread_info = host_threads(d)
-    dec = jdamd.Decoder(d["device_index"], timing=True, path=args.path, parse_threads=threads)
+    dec = jdamd.Decoder(d["device_index"], timing=True, path=args.path, parse_threads=threads, fancy=args.fancy)
     batches = [dec.make_batch(hosts, [jpeg_dev.data_ptr() + o for o in in_offs],
                               [rb.data_ptr() + o for o in out_offs]) for rb in rgb_bufs]
     pixels = float(sum(h.width * h.height for h in hdrs))
@@ -517,7 +520,7 @@ def main():
 
         for i in sorted({0, n // 2, n - 1}):
             h = hdrs[i]
-            st, ref = jdoracle.decode(datas[i])
+            st, ref = jdoracle.decode(datas[i], fancy=args.fancy)
             for rb in rgb_bufs:
                 got = rb[out_offs[i]:out_offs[i] + h.width * h.height * 3].cpu().numpy().reshape(h.height, h.width, 3)
                 if st != 0 or not np.array_equal(got, ref):
@@ -622,6 +625,7 @@ def main():
                        "global_batch": int(allc[:, 6].sum()), "width": W, "height": H, "subsampling": ss,
                        "restart_rows": rrows, "parallelism": f"dp{world} (image sharding)",
                        "entropy_path": args.path, "host_pipelined": pipelined,
+                       "upsampling": "fancy (libjpeg triangular)" if args.fancy else "replicate",
                        "bpp_file": 8 * jpeg_bytes / px_rank, "bpp_ecs": 8 * ecs / px_rank},
             "world_size_seen": d["world_seen"],
             "dist_backend": d["backend"],

@@ -574,8 +574,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     }
     if (in_bytes) {
         // Host-memory inputs: copied into this slot's pinned staging by the host workers in
-        // parallel (pieces of at most 1 MiB), then one H2D on the slot's stream, which overlaps
-        // the other slot's kernels.  The slot is idle here (collected above).
+        // parallel (pieces of at most 1 MiB), chunk by chunk; each chunk's H2D is issued on the
+        // slot's stream as soon as it is staged, so the DMA of chunk c overlaps the copy of chunk
+        // c + 1, and both overlap the other slot's kernels.  The slot is idle
+        // here (collected above).
         Range r("jd_stage_inputs");
         const auto ts0 = std::chrono::steady_clock::now();
         HIPCHK(ctx, ensure_dev(ctx, pd.d_input, in_bytes));
@@ -592,8 +594,19 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             off += align_up(items[i].len + 64, 256);
         }
         uint8_t* const stage = static_cast<uint8_t*>(pd.in_host);
-        ctx->pool->run(int(pieces.size()), [&](int k) { memcpy(stage + pieces[size_t(k)].off, pieces[size_t(k)].src, pieces[size_t(k)].n); });
-        HIPCHK(ctx, hipMemcpyAsync(pd.d_input.p, pd.in_host, in_bytes, hipMemcpyHostToDevice, s));
+        uint8_t* const dstage = static_cast<uint8_t*>(pd.d_input.p);
+        constexpr size_t kStageChunk = size_t(32) << 20;  // H2D granularity
+        for (size_t p0 = 0; p0 < pieces.size();) {
+            size_t p1 = p0 + 1;
+            while (p1 < pieces.size() && pieces[p1].off + pieces[p1].n - pieces[p0].off <= kStageChunk) p1++;
+            ctx->pool->run(int(p1 - p0), [&](int k) {
+                const Piece& q = pieces[p0 + size_t(k)];
+                memcpy(stage + q.off, q.src, q.n);
+            });
+            const size_t c0 = pieces[p0].off, c1 = (p1 < pieces.size()) ? pieces[p1].off : in_bytes;
+            HIPCHK(ctx, hipMemcpyAsync(dstage + c0, stage + c0, c1 - c0, hipMemcpyHostToDevice, s));
+            p0 = p1;
+        }
         ctx->stats.host_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
         ctx->stats.h2d_bytes += double(in_bytes);
     }
