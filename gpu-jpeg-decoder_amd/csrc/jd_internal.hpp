@@ -302,7 +302,7 @@ struct BatchDev {
     uint32_t mode_off[4], mode_cnt[4], mode_max_tiles[4];
     unsigned long long* stamps;   // diagnostic builds (JD_STAMP): 8 s_memtime stamps per IDCT tile, else null
     uint32_t fancy;
-    uint32_t max_fancy_wgs;       // k_colour_fancy workgroups per image (grid x)
+    uint32_t max_fancy_wgs;       // k_colour_fancy bands per image: x in bits 0..15, y in 16..31
 };
 
 }  // namespace jd

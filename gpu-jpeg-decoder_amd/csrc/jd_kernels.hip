@@ -2864,69 +2864,282 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
 // reference's un-shifted samples, edges replicated at the component's real sample extent; the
 // same definition as oracle/jdoracle.c fancy_sample().  Other ratios replicate.
 // ------------------------------------------------------------------------------------------
-struct FancyPlane {
-    const int16_t* p;
-    uint32_t pitch, rx, ry, cw, ch;
-    __device__ __forceinline__ int at(uint32_t x, uint32_t y) const { return gptr(p)[size_t(y) * pitch + x]; }
+// Fancy upsampling (libjpeg's h2v1 / h2v2 / h1v2 triangular filters, restated in
+// oracle/jdoracle.c fancy_sample; other ratios replicate) + colour, from the int16 component
+// planes k_idct_color wrote to HBM.  One 256-thread workgroup per 128 x 16-pixel band (four
+// bands stacked per workgroup): every component's window of plane samples (the band's rows and
+// columns plus the filter's one-sample halo, 16-byte aligned) is staged in LDS with coalesced
+// 16-byte loads, then thread t colours 8 consecutive pixels of row t / 16 and stores their 24 bytes.
+constexpr uint32_t kFancyW = 128, kFancyH = 16, kFancyThreads = 256;
+constexpr uint32_t kFancyRows = kFancyH + 2, kFancyCols = kFancyW + 16;  // window bound per component
+static_assert((kFancyW / 8) * kFancyH == kFancyThreads, "one 8-pixel group per thread");
+
+struct FancyWin {
+    const int16_t* s;       // LDS window: rows r0.., pitch kFancyCols samples, first column c0, ncols used
+    int r0, c0, ncols;
+    uint32_t rx, ry, cw, ch;
+    __device__ __forceinline__ const int16_t* row(int y) const { return s + __mul24(y - r0, int(kFancyCols)); }
+    __device__ __forceinline__ int at(int x, int y) const { return row(y)[x - c0]; }
 };
 
-__device__ __forceinline__ int fancy_px(const FancyPlane& P, uint32_t x, uint32_t y) {
-    if (P.rx == 2 && P.ry == 1) {
-        const uint32_t i = x >> 1;
-        if (x & 1) return i + 1 >= P.cw ? P.at(i, y) : (3 * P.at(i, y) + P.at(i + 1, y) + 2) >> 2;
+__device__ __forceinline__ int fancy_win(const FancyWin& P, uint32_t x, uint32_t y) {
+    if (P.rx == 2 && P.ry == 1) {  // h2v1_fancy_upsample
+        const int i = int(x >> 1);
+        if (x & 1) return uint32_t(i) + 1 >= P.cw ? P.at(i, y) : (3 * P.at(i, y) + P.at(i + 1, y) + 2) >> 2;
         return i == 0 ? P.at(0, y) : (3 * P.at(i, y) + P.at(i - 1, y) + 1) >> 2;
     }
-    if (P.ry == 2 && (P.rx == 1 || P.rx == 2)) {
-        const uint32_t r = y >> 1;
-        const uint32_t far = (y & 1) ? min(r + 1, P.ch - 1) : (r == 0 ? 0u : r - 1);
+    if (P.ry == 2 && (P.rx == 1 || P.rx == 2)) {  // h1v2 / h2v2_fancy_upsample
+        const int r = int(y >> 1);
+        const int far = (y & 1) ? min(r + 1, int(P.ch) - 1) : (r == 0 ? 0 : r - 1);
         if (P.rx == 1) return (3 * P.at(x, r) + P.at(x, far) + ((y & 1) ? 2 : 1)) >> 2;
-        const uint32_t i = x >> 1;
+        const int i = int(x >> 1);
         const int cs = 3 * P.at(i, r) + P.at(i, far);
         if (x & 1) {
-            if (i + 1 >= P.cw) return (4 * cs + 7) >> 4;
+            if (uint32_t(i) + 1 >= P.cw) return (4 * cs + 7) >> 4;
             return (3 * cs + 3 * P.at(i + 1, r) + P.at(i + 1, far) + 7) >> 4;
         }
         if (i == 0) return (4 * cs + 8) >> 4;
         return (3 * cs + 3 * P.at(i - 1, r) + P.at(i - 1, far) + 8) >> 4;
     }
-    return P.at(x / P.rx, y / P.ry);
+    return P.at(int(x / P.rx), int(y / P.ry));  // replicate
 }
 
-__global__ __launch_bounds__(256) void k_colour_fancy(BatchDev b) {
-    const ImgDesc& im = b.imgs[blockIdx.y];
-    const uint32_t W = im.width, H = im.height, gpr = (W + 7) >> 3;
-    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= gpr * H) return;
-    const uint32_t y = g / gpr, x0 = (g - y * gpr) << 3;
-    const uint32_t n = min(8u, W - x0);
-    FancyPlane P[3];
-    size_t off = 0;
+// The 8 chroma values under output pixels gx .. gx + 7 (gx a multiple of 8) of row y, for the
+// window's filter mode (both chroma planes share it): MODE 0 none (1x1), 1 h2v2, 2 h2v1, 3 h1v2.
+// Vector LDS reads: a 2x-horizontal filter needs samples i0 - 1 .. i0 + 4 of its rows (i0 = gx / 2,
+// a multiple of 4: one 8-byte read plus the two neighbours), a 1x one the 8 samples (16 bytes).
+template <int MODE>
+__device__ __forceinline__ void fancy_row8(const FancyWin& P, uint32_t gx, uint32_t y, int (&v)[8]) {
+    auto s16 = [](uint32_t w, int hi) { return hi ? int32_t(w) >> 16 : int(int16_t(w & 0xFFFFu)); };
+    if (MODE == 0 || MODE == 3) {
+        const int rr = MODE == 0 ? int(y) : int(y >> 1);
+        const uint4 q = *reinterpret_cast<const uint4*>(P.row(rr) + (int(gx) - P.c0));
+        const uint32_t a[4] = {q.x, q.y, q.z, q.w};
+        if (MODE == 0) {
 #pragma unroll
-    for (int c = 0; c < 3; c++) {
-        const uint32_t cc = uint32_t(c) < im.ncomp ? uint32_t(c) : 0u;
-        P[c].pitch = im.mcux * im.h[cc] * 8;
-        P[c].p = reinterpret_cast<const int16_t*>(im.planes) + (uint32_t(c) < im.ncomp ? off : 0);
-        P[c].rx = im.hmax / im.h[cc];
-        P[c].ry = im.vmax / im.v[cc];
-        P[c].cw = (W * im.h[cc] + im.hmax - 1) / im.hmax;
-        P[c].ch = (H * im.v[cc] + im.vmax - 1) / im.vmax;
-        if (uint32_t(c) < im.ncomp) off += size_t(P[c].pitch) * (im.mcuy * im.v[cc] * 8);
+            for (int j = 0; j < 8; j++) v[j] = s16(a[j >> 1], j & 1);
+            return;
+        }
+        const int far = (y & 1) ? min(rr + 1, int(P.ch) - 1) : max(rr - 1, 0);
+        const uint4 f = *reinterpret_cast<const uint4*>(P.row(far) + (int(gx) - P.c0));
+        const uint32_t b[4] = {f.x, f.y, f.z, f.w};
+        const int rnd = (y & 1) ? 2 : 1;
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = (3 * s16(a[j >> 1], j & 1) + s16(b[j >> 1], j & 1) + rnd) >> 2;
+        return;
     }
-    uint32_t rgb[8][3];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint32_t x = min(x0 + uint32_t(j), W - 1);
-        const int yv = fancy_px(P[0], x, y);
-        if (im.ncomp == 1) {
-            rgb[j][0] = rgb[j][1] = rgb[j][2] = clamp_u8(yv + 128);
-        } else {
-            const int cb = fancy_px(P[1], x, y), cr = fancy_px(P[2], x, y);
-            colour_px(yv, cb, cr, chroma_terms(cb, cr), rgb[j][0], rgb[j][1], rgb[j][2]);
+    const int i0 = int(gx >> 1);
+    const int lo = max(i0 - 1, P.c0) - P.c0, hi = min(i0 + 4 - P.c0, P.ncols - 1);
+    int C[6];  // columns i0 - 1 .. i0 + 4: 3 S(i, r) + S(i, far) (h2v2) or S(i, y) (h2v1)
+    {
+        const int rr = MODE == 1 ? int(y >> 1) : int(y);
+        const int16_t* row = P.row(rr);
+        const uint2 q = *reinterpret_cast<const uint2*>(row + (i0 - P.c0));
+        C[0] = row[lo];
+        C[1] = s16(q.x, 0);
+        C[2] = s16(q.x, 1);
+        C[3] = s16(q.y, 0);
+        C[4] = s16(q.y, 1);
+        C[5] = row[hi];
+        if (MODE == 1) {
+            const int far = (y & 1) ? min(rr + 1, int(P.ch) - 1) : max(rr - 1, 0);
+            const int16_t* frow = P.row(far);
+            const uint2 f = *reinterpret_cast<const uint2*>(frow + (i0 - P.c0));
+            C[0] = 3 * C[0] + frow[lo];
+            C[1] = 3 * C[1] + s16(f.x, 0);
+            C[2] = 3 * C[2] + s16(f.x, 1);
+            C[3] = 3 * C[3] + s16(f.y, 0);
+            C[4] = 3 * C[4] + s16(f.y, 1);
+            C[5] = 3 * C[5] + frow[hi];
         }
     }
-    uint32_t w[6];
-    pack24(rgb, w);
-    store24(reinterpret_cast<uint8_t*>(im.rgb) + (size_t(y) * W + x0) * 3, w, n);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // pixels 2k (even: sample i0 + k and its left) and 2k + 1 (odd: its right)
+        const int i = i0 + k, c = C[k + 1];
+        const bool first = i == 0, last = uint32_t(i) + 1 >= P.cw;
+        if (MODE == 1) {
+            v[2 * k] = first ? (4 * c + 8) >> 4 : (3 * c + C[k] + 8) >> 4;
+            v[2 * k + 1] = last ? (4 * c + 7) >> 4 : (3 * c + C[k + 2] + 7) >> 4;
+        } else {
+            v[2 * k] = first ? c : (3 * c + C[k] + 1) >> 2;
+            v[2 * k + 1] = last ? c : (3 * c + C[k + 2] + 2) >> 2;
+        }
+    }
+}
+
+// 8 pixels: Y (1x1 window), filtered chroma, then the packed integer colour of k_idct_color (terms
+// per pixel here) with the same double-precision G patch.
+template <int MODE>
+__device__ __forceinline__ void fancy_colour8(const FancyWin (&P)[3], uint32_t gx, uint32_t y, uint32_t (&w)[6]) {
+    const uint4 Yq = *reinterpret_cast<const uint4*>(P[0].row(int(y)) + (int(gx) - P[0].c0));
+    int cb[8], cr[8];
+    fancy_row8<MODE>(P[1], gx, y, cb);
+    fancy_row8<MODE>(P[2], gx, y, cr);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {  // filtered samples stay in [-256, 255]: say so, so that
+        cb[j] = int(int16_t(cb[j]));  // chroma_terms' products are 24-bit multiplies
+        cr[j] = int(int16_t(cr[j]));
+    }
+    uint32_t TR[4], TG[4], TB[4], ex = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const ChromaTerms t0 = chroma_terms(cb[2 * u], cr[2 * u]), t1 = chroma_terms(cb[2 * u + 1], cr[2 * u + 1]);
+        ex |= (t0.exact ? 1u : 0u) << (2 * u);
+        ex |= (t1.exact ? 1u : 0u) << (2 * u + 1);
+        TR[u] = pair16(t0.r, t1.r);
+        TG[u] = pair16(t0.g, t1.g);
+        TB[u] = pair16(t0.b, t1.b);
+    }
+    row_rgb_packed(Yq, TR, TG, TB, w);
+    if (__any(ex != 0u)) {
+        const uint32_t Y[4] = {Yq.x, Yq.y, Yq.z, Yq.w};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if ((ex >> j) & 1u) {
+                const int yv = (j & 1) ? int32_t(Y[j >> 1]) >> 16 : int(int16_t(Y[j >> 1] & 0xFFFFu));
+                const int g = color_g_exact(yv, cb[j], cr[j]);
+                const int byte = 3 * j + 1;
+                w[byte >> 2] = (w[byte >> 2] & ~(0xFFu << (8 * (byte & 3)))) | (uint32_t(g) << (8 * (byte & 3)));
+            }
+        }
+    }
+}
+
+// Bands per workgroup (stacked vertically): the next band's window is fetched into registers
+// while the current band is coloured, so a workgroup waits on HBM latency once, not per band.
+constexpr uint32_t kFancyBands = 4;
+constexpr int kFancyQuadsPerThread = 2;  // window quads per thread and component: 18 x 18 <= 512
+static_assert((kFancyRows * (kFancyCols / 8) + kFancyThreads - 1) / kFancyThreads <= kFancyQuadsPerThread,
+              "window quads per thread");
+
+// One instance per sampling layout (the images of b.mode_imgs, as k_idct_color<M>): 4:2:0 is the
+// h2v2 filter, 4:2:2 h2v1, 4:4:4 none (all vectorised, fancy_colour8, with the layout's ratios as
+// compile-time constants); every other layout (h1v2, grayscale, other ratios) takes the per-pixel
+// fancy_win path with ratios from the image descriptor.
+template <int M>
+__global__ __launch_bounds__(kFancyThreads) void k_colour_fancy(BatchDev b) {
+    __shared__ __attribute__((aligned(16))) int16_t s_win[3][kFancyRows * kFancyCols];
+    constexpr bool kFixed = M != kModeGen;
+    constexpr int kFilt = M == kMode420 ? 1 : M == kMode422 ? 2 : 0;
+    constexpr uint32_t kLgRx = (M == kMode420 || M == kMode422) ? 1u : 0u, kLgRy = M == kMode420 ? 1u : 0u;
+    const ImgDesc& im = b.imgs[b.mode_imgs[b.mode_off[M] + blockIdx.z]];
+    const uint32_t W = im.width, H = im.height;
+    const uint32_t x0 = blockIdx.x * kFancyW, yb = blockIdx.y * (kFancyH * kFancyBands);
+    if (x0 >= W || yb >= H) return;  // workgroup-uniform (the grid covers the layout's largest image)
+    const uint32_t t = threadIdx.x, nc = kFixed ? 3u : im.ncomp;
+    FancyWin P[3];
+    const int16_t* src[3];
+    uint32_t pitch[3], prow[3], qpr[3], qmagic[3];
+    {
+        size_t off = 0;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint32_t cc = uint32_t(c) < nc ? uint32_t(c) : 0u;
+            FancyWin& F = P[c];
+            if (kFixed) {  // Y 1x1, chroma 2^kLgRx x 2^kLgRy
+                const uint32_t lx = c ? kLgRx : 0u, ly = c ? kLgRy : 0u;
+                F.rx = 1u << lx;
+                F.ry = 1u << ly;
+                F.cw = (W + F.rx - 1) >> lx;
+                F.ch = (H + F.ry - 1) >> ly;
+                pitch[c] = im.mcux * ((c ? 1u : 1u << kLgRx) * 8);
+                prow[c] = im.mcuy * ((c ? 1u : 1u << kLgRy) * 8);
+            } else {
+                F.rx = im.hmax / im.h[cc];
+                F.ry = im.vmax / im.v[cc];
+                F.cw = (W * im.h[cc] + im.hmax - 1) / im.hmax;
+                F.ch = (H * im.v[cc] + im.vmax - 1) / im.vmax;
+                pitch[c] = im.mcux * im.h[cc] * 8;
+                prow[c] = im.mcuy * im.v[cc] * 8;
+            }
+            const uint32_t xs = kFixed ? (x0 >> (c ? kLgRx : 0u)) : x0 / F.rx;
+            const uint32_t xe = kFixed ? ((x0 + kFancyW - 1) >> (c ? kLgRx : 0u)) : (x0 + kFancyW - 1) / F.rx;
+            const int c0 = max(0, (int(xs) - 1) & ~7);
+            const int c1 = min(int(pitch[c]), int((xe + 9) & ~7u));
+            F.s = s_win[c];
+            F.c0 = c0;
+            F.ncols = c1 - c0;
+            qpr[c] = uint32_t(F.ncols) >> 3;
+            qmagic[c] = (65536u + qpr[c] - 1u) / qpr[c];
+            src[c] = reinterpret_cast<const int16_t*>(im.planes) + off + c0;
+            if (uint32_t(c) < nc) off += size_t(pitch[c]) * prow[c];
+        }
+    }
+    // window rows of a band: the band's sample rows plus the vertical filters' one-row halo
+    auto rows_of = [&](int c, uint32_t y0, int& r0, int& r1) {
+        const int vh = P[c].ry == 2 ? 1 : 0;
+        const uint32_t ys = kFixed ? (y0 >> (c ? kLgRy : 0u)) : y0 / P[c].ry;
+        const uint32_t ye = kFixed ? ((y0 + kFancyH - 1) >> (c ? kLgRy : 0u)) : (y0 + kFancyH - 1) / P[c].ry;
+        r0 = max(0, int(ys) - vh);
+        r1 = min(int(prow[c]) - 1, int(ye) + vh);
+    };
+    u32x4 pf[3][kFancyQuadsPerThread];
+    uint32_t pdst[3][kFancyQuadsPerThread];  // LDS word offset of each fetched quad (~0u: none)
+    auto fetch = [&](uint32_t y0) {  // this thread's quads of every component's window -> registers
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            int r0, r1;
+            rows_of(c, y0, r0, r1);
+            const uint32_t nq = uint32_t(c) < nc ? qpr[c] * uint32_t(r1 - r0 + 1) : 0u;
+#pragma unroll
+            for (int k = 0; k < kFancyQuadsPerThread; k++) {
+                const uint32_t q = t + uint32_t(k) * kFancyThreads;
+                pdst[c][k] = ~0u;
+                if (q < nq) {
+                    const uint32_t rr = __umul24(q, qmagic[c]) >> 16, cq = q - rr * qpr[c];
+                    pf[c][k] = *gptr(reinterpret_cast<const u32x4*>(src[c] + size_t(uint32_t(r0) + rr) * pitch[c] + 8 * cq));
+                    pdst[c][k] = __umul24(rr, kFancyCols) + 8 * cq;
+                }
+            }
+        }
+    };
+    auto put = [&]() {  // registers -> the LDS windows
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+#pragma unroll
+            for (int k = 0; k < kFancyQuadsPerThread; k++)
+                if (pdst[c][k] != ~0u) *reinterpret_cast<u32x4*>(s_win[c] + pdst[c][k]) = pf[c][k];
+    };
+    fetch(yb);
+    put();
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t band = 0; band < kFancyBands; band++) {
+        const uint32_t y0 = yb + band * kFancyH;
+        const bool next = band + 1 < kFancyBands && y0 + kFancyH < H;  // workgroup-uniform
+        if (next) fetch(y0 + kFancyH);  // in flight while this band is coloured
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            int r1;
+            rows_of(c, y0, P[c].r0, r1);
+        }
+        const uint32_t y = y0 + (t >> 4), gx = x0 + ((t & 15u) << 3);
+        if (y < H && gx < W) {
+            uint32_t w[6];
+            if (kFixed) {
+                fancy_colour8<kFilt>(P, gx, y, w);
+            } else {  // grayscale, h1v2, a subsampled Y, or chroma planes with different ratios: per pixel
+                uint32_t rgb[8][3];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t x = min(gx + uint32_t(j), W - 1);
+                    const int yv = fancy_win(P[0], x, y);
+                    if (nc == 1) {
+                        rgb[j][0] = rgb[j][1] = rgb[j][2] = clamp_u8(yv + 128);
+                    } else {
+                        const int cb = fancy_win(P[1], x, y), cr = fancy_win(P[2], x, y);
+                        colour_px(yv, cb, cr, chroma_terms(cb, cr), rgb[j][0], rgb[j][1], rgb[j][2]);
+                    }
+                }
+                pack24(rgb, w);
+            }
+            store24(reinterpret_cast<uint8_t*>(im.rgb) + (size_t(y) * W + gx) * 3, w, min(8u, W - gx));
+        }
+        if (!next) break;
+        __syncthreads();  // every read of this band's windows is done
+        put();
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3088,7 +3301,17 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             hipLaunchKernelGGL(k_idct_color_exact, dim3(1024), dim3(kIdctThreads), 0, s, b);
             break;
         case 10:
-            if (b.fancy && b.max_fancy_wgs) hipLaunchKernelGGL(k_colour_fancy, dim3(b.max_fancy_wgs, b.nimg), dim3(256), 0, s, b);
+            if (b.fancy && b.max_fancy_wgs) {  // one launch per sampling layout present in the batch
+                const dim3 g(b.max_fancy_wgs & 0xFFFFu, b.max_fancy_wgs >> 16, 1);
+                if (b.mode_cnt[kModeGen])
+                    hipLaunchKernelGGL(k_colour_fancy<kModeGen>, dim3(g.x, g.y, b.mode_cnt[kModeGen]), dim3(kFancyThreads), 0, s, b);
+                if (b.mode_cnt[kMode420])
+                    hipLaunchKernelGGL(k_colour_fancy<kMode420>, dim3(g.x, g.y, b.mode_cnt[kMode420]), dim3(kFancyThreads), 0, s, b);
+                if (b.mode_cnt[kMode422])
+                    hipLaunchKernelGGL(k_colour_fancy<kMode422>, dim3(g.x, g.y, b.mode_cnt[kMode422]), dim3(kFancyThreads), 0, s, b);
+                if (b.mode_cnt[kMode444])
+                    hipLaunchKernelGGL(k_colour_fancy<kMode444>, dim3(g.x, g.y, b.mode_cnt[kMode444]), dim3(kFancyThreads), 0, s, b);
+            }
             break;
         default: return hipErrorInvalidValue;
     }

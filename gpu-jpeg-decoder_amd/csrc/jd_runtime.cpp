@@ -178,6 +178,7 @@ struct jd_ctx {
     int64_t spare_pieces = -1;          // spare re-walk regions per image (JD_SPARE_PIECES; -1: default)
     int64_t piece_overlap = -1;         // warm-up bits (JD_PIECE_OVERLAP_BITS; -1: default)
     bool fixed_pieces = false;          // JD_FIXED_PIECES: keep the host's piece size (no k_pieceplan)
+    size_t stage_chunk = size_t(128) << 20;  // host-input H2D chunk (JD_STAGE_CHUNK_MB; 0: one copy per batch)
     jd_stats stats{};
 
     std::vector<ParsedJpeg> parsed;
@@ -595,7 +596,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         }
         uint8_t* const stage = static_cast<uint8_t*>(pd.in_host);
         uint8_t* const dstage = static_cast<uint8_t*>(pd.d_input.p);
-        constexpr size_t kStageChunk = size_t(32) << 20;  // H2D granularity
+        const size_t kStageChunk = ctx->stage_chunk;  // H2D granularity (JD_STAGE_CHUNK_MB)
         for (size_t p0 = 0; p0 < pieces.size();) {
             size_t p1 = p0 + 1;
             while (p1 < pieces.size() && pieces[p1].off + pieces[p1].n - pieces[p0].off <= kStageChunk) p1++;
@@ -651,8 +652,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
                 for (uint32_t c = 0; c < d.ncomp; c++) n += size_t(d.mcux * d.h[c] * 8) * (d.mcuy * d.v[c] * 8) * 2;
                 poff[i] = tot;
                 tot += align_up(n, 256);
-                const uint64_t groups = uint64_t((d.width + 7) / 8) * d.height;
-                max_fancy_wgs = std::max<uint32_t>(max_fancy_wgs, uint32_t((groups + 255) / 256));
+                // k_colour_fancy's grid: 128 x 64-pixel workgroups of four 16-row bands (x in the low
+                // 16 bits, y in the high)
+                max_fancy_wgs = std::max<uint32_t>(max_fancy_wgs & 0xFFFFu, (d.width + 127) / 128) |
+                                (std::max<uint32_t>(max_fancy_wgs >> 16, (d.height + 63) / 64) << 16);
             }
             HIPCHK(ctx, ensure_dev(ctx, pd.d_planes, std::max<size_t>(16, tot)));
             for (size_t i = 0; i < P.imgs.size(); i++)
@@ -981,6 +984,10 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_SPARE_PIECES")) ctx->spare_pieces = std::strtoll(e, nullptr, 0);
     if (const char* e = std::getenv("JD_FIXED_PIECES")) ctx->fixed_pieces = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
+    if (const char* e = std::getenv("JD_STAGE_CHUNK_MB")) {
+        const long long mb = std::strtoll(e, nullptr, 0);
+        ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);
+    }
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return JD_ERR_HIP;

@@ -5,6 +5,12 @@ import sys
 
 import pytest
 
+# PyTorch-ROCm bundles its own libamdhip64.so.7 and libjdamd.so links the system one under the same
+# soname: whichever loads first serves the process.  torch must come first (a torch that finds the
+# system runtime already loaded reports "No HIP GPUs are available"), so the GPU tests that also use
+# torch streams / tensors run in any order and selection.
+import torch  # noqa: E402,F401
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "gpu-jpeg-decoder_amd")
 GOLDEN = os.path.join(ROOT, "tests", "golden")

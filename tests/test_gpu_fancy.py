@@ -32,6 +32,8 @@ def fancy_decoder():
     (1920, 1080, "4:2:0", 1), (333, 217, "4:2:0", 0), (333, 217, "4:2:2", 2), (333, 217, "4:4:0", 0),
     (129, 65, "4:4:4", 0), (17, 9, "4:2:0", 0), (1, 1, "4:2:0", 0), (2, 3, "4:2:0", 0), (9, 3, "4:2:2", 0),
     (3, 9, "4:4:0", 1), (16, 16, "4:2:0", 1), (250, 1, "4:2:2", 0),
+    # k_colour_fancy's 128 x 16 bands: widths and heights just across band and window edges
+    (257, 35, "4:2:0", 0), (130, 33, "4:2:2", 1), (300, 47, "4:4:0", 0), (383, 17, "4:2:0", 2), (128, 16, "4:2:0", 0),
 ])
 def test_fancy_vs_oracle(fancy_decoder, w, h, ss, rows):
     data = jd_synth.encode(jd_synth.synth_pixels(w, h, 5), 90, ss, rows)
