@@ -47,6 +47,9 @@ CONFIGS = {
     "c3": (3840, 2160, "4:2:0", 1, 256, "256 x 3840x2160 4:2:0 q90, DRI = 1 MCU row (BASELINE config 3)"),
     "c5": (1920, 1080, "mixed", 0, 1024, "1024 x 1080p mixed 4:4:4/4:2:2/4:2:0, q in {50,75,90,95}, no RST "
                                          "(BASELINE config 5)"),
+    # config 2 with libjpeg's fancy upsampling (JD_FLAG_FANCY_UPSAMPLING; --fancy on any config)
+    "c2f": (1920, 1080, "4:2:0", 1, 1024, "1024 x 1920x1080 4:2:0 q90, DRI = 1 MCU row, fancy upsampling "
+                                          "(BASELINE config 2 shape, an option beyond the reference)"),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SIMDS = 1024               # 256 CUs x 4 SIMD-32
@@ -451,6 +454,8 @@ def main():
                     help="one blocking jd_decode_batch per step instead of jd_decode_batch_async (which "
                          "parses and plans step k+1 on the host while the GPU decodes step k)")
     args = ap.parse_args()
+    if args.config == "c2f":
+        args.fancy = True
     rc = maybe_launch(args)
     if rc is not None:
         sys.exit(rc)

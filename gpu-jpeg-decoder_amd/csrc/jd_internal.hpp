@@ -57,7 +57,9 @@ JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
 //       bit  7      E2   the second symbol stores a coefficient (tested against zn << 1)
 //       bit  8      P    a second AC symbol follows within the index (pair)
 //       bits 9..13  L1   bits of the first symbol, code + magnitude (<= 31)
-//       bit  15     R    rare: hi holds the 32-bit entry above (0: a code longer than kLutBits);
+//       bit  15     R    rare: hi holds the 32-bit entry above << kRareShift (0: a code longer than
+//                        kLutBits; the shift keeps hi's adv fields 0, so a rare entry the walk does not
+//                        resolve in this iteration leaves the decoder state unchanged);
 //                        codes longer than kLutBits, AC magnitudes of 10 bits or more (they need an
 //                        escaped slot), DC sizes above 11.  lo = R alone (no flags, no pair)
 //       bits 16..31 M1   int16: the coefficient is s - (M1 ^ (s >> 31)) for s = the magnitude bits
@@ -83,6 +85,7 @@ static_assert(sizeof(HuffLut) % 16 == 0, "HuffLut must stay 16-byte aligned");
 constexpr int kLutWords = int(sizeof(HuffLut) / 4);
 constexpr uint32_t kLoDc = 1u << 5, kLoE1 = 1u << 6, kLoE2 = 1u << 7, kLoPair = 1u << 8, kLoRare = 1u << 15;
 constexpr uint32_t kLoL1Shift = 9;
+constexpr uint32_t kRareShift = 12;  // the 20-bit rare entry (lut_entry) sits in hi bits 12..31
 
 // Maximum Huffman tables a table set (one workgroup of the Huffman kernel) stages into LDS.
 constexpr int kSlotsPerSet = 6;

@@ -716,6 +716,18 @@ static_assert(row_words(kWin) % 2 == 1, "row pitch must be odd");
 #define JD_ABL 0
 #endif
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
+// Walk iterations between two executions of the rare-entry branch (a power of two; 1: every
+// iteration).  A rare entry is 0.45 % of lookups on the bench images, but with 64 lanes a quarter
+// of the wave-iterations would take the ~40-instruction branch.
+#ifndef JD_RARE_EVERY
+#define JD_RARE_EVERY 4
+#endif
+constexpr uint32_t kRareEvery = JD_RARE_EVERY;
+#ifndef JD_RARE_COUNT
+#define JD_RARE_COUNT 0  // > 0: also as soon as this many lanes of the wave are stalled on a rare entry
+#endif
+constexpr int kRareCount = JD_RARE_COUNT;
+static_assert((kRareEvery & (kRareEvery - 1u)) == 0u, "kRareEvery: a power of two");
 // items (entries + block records) one window round can add: every item takes >= 2 bits
 constexpr uint32_t kRoundItems = (kWin * 8 + 31) / 2 + 4;
 static_assert(kRegionSlack >= 640 + kRoundItems + 2, "region slack: straddling MCU + one round past the data");
@@ -993,8 +1005,17 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             ent += pr ? (lo & ~(zn2 << 1) & wm2) >> 7 : 0u;
             L += pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : 0u;
             zn = pr ? zn2 : zn;
-            if (lo & kLoRare) {  // codes longer than the index, escaped magnitudes, corrupt codes
-                uint32_t e = hi;
+            // A rare entry consumes nothing in the common path above (L = 0, no emit, no pair,
+            // zn = z): it is resolved in this one-sided branch, taken only every kRareEvery-th
+            // iteration, so the wave pays for the branch once for all the lanes that have met a
+            // rare entry since (they stall in place meanwhile).
+            // (also as soon as every lane still in this window round is stalled: the round would
+            // otherwise idle until the period comes round)
+            const bool rare = (lo & kLoRare) != 0;
+            const bool rare_now = (it & (kRareEvery - 1u)) == kRareEvery - 1u || __ballot(!rare) == 0 ||
+                                  (kRareCount && __popcll(__ballot(rare)) >= kRareCount);  // wave-uniform
+            if (rare && rare_now) {  // codes longer than the index, escaped magnitudes, corrupt codes
+                uint32_t e = hi >> kRareShift;
                 if ((e & 31u) == 0) e = huff_slow(TS::at(tab), peek);
                 const int val = huff_value(peek, e);
                 // EOB / ZRL / run-size (parser.cpp:114-134)
@@ -1029,7 +1050,8 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             esc_blk = fin ? 0u : esc_blk;
             z = fin ? 0u : zn;
             b3 += fin ? 3u : 0u;
-            tab = lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
+            // (a stalled rare lane keeps its table: its symbol, DC or AC, is still ahead)
+            tab = (rare && !rare_now) ? tab : lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
             // MCU end: the common case only counts; the branch is taken at the next threshold
             // (piece start while warm, piece end, data end, checkpoint) or after an error
             const bool mend = b3 == bpm3;

@@ -199,7 +199,7 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
         const uint32_t sz1 = is_dc ? sym1 : (sym1 & 15u);
         if (e1 == 0 || (is_dc ? sz1 > 11u : sz1 >= 10u)) {  // rare: the walks' generic branch
             lo = kLoRare;
-            hi = e1;
+            hi = e1 << kRareShift;  // bits 5..18 clear: the common path's fields read 0 (a no-op)
             continue;
         }
         const uint32_t L1 = l1 + sz1, adv1 = (e1 >> 8) & 127u;
