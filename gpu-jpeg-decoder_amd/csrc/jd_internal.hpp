@@ -133,6 +133,8 @@ struct alignas(16) ImgDesc {
     uint32_t entry_cap;               // AC-entry slots of this image (entry indices are image-relative):
                                       // its pieces' regions, then spare regions for re-walks
     uint64_t entry_base;              // first AC-entry slot of this image in BatchDev::entries
+    uint32_t rw_div;                  // fewest walk bits per region word (jd_plan.cpp region_divisor)
+    uint32_t rsv_[3];
 };
 static_assert(sizeof(ImgDesc) % 16 == 0, "ImgDesc must stay 16-byte aligned");
 
@@ -209,12 +211,16 @@ struct alignas(16) CpRec {
 constexpr uint32_t kNoError = 0xFFFFFFFFu;
 
 // Per-piece output region (image-relative AC-entry slots): AC entries ascend from its start, one
-// 32-bit record per block (AC-entry count << 16 | 16-bit DC difference) descends from its end.  An
-// emitted entry and a block each take at least 2 bits of the walk, so a piece of plen bits fills
-// at most plen / 2 + kRegionSlack words: the MCU that straddles the piece's end (<= 10 blocks x 64)
-// and one window round past the data end (<= 272), see jd_kernels.hip walk_piece.
+// 32-bit record per block (AC-entry count << 16 | 16-bit DC difference) descends from its end.  A
+// block (one word) and an emitted entry (half a word) each take at least a table-dependent number
+// of walk bits (jd_plan.cpp region_divisor: at least 2 for any tables, 4 for the standard Annex K
+// tables), so a piece of plen bits fills at most plen / div + kRegionSlack words: the MCU that
+// straddles the piece's end (<= 10 blocks x 64) and one window round past the data end (<= 272), see
+// jd_kernels.hip walk_piece, whose region guard stops a walk (as an error) before it could overrun.
 constexpr uint32_t kRegionSlack = 1040;
-JD_HD inline uint32_t region_words(uint32_t plen) { return ((plen + 1u) / 2u + kRegionSlack + 3u) & ~3u; }
+JD_HD inline uint32_t region_words(uint32_t plen, uint32_t div = 2u) {
+    return ((plen + div - 1u) / div + kRegionSlack + 3u) & ~3u;
+}
 
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
 #ifndef JD_TILE_BLOCKS

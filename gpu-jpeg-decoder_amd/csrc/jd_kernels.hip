@@ -536,6 +536,7 @@ struct SegInfo {
     uintptr_t last;    // last mapped 16-byte chunk of the image's un-stuffed region
     uint32_t ent0;     // first region word of the interval's pieces (image-relative, k_subplan)
     uint32_t pattern, bpm;
+    uint32_t rw_div;   // the image's region divisor (region_words)
     uint32_t* eimg;    // the image's AC entries (BatchDev::entries + ImgDesc::entry_base)
 };
 
@@ -563,6 +564,7 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
     S.eimg = b.entries + im.entry_base;
     S.pattern = im.block_pattern;
     S.bpm = im.bpm;
+    S.rw_div = im.rw_div;
 }
 
 // Nominal piece length of an interval cut into npc pieces: equal shares of its bits (at most
@@ -578,6 +580,7 @@ __device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
     S.eimg = b.entries;
     S.pattern = 0;
     S.bpm = 1;
+    S.rw_div = 2;
 }
 
 __device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads) {
@@ -664,7 +667,7 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
             const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
             const uint32_t bits = (ce - cs) * 8;
             n = max(1u, uint32_t((uint64_t(bits) + piece_bits - 1) / piece_bits));
-            w = n * region_words((bits + n - 1u) / n);
+            w = n * region_words((bits + n - 1u) / n, im.rw_div);
         }
         const uint32_t incl = wave_incl_scan(n), wincl = wave_incl_scan(w);
         if (k < im.nseg) {
@@ -677,7 +680,7 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
         wrun += __shfl(int(wincl), 63, 64);
     }
     // run <= sub_cap and wrun <= entry_cap by construction (host bounds: ceil(ECS bits /
-    // piece_bits) + nseg pieces, ECS bits / 2 + kRegionSlack + 4 words per piece)
+    // piece_bits) + nseg pieces, ECS bits / rw_div + kRegionSlack + 4 words per piece)
     if (lane == 0) b.img_pool[blockIdx.x] = wrun;
     const uint32_t used = min(run, im.sub_cap);
     // the image's slots: the next `used` of its table set's range (every image's share fits: the
@@ -1162,7 +1165,7 @@ __device__ __forceinline__ PieceGeo piece_geo(const BatchDev& b, const SegInfo& 
     P.j = u - b.seg_sub_base[s];
     P.npc = b.seg_nsub[s];
     P.plen = piece_len(S, P.npc);
-    P.rw = region_words(P.plen);
+    P.rw = region_words(P.plen, S.rw_div);
     P.own = S.ent0 + P.j * P.rw;
     return P;
 }
@@ -2005,14 +2008,40 @@ __device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, i
     out[6] = (x3 - x2) >> 8;
     out[7] = (x7 - y1) >> 8;
 }
-__device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], int (&blk)[64]) {
+// NR: rows 0 .. NR - 1 may hold nonzero coefficients, the rest are zero in every lane of the wave
+// (their row outputs are 0: (0 + 128) >> 8), so their row passes are skipped and the column pass's
+// products with them fold away at compile time.
+// skip7 (wave-uniform): row 7 is zero in every lane, its row pass is skipped at run time.
+template <int NR = 8>
+__device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], int (&blk)[64], bool skip7 = false) {
     int c128;
     asm("v_mov_b32 %0, 0x80" : "=v"(c128));  // one VGPR holding the row pass's rounding term
 #pragma unroll
-    for (int r = 0; r < 8; r++) idct_row_dot2(dw, r, blk + 8 * r, c128);
+    for (int r = 0; r < 8; r++) {
+        if (r < NR && !(r == 7 && skip7)) {
+            idct_row_dot2(dw, r, blk + 8 * r, c128);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++) blk[8 * r + k] = 0;
+        }
+    }
 #pragma unroll
     for (int c = 0; c < 8; c++) idct_col_fast(blk + c);
 }
+// OR of the natural row r's eight zig-zag-ordered int16 coefficients held in the pair words dw.
+template <int R>
+__device__ __forceinline__ uint32_t row_bits(const uint32_t (&dw)[32]) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        const int z = kZzOfNat.v[8 * R + c];
+        acc |= dw[z >> 1] & ((z & 1) ? 0xFFFF0000u : 0x0000FFFFu);
+    }
+    return acc;
+}
+#ifndef JD_IDCT_ZROWS
+#define JD_IDCT_ZROWS 1  // skip the row pass of coefficient row 7 when it is zero across the wave
+#endif
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
 
@@ -2601,7 +2630,13 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         }
         dw[0] = __builtin_amdgcn_perm(dw[0], uint32_t(dq0), 0x07060100u);
 #if !(JD_ABL & 2)
-        idct_block_dot2(dw, blk);
+        if (JD_IDCT_ZROWS) {
+            // row 7 is zero across a whole C2 tile in 96 % of tiles: its row pass is skipped by a
+            // wave-uniform branch (a second copy of the IDCT without it made the kernel spill)
+            idct_block_dot2<8>(dw, blk, __all(!have || row_bits<7>(dw) == 0u));
+        } else {
+            idct_block_dot2(dw, blk);
+        }
 #endif
     } else {
 #pragma unroll

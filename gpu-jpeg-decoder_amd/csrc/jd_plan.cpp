@@ -16,6 +16,52 @@ uint32_t image_mode(const ImgDesc& d) {
     return 0;
 }
 
+// Region words per walk bit, bounded from the image's Huffman tables (any table may meet any block
+// in a speculative walk, so minima run over every component's tables).  A block is one record word
+// plus half a word per emitted entry.  It takes its DC symbol (>= min_dc bits: code + magnitude) and
+// either ends with an EOB (>= min_eob) after E entries (>= mbe bits each: code + >= 1 magnitude bit),
+// or reaches coefficient 63 without one, which takes >= 4 AC symbols (a symbol advances the index
+// by at most 16): E entries and 4 - E other symbols (ZRL and other size-0 codes, >= min_ne).  The
+// words-per-bit ratio of a block shape, (2 + E) / (2 bits), is monotonic in E, so its maximum is at
+// E = 0, at E = 4 or at E -> infinity (1 / (2 mbe)); the divisor is the largest d in [2, 8] with
+// d x ratio <= 1 for all of them (2 holds for any tables: every item takes >= 2 bits).
+uint32_t region_divisor(const ParsedJpeg& pj) {
+#ifdef JD_RW_DIV_FORCE
+    return JD_RW_DIV_FORCE;  // experiment builds: the table-free bound (2) for A/B
+#endif
+    const jd_header& h = pj.hdr;
+    constexpr uint32_t kInf = 1u << 20;
+    uint32_t min_dc = kInf, min_eob = kInf, mbe = kInf, min_ne = kInf;
+    for (int c = 0; c < h.ncomp; c++) {
+        const HuffSpec& dc = pj.dc[pj.td[c]];
+        const HuffSpec& ac = pj.ac[pj.ta[c]];
+        for (int l = 1, k = 0; l <= 16; l++)
+            for (int i = 0; i < dc.counts[l] && k < dc.nvals; i++, k++) min_dc = std::min<uint32_t>(min_dc, uint32_t(l) + dc.vals[k]);
+        for (int l = 1, k = 0; l <= 16; l++)
+            for (int i = 0; i < ac.counts[l] && k < ac.nvals; i++, k++) {
+                const uint32_t sym = ac.vals[k], sz = sym & 15u;
+                if (sym == 0) min_eob = std::min<uint32_t>(min_eob, uint32_t(l));
+                else if (sz) mbe = std::min<uint32_t>(mbe, uint32_t(l) + sz);
+                else min_ne = std::min<uint32_t>(min_ne, uint32_t(l));
+            }
+    }
+    if (min_dc == kInf) return 2u;
+    // candidate block shapes as words-per-bit fractions num / den
+    uint64_t num[8], den[8];
+    int n = 0;
+    if (min_eob < kInf) num[n] = 1, den[n++] = uint64_t(min_dc) + min_eob;
+    if (mbe < kInf) num[n] = 1, den[n++] = 2ull * mbe;
+    for (uint32_t e = 0; e <= 4; e++) {  // no EOB: e entries and 4 - e other symbols
+        if ((e > 0 && mbe == kInf) || (e < 4 && min_ne == kInf)) continue;
+        num[n] = 2 + e;
+        den[n++] = 2ull * (uint64_t(min_dc) + uint64_t(e) * (e ? mbe : 0u) + uint64_t(4 - e) * (e < 4 ? min_ne : 0u));
+    }
+    uint32_t d = 8;
+    for (int i = 0; i < n; i++)
+        while (d > 2 && uint64_t(d) * num[i] > den[i]) d--;
+    return d;
+}
+
 // Fills d (everything but the piece ranges) for item it; pure function of the header + bases.
 void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uint64_t out_addr, const PlanImg& pi,
                ImgDesc& d) {
@@ -78,6 +124,7 @@ void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uin
     d.nchunks = pi.nchunks;  // scan chunks over [align16(file + ecs_off), file + len)
     d.chunk_base = pi.chunk_base;
     d.comp = pi.comp;  // offset for now; rebased onto the pool in launch_batch
+    d.rw_div = region_divisor(pj);
 }
 
 

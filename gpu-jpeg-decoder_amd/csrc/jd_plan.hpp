@@ -25,12 +25,17 @@ uint32_t image_mode(const ImgDesc& d);
 inline uint64_t piece_slots(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits) {
     return (ecs_bytes * 8 + piece_bits - 1) / piece_bits + nseg;
 }
-inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits, int64_t spare_pieces = -1) {
+inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits, int64_t spare_pieces = -1,
+                            uint32_t div = 2u) {
     const uint64_t bits = ecs_bytes * 8, slots = piece_slots(ecs_bytes, nseg, piece_bits);
     uint64_t spare = (piece_bits >= bits) ? 0 : (piece_bits >= 4096 ? slots / 16 + 8 : slots);
     if (spare_pieces >= 0) spare = uint64_t(spare_pieces);  // JD_SPARE_PIECES (tests: in-place re-walks)
-    return bits / 2 + 4 + slots * (kRegionSlack + 8) + spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)));
+    return bits / div + 4 + slots * (kRegionSlack + 8) +
+           spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)), div);
 }
+// Fewest walk bits per region word any block or entry of the image can take, from its Huffman
+// tables (in [2, 8]; 2 holds for any tables): the divisor of its piece regions (region_words).
+uint32_t region_divisor(const ParsedJpeg& pj);
 inline uint32_t image_segments(const jd_header& h) {
     const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
     return h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;

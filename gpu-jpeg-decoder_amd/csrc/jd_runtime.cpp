@@ -188,6 +188,7 @@ struct jd_ctx {
     BatchDev last{};
     uint64_t last_blocks = 0, last_entries = 0;
     std::vector<uint64_t> last_entry_base;  // per image (jd_debug_fetch 20)
+    std::vector<uint32_t> last_rw_div;      // per image (jd_debug_fetch 21)
     uint64_t dev_bytes = 0, dev_peak = 0;   // device pool bytes held now / at most (jd_device_bytes)
 };
 
@@ -324,7 +325,8 @@ int batch_split(jd_ctx* ctx, int lo, int n, const jd_item* items) {
     for (; hi < n; hi++) {
         if (ctx->pst[hi] != JD_OK) continue;
         const jd_header& h = ctx->parsed[hi].hdr;
-        const uint64_t w = entry_words(items[hi].len - h.ecs_offset, image_segments(h), kPieceBits);
+        const uint64_t w = entry_words(items[hi].len - h.ecs_offset, image_segments(h), kPieceBits, -1,
+                                       region_divisor(ctx->parsed[hi]));
         if (hi > lo && cap + w > limit) break;
         cap += w;
     }
@@ -508,7 +510,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             d.sub_base = uint32_t(sub);
             d.sub_cap = uint32_t(piece_slots(d.len - d.ecs_off, d.nseg, P.piece_bits));
             d.entry_base = entry_cursor;
-            d.entry_cap = uint32_t(entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces));
+            d.entry_cap = uint32_t(entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces, d.rw_div));
             entry_cursor += align_up(size_t(d.entry_cap), 4);
             sub += d.sub_cap;
             for (uint32_t k = 0; k < d.nseg; k++) P.chain_seg.push_back(d.seg_base + k);
@@ -787,7 +789,11 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         ctx->last_blocks = P.total_blocks;
         ctx->last_entries = P.total_entry_cap;
         ctx->last_entry_base.resize(P.imgs.size());
-        for (size_t i = 0; i < P.imgs.size(); i++) ctx->last_entry_base[i] = P.imgs[i].entry_base;
+        ctx->last_rw_div.resize(P.imgs.size());
+        for (size_t i = 0; i < P.imgs.size(); i++) {
+            ctx->last_entry_base[i] = P.imgs[i].entry_base;
+            ctx->last_rw_div[i] = P.imgs[i].rw_div;
+        }
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
         const double t_upload = tms();
         rng.reset(new Range("jd_launch"));
@@ -1241,6 +1247,10 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
         case 20:  // per image of the last batch: ImgDesc::entry_base (u64, 32-bit words), host copy
             *nbytes = ctx->last_entry_base.size() * 8;
             if (dst) memcpy(dst, ctx->last_entry_base.data(), std::min(*nbytes, cap));
+            return JD_OK;
+        case 21:  // per image of the last batch: ImgDesc::rw_div (u32), host copy
+            *nbytes = ctx->last_rw_div.size() * 4;
+            if (dst) memcpy(dst, ctx->last_rw_div.data(), std::min(*nbytes, cap));
             return JD_OK;
         default: return JD_ERR_INVALID_ARG;
     }

@@ -393,7 +393,7 @@ class Decoder:
                     "piece_mcu0": (12, np.uint32, 1), "piece_abase": (13, np.uint32, 1),
                     "piece_cp": (14, np.uint32, 36), "stamps": (15, np.uint64, 8), "piece_emcu": (16, np.uint32, 1),
                     "piece_amcu": (17, np.uint32, 1), "piece_join": (18, np.uint32, 1), "seg_ent": (19, np.uint32, 1),
-                    "entry_base": (20, np.uint64, 1)}
+                    "entry_base": (20, np.uint64, 1), "rw_div": (21, np.uint32, 1)}
 
     def debug_fetch(self, name: str) -> np.ndarray:
         """Internal array of the most recent batch (white-box tests and debugging)."""

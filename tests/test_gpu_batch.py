@@ -27,21 +27,22 @@ import jd_synth  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def region_words(plen):
-    """jd_internal.hpp region_words: one piece's AC-entry region in 32-bit words."""
-    return ((plen + 1) // 2 + 1040 + 3) & ~3
+def region_words(plen, div=2):
+    """jd_internal.hpp region_words: one piece's AC-entry region in 32-bit words (div: the image's
+    jd_plan.cpp region_divisor; 4 for the Annex K tables, tests/test_sanitize.py)."""
+    return ((plen + div - 1) // div + 1040 + 3) & ~3
 
 
-def entry_words(data, h, piece_bits=16384, spare=None):
-    """jd_runtime.cpp entry_words: the AC-entry words one image reserves (its pieces' regions and
-    the spare regions of re-walks), from its entropy-coded bytes and restart intervals."""
+def entry_words(data, h, piece_bits=16384, spare=None, div=2):
+    """jd_plan.hpp entry_words: the AC-entry words one image reserves (its pieces' regions and the
+    spare regions of re-walks), from its entropy-coded bytes and restart intervals."""
     bits = (len(data) - h.ecs_offset) * 8
     nmcu = h.mcux * h.mcuy
     nseg = -(-nmcu // h.restart_interval) if h.restart_interval else 1
     slots = -(-bits // piece_bits) + nseg
     if spare is None:
         spare = 0 if piece_bits >= bits else (slots // 16 + 8 if piece_bits >= 4096 else slots)
-    return bits // 2 + 4 + slots * (1040 + 8) + spare * region_words(min(piece_bits, bits))
+    return bits // div + 4 + slots * (1040 + 8) + spare * region_words(min(piece_bits, bits), div)
 
 
 def _device_batch(dec, datas):
@@ -67,12 +68,12 @@ def test_mixed_batch_tail_beyond_2_32_entry_words(monkeypatch):
     """the batch's real entry bases (jd_debug_fetch) put its tail images past 2^32
     32-bit words, so their 64-bit ImgDesc::entry_base and the kernels' image-relative offsets on top
     of it are exercised.  Spare re-walk regions (JD_SPARE_PIECES) pad every image's reservation so
-    that the C5-shaped batch crosses 2^32 words about a third of the way in."""
+    that the C5-shaped batch crosses 2^32 words about half way in."""
     n = 1024
     datas = jd_synth.make_batch(n, 1920, 1080, mixed=True, seed0=500000)
     hdrs0 = [jdamd.parse(d) for d in datas]
-    natural = sum(entry_words(d, h) for d, h in zip(datas, hdrs0))
-    pad = max(0, (3 << 32) // 2 - natural) // n  # total ~1.5 x 2^32 words (~24 GB of entry pool)
+    natural = sum(entry_words(d, h) for d, h in zip(datas, hdrs0))  # an upper bound (divisor 2)
+    pad = max(0, (2 << 32) - natural) // n  # total ~1.6-2 x 2^32 words (~30 GB of entry pool)
     monkeypatch.setenv("JD_SPARE_PIECES", str(pad // region_words(16384) + 16))
     dec = jdamd.Decoder(0)
     try:
@@ -100,7 +101,7 @@ def test_forced_split_host_inputs_and_outputs(monkeypatch):
     pool; each must be collected before the next is launched."""
     datas = jd_synth.make_batch(24, 640, 480, 90, "4:2:0", 1, 0, seed0=7000)
     datas += jd_synth.make_batch(12, 800, 600, 75, "4:4:4", 0, 0, seed0=8000)
-    per = entry_words(datas[0], jdamd.parse(datas[0]))  # batch_split's estimate (full-size pieces)
+    per = entry_words(datas[0], jdamd.parse(datas[0]), div=4)  # batch_split's estimate (Annex K tables)
     monkeypatch.setenv("JD_MAX_BATCH_ENTRIES", str(per * 14))  # ~14 images of the first kind
     dec = jdamd.Decoder(0)
     try:

@@ -51,6 +51,8 @@ def test_intervals_and_piece_starts(sync_decoder, name):
     pab = sync_decoder.debug_fetch("piece_abase")
     pjoin = sync_decoder.debug_fetch("piece_join")
     sent = sync_decoder.debug_fetch("seg_ent")
+    div = int(sync_decoder.debug_fetch("rw_div")[0])  # jd_plan.cpp region_divisor of the image
+    assert 2 <= div <= 8
     errs = []
     for s, seg in enumerate(truth):
         if (int(ce[s]) - int(cs[s])) * 8 != seg["bits"]:
@@ -61,7 +63,7 @@ def test_intervals_and_piece_starts(sync_decoder, name):
             errs.append(f"seg {s}: pieces gpu {nsub[s]} want {want_n}")
             continue
         plen = -(-seg["bits"] // want_n)
-        rw = ((plen + 1) // 2 + 1040 + 3) // 4 * 4  # jd_internal.hpp region_words
+        rw = ((plen + div - 1) // div + 1040 + 3) // 4 * 4  # jd_internal.hpp region_words
         starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
         nm = 0
         for j in range(want_n):

@@ -13,6 +13,7 @@ The reference's only memory checking is a valgrind log of a legacy variant with 
 import os
 import struct
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -22,6 +23,7 @@ from test_abi import _fuzz_corpus, mutate
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "gpu-jpeg-decoder_amd")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 HARNESS = os.path.join(PKG, "fuzz_host_asan")
 
 
@@ -56,8 +58,9 @@ def test_harness_clean_on_golden_corpus(harness, tmp_path):
         assert o[0] == st
         if st == 0:
             assert o[9] == 0, "a valid file must plan"  # plan status
-            mode, tiles_x, tiles_y = o[10:13]
+            mode, tiles_x, tiles_y, rw_div = o[10:14]
             assert tiles_x >= 1 and tiles_y == info.mcuy
+            assert 2 <= rw_div <= 8  # jd_plan.cpp region_divisor
 
 
 def test_parse_and_plan_mutation_fuzz_under_asan_ubsan(harness, tmp_path):
@@ -81,6 +84,21 @@ def test_parse_and_plan_mutation_fuzz_under_asan_ubsan(harness, tmp_path):
             n_ok += 1
             assert o[1:9] == [info.width, info.height, info.ncomp, info.mcux, info.mcuy, info.blocks_per_mcu,
                               info.restart_interval, info.ecs_offset], it
+            if o[9] == 0:
+                assert 2 <= o[13] <= 8
         else:
             n_bad += 1
     assert n_ok > 100 and n_bad > 1000, (n_ok, n_bad)
+
+
+def test_region_divisor_of_standard_tables(harness, tmp_path):
+    """Annex K tables: the densest block shapes are a 2-bit DC code plus a 2-bit chroma EOB (one word
+    in 4 bits) and, for luminance, a 2-bit DC code plus four 3-bit entries reaching coefficient 63
+    without an EOB (3 words in 14 bits), so the piece regions take one word per 4 walk bits (half the
+    table-free bound)."""
+    import jd_synth
+
+    datas = [jd_synth.encode(jd_synth.synth_pixels(64, 48, 1), 90, ss, 0) for ss in ("4:2:0", "4:2:2", "4:4:4")]
+    datas.append(jd_synth.encode(jd_synth.synth_pixels(64, 48, 1, gray=True), 90))
+    out = _run(harness, datas, tmp_path)
+    assert [o[13] for o in out] == [4, 4, 4, 4]

@@ -9,7 +9,7 @@
 //   (the LUT cache, jd_runtime.cpp lut_id), image_fits / entry_words / piece_slots (the AC-entry
 //   reservation) and fill_desc + image_mode (the device descriptor, jd_plan.cpp),
 // and prints one line: parse status, then (status 0) width height ncomp mcux mcuy blocks_per_mcu
-// restart_interval ecs_offset plan mode tiles_x tiles_y.  `plan` is 0, or JD_ERR_CORRUPT for a table
+// restart_interval ecs_offset plan mode tiles_x tiles_y rw_div.  `plan` is 0, or JD_ERR_CORRUPT for a table
 // the LUT builder rejects, or JD_ERR_CAPACITY for an image beyond the 32-bit entry offsets.
 // Any sanitizer finding aborts the process with a non-zero status (-fno-sanitize-recover=all).
 #include <stdio.h>
@@ -76,9 +76,9 @@ int main(int argc, char** argv) {
             ImgDesc d;
             memset(&d, 0, sizeof(d));
             const int plan = plan_one(buf, len, *pj, d);
-            printf("0 %d %d %d %d %d %d %d %llu %d %u %u %u\n", h.width, h.height, h.ncomp, h.mcux, h.mcuy,
+            printf("0 %d %d %d %d %d %d %d %llu %d %u %u %u %u\n", h.width, h.height, h.ncomp, h.mcux, h.mcuy,
                    h.blocks_per_mcu, h.restart_interval, (unsigned long long)h.ecs_offset, plan,
-                   plan ? 0u : image_mode(d), d.tiles_x, d.tiles_y);
+                   plan ? 0u : image_mode(d), d.tiles_x, d.tiles_y, plan ? 0u : d.rw_div);
         }
         delete pj;
         free(buf);
