@@ -5,6 +5,7 @@
 // status D2H.  Device buffers are grow-only pools owned by the context, so steady-state batches do
 // no allocation.  Replaces the reference's per-image extract()/allocate()/clean() cycle
 // (cuda-decoder/benchmark_thoughput/benchmark.cu:49-93) which cudaMalloc'ed every image.
+#include <emmintrin.h>
 #include <hip/hip_runtime_api.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdio.h>
@@ -43,6 +44,26 @@ struct DevBuf {
 
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Host-input staging copy into pinned memory with streaming (non-temporal) stores: the staging
+// buffer is only read again by the H2D DMA, so its lines need not be fetched (no read-for-
+// ownership) nor kept in the caches.  dst is 16-byte aligned (staging offsets are 256-B aligned,
+// pieces 1 MiB apart); the fence makes the stores globally visible before the worker reports done.
+void stage_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    if (i < n) memcpy(dst + i, src + i, n - i);
+    _mm_sfence();
+}
 
 // roctx range over a host phase (parse / plan / launch / collect), visible in rocprofv3
 // --marker-trace next to the kernels; the analogue of the reference's NVTX ranges
@@ -179,6 +200,7 @@ struct jd_ctx {
     int64_t piece_overlap = -1;         // warm-up bits (JD_PIECE_OVERLAP_BITS; -1: default)
     bool fixed_pieces = false;          // JD_FIXED_PIECES: keep the host's piece size (no k_pieceplan)
     size_t stage_chunk = size_t(128) << 20;  // host-input H2D chunk (JD_STAGE_CHUNK_MB; 0: one copy per batch)
+    bool stage_nt = true;                     // streaming-store staging copy (JD_STAGE_NT=0: memcpy)
     jd_stats stats{};
 
     std::vector<ParsedJpeg> parsed;
@@ -604,7 +626,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             while (p1 < pieces.size() && pieces[p1].off + pieces[p1].n - pieces[p0].off <= kStageChunk) p1++;
             ctx->pool->run(int(p1 - p0), [&](int k) {
                 const Piece& q = pieces[p0 + size_t(k)];
-                memcpy(stage + q.off, q.src, q.n);
+                if (ctx->stage_nt) stage_copy(stage + q.off, q.src, q.n);
+                else memcpy(stage + q.off, q.src, q.n);
             });
             const size_t c0 = pieces[p0].off, c1 = (p1 < pieces.size()) ? pieces[p1].off : in_bytes;
             HIPCHK(ctx, hipMemcpyAsync(dstage + c0, stage + c0, c1 - c0, hipMemcpyHostToDevice, s));
@@ -990,6 +1013,7 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_SPARE_PIECES")) ctx->spare_pieces = std::strtoll(e, nullptr, 0);
     if (const char* e = std::getenv("JD_FIXED_PIECES")) ctx->fixed_pieces = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
+    if (const char* e = std::getenv("JD_STAGE_NT")) ctx->stage_nt = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_STAGE_CHUNK_MB")) {
         const long long mb = std::strtoll(e, nullptr, 0);
         ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);

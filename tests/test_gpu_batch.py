@@ -68,13 +68,14 @@ def test_mixed_batch_tail_beyond_2_32_entry_words(monkeypatch):
     """the batch's real entry bases (jd_debug_fetch) put its tail images past 2^32
     32-bit words, so their 64-bit ImgDesc::entry_base and the kernels' image-relative offsets on top
     of it are exercised.  Spare re-walk regions (JD_SPARE_PIECES) pad every image's reservation so
-    that the C5-shaped batch crosses 2^32 words about half way in."""
+    that the C5-shaped batch crosses 2^32 words about a third of the way in."""
     n = 1024
     datas = jd_synth.make_batch(n, 1920, 1080, mixed=True, seed0=500000)
     hdrs0 = [jdamd.parse(d) for d in datas]
-    natural = sum(entry_words(d, h) for d, h in zip(datas, hdrs0))  # an upper bound (divisor 2)
-    pad = max(0, (2 << 32) - natural) // n  # total ~1.6-2 x 2^32 words (~30 GB of entry pool)
-    monkeypatch.setenv("JD_SPARE_PIECES", str(pad // region_words(16384) + 16))
+    # Annex K tables: region divisor 4 (tests/test_sanitize.py)
+    natural = sum(entry_words(d, h, div=4) for d, h in zip(datas, hdrs0))
+    pad = max(0, (3 << 32) // 2 - natural) // n  # total ~1.5 x 2^32 words (~26 GB of entry pool)
+    monkeypatch.setenv("JD_SPARE_PIECES", str(pad // region_words(16384, 4) + 16))
     dec = jdamd.Decoder(0)
     try:
         hosts, hdrs, din, dout, offs, ooffs = _device_batch(dec, datas)
