@@ -3064,7 +3064,13 @@ __device__ __forceinline__ void fancy_colour8(const FancyWin (&P)[3], uint32_t g
 
 // Bands per workgroup (stacked vertically): the next band's window is fetched into registers
 // while the current band is coloured, so a workgroup waits on HBM latency once, not per band.
-constexpr uint32_t kFancyBands = 4;
+#ifndef JD_FANCY_BANDS
+#define JD_FANCY_BANDS 4
+#endif
+#ifndef JD_FANCY_LB
+#define JD_FANCY_LB 1  // minimum waves per SIMD asked of the compiler (register budget)
+#endif
+constexpr uint32_t kFancyBands = JD_FANCY_BANDS;
 constexpr int kFancyQuadsPerThread = 2;  // window quads per thread and component: 18 x 18 <= 512
 static_assert((kFancyRows * (kFancyCols / 8) + kFancyThreads - 1) / kFancyThreads <= kFancyQuadsPerThread,
               "window quads per thread");
@@ -3074,7 +3080,7 @@ static_assert((kFancyRows * (kFancyCols / 8) + kFancyThreads - 1) / kFancyThread
 // compile-time constants); every other layout (h1v2, grayscale, other ratios) takes the per-pixel
 // fancy_win path with ratios from the image descriptor.
 template <int M>
-__global__ __launch_bounds__(kFancyThreads) void k_colour_fancy(BatchDev b) {
+__global__ __launch_bounds__(kFancyThreads, JD_FANCY_LB) void k_colour_fancy(BatchDev b) {
     __shared__ __attribute__((aligned(16))) int16_t s_win[3][kFancyRows * kFancyCols];
     constexpr bool kFixed = M != kModeGen;
     constexpr int kFilt = M == kMode420 ? 1 : M == kMode422 ? 2 : 0;

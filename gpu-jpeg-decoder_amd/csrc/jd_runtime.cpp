@@ -567,6 +567,12 @@ size_t reserve(size_t& end, size_t bytes) {
 
 jd_status finish_batch(jd_ctx* ctx, Pending& pd);
 
+// k_colour_fancy's rows per workgroup (jd_kernels.hip kFancyH x kFancyBands)
+#ifndef JD_FANCY_BANDS
+#define JD_FANCY_BANDS 4
+#endif
+constexpr uint32_t kFancyRowsPerWg = 16u * JD_FANCY_BANDS;
+
 // Grow-only pinned buffer of a pending slot (the slot is idle when this is called).
 hipError_t ensure_pinned(void*& p, size_t& cap, size_t bytes) {
     if (bytes <= cap) return hipSuccess;
@@ -680,7 +686,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
                 // k_colour_fancy's grid: 128 x 64-pixel workgroups of four 16-row bands (x in the low
                 // 16 bits, y in the high)
                 max_fancy_wgs = std::max<uint32_t>(max_fancy_wgs & 0xFFFFu, (d.width + 127) / 128) |
-                                (std::max<uint32_t>(max_fancy_wgs >> 16, (d.height + 63) / 64) << 16);
+                                (std::max<uint32_t>(max_fancy_wgs >> 16, (d.height + kFancyRowsPerWg - 1) / kFancyRowsPerWg) << 16);
             }
             HIPCHK(ctx, ensure_dev(ctx, pd.d_planes, std::max<size_t>(16, tot)));
             for (size_t i = 0; i < P.imgs.size(); i++)
