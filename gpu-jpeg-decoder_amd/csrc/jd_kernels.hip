@@ -26,6 +26,7 @@
 // utils/color.cpp); the restatement used as checker lives in oracle/ (tests only).
 #include <hip/hip_runtime.h>
 #include <mutex>
+#include <type_traits>
 
 #include "jd_kernels.hpp"
 
@@ -755,6 +756,9 @@ size_t piece_lds_bytes(uint32_t max_slots, int nt) {
 constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
 static_assert((kPieceThreads * row_words(kWin) * 4) % 16 == 0, "rings must start 16-byte aligned");
 
+typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return uint32_t(size_t((lds_u32*)p)); }
+
 // Stream reader over a lane's LDS row of big-endian words.  A and B are the words under the read
 // position and s = 32 - (bits of A consumed), 0..31 (s = 0: A is used up, the next symbol starts
 // at B), so the next 32 stream bits are alignbit(A, B, s).  nextw = row[rp] is the word after B,
@@ -783,6 +787,7 @@ struct BitRow {
         nextw = row[rp];
     }
     __device__ __forceinline__ uint32_t bit() const { return uint32_t((rp << 5) + wb - s); }
+    __device__ __forceinline__ bool in_window() const { return rp <= kWin / 4; }
     template <int WIN>
     __device__ __forceinline__ void next_window() {
         rp -= WIN / 4;
@@ -801,11 +806,11 @@ __device__ __forceinline__ u32x4 win_load(uintptr_t a, int q, uintptr_t last) {
 }
 #define JD_ROW_FILL(row, v, q)                                              \
     do {                                                                    \
-        (row)[4 * (q) + 0] = __builtin_bswap32(v.x);                        \
-        (row)[4 * (q) + 1] = __builtin_bswap32(v.y);                        \
+        (row)[4 * (q) + 0] = __builtin_bswap32(v.x);                 \
+        (row)[4 * (q) + 1] = __builtin_bswap32(v.y);                 \
         if ((q) < win_loads(kWin) - 1 || kRowOverlap == 16) {               \
-            (row)[4 * (q) + 2] = __builtin_bswap32(v.z);                    \
-            (row)[4 * (q) + 3] = __builtin_bswap32(v.w);                    \
+            (row)[4 * (q) + 2] = __builtin_bswap32(v.z);             \
+            (row)[4 * (q) + 3] = __builtin_bswap32(v.w);             \
         }                                                                   \
     } while (0)
 
@@ -815,8 +820,6 @@ __device__ __forceinline__ u32x4 win_load(uintptr_t a, int q, uintptr_t last) {
 constexpr uint32_t kLutBytes = sizeof(HuffLut);
 // tab is an LDS address: lut_fast is one v_lshl_add of the index onto it and the LDS read (the
 // empty asm keeps the compiler from re-associating (peek >> 22) << 2 into a shift-and-mask).
-typedef const __attribute__((address_space(3))) uint32_t lds_u32;
-__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return uint32_t(size_t((lds_u32*)p)); }
 __device__ __forceinline__ const uint32_t* lut_at(uint32_t tab) { return (const uint32_t*)(lds_u32*)size_t(tab); }
 typedef const __attribute__((address_space(3))) u32x2 lds_u64;
 __device__ __forceinline__ u32x2 lut_fast(uint32_t tab, uint32_t peek) {
@@ -891,6 +894,9 @@ __device__ __forceinline__ void st_ent(uint4* p, const uint4& v) {
     }
 }
 
+#ifndef JD_DC_BFI
+#define JD_DC_BFI 1
+#endif
 #ifndef JD_PSTAT
 #define JD_PSTAT 0  // diagnostic builds: k_piece walk statistics summed into BatchDev::stamps[0..15]
 #endif
@@ -977,7 +983,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
 #pragma unroll
         for (int q = 0; q < win_loads(kWin); q++) nx[q] = win_load(na, q, S.last);
         uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
-        while (active && R.rp <= kWin / 4) {
+        while (active && R.in_window()) {
             it++;
             const uint32_t peek = R.peek();
             const u32x2 E = TS::fast(tab, peek);
@@ -999,7 +1005,13 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             // bit 6 of lo & ~zn & wm) advances ent
             ring16[ent & 15u] = uint16_t((uint32_t(v1) << 6) | zn);
             ent += (lo & ~zn & wm) >> 6;
-            dcd = (lo & kLoDc) ? v1 : dcd;
+            if (JD_DC_BFI) {  // dcd = DC ? v1 : dcd as one bit-field select on the sign-extended DC
+                              // flag (bit 5); asm: the compiler turns it back into and + cmp + cndmask
+                const int m = __builtin_amdgcn_sbfe(int(lo), 5u, 1u);
+                asm("v_bfi_b32 %0, %1, %2, %0" : "+v"(dcd) : "v"(m), "v"(v1));
+            } else {
+                dcd = (lo & kLoDc) ? v1 : dcd;
+            }
             // the second symbol of a pair, when the first left the block open (its slot goes to
             // the next free position either way; E2 is bit 7 of lo)
             const bool pr = (lo & kLoPair) && zn < 63u;
@@ -3065,7 +3077,7 @@ __device__ __forceinline__ void fancy_colour8(const FancyWin (&P)[3], uint32_t g
 // Bands per workgroup (stacked vertically): the next band's window is fetched into registers
 // while the current band is coloured, so a workgroup waits on HBM latency once, not per band.
 #ifndef JD_FANCY_BANDS
-#define JD_FANCY_BANDS 4
+#define JD_FANCY_BANDS 8
 #endif
 #ifndef JD_FANCY_LB
 #define JD_FANCY_LB 1  // minimum waves per SIMD asked of the compiler (register budget)

@@ -569,7 +569,7 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd);
 
 // k_colour_fancy's rows per workgroup (jd_kernels.hip kFancyH x kFancyBands)
 #ifndef JD_FANCY_BANDS
-#define JD_FANCY_BANDS 4
+#define JD_FANCY_BANDS 8
 #endif
 constexpr uint32_t kFancyRowsPerWg = 16u * JD_FANCY_BANDS;
 
