@@ -862,10 +862,9 @@ __device__ __forceinline__ uint32_t entry16(int v, uint32_t zz, bool big) {
 }
 
 // One piece walk.
-//   kSpec: from `start` (piece_overlap bits before the nominal start, with a guessed state) a
-//          warm-up that only follows the symbols to the first MCU boundary at/after warm_to, the
-//          piece start (warm_to == start: the true state at an MCU boundary, piece 0); then the
-//          writing walk, with a checkpoint at the first MCU boundary after every cp_bits bits.
+//   kSpec: the writing walk from `start`, an MCU boundary (piece 0: bit 0; piece j > 0: where its
+//          warm-up, sync_piece, synchronised), with a checkpoint at the first MCU boundary after
+//          every cp_bits bits.
 //   kRedo: the writing walk from the true MCU boundary `start`; it stops at the first MCU
 //          boundary that is one of the speculative walk's checkpoints (cpb) and joins it.
 // The writing walk stores, per block, one record (count, DC difference) and the AC entries, into
@@ -874,7 +873,7 @@ __device__ __forceinline__ uint32_t entry16(int v, uint32_t zz, bool big) {
 // The chain decides which MCUs count (the last interval's trailing bytes are ignored, as the
 // oracle ignores them).
 struct PWalk {
-    uint32_t start, warm_to, stop_at;
+    uint32_t start, stop_at;
     uint32_t* reg;
     uint32_t rw;
     uint32_t m_start, m_end, mcus, ents, emcu, ncp, join;
@@ -925,25 +924,21 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     uint16_t* const ring16 = reinterpret_cast<uint16_t*>(ring);
     uint32_t z = 0, b3 = 0;
     TabT tab = tab_dc0;
-    bool warm = KIND == kSpec && W.warm_to != W.start;
     bool active = active_in;
-    uint32_t m_start = warm ? kNoPiece : W.start, m_end = W.start;
-    if (!warm && W.start + 8 > sbits) active = false;  // starts at the data end: empty
+    uint32_t m_start = W.start, m_end = W.start;
+    if (W.start + 8 > sbits) active = false;  // starts at the data end: empty
     uint32_t next_cp = W.start + cp_bits, ncp = 0, join = 0;
     // an MCU end at/after end_thr leaves fewer than 8 bits: the data end (padding before RSTn/EOI)
     const uint32_t end_thr = sbits >= 8u ? sbits - 7u : 0u;
-    // the next bit at which an MCU end needs the slow branch: the piece start while warming up,
-    // then the next of piece end, data end, checkpoint (0 after an error)
-    uint32_t thr = W.warm_to;
-    if (!warm) {
-        uint32_t nxt = next_cp;
-        if (KIND == kRedo) {
-            nxt = 0xFFFFFFFFu;
+    // the next bit at which an MCU end needs the slow branch: the next of piece end, data end,
+    // checkpoint (0 after an error)
+    uint32_t nxt0 = next_cp;
+    if (KIND == kRedo) {
+        nxt0 = 0xFFFFFFFFu;
 #pragma unroll
-            for (int c = 0; c < kCpMax; c++) nxt = (cpb[c] > W.start) ? min(nxt, cpb[c]) : nxt;
-        }
-        thr = min(min(W.stop_at, end_thr), nxt);
+        for (int c = 0; c < kCpMax; c++) nxt0 = (cpb[c] > W.start) ? min(nxt0, cpb[c]) : nxt0;
     }
+    uint32_t thr = min(min(W.stop_at, end_thr), nxt0);
     uint32_t mcus = 0, emcu = kNoError, errs = 0;
     uint32_t ent = 0, ent_blk = 0, blk = 0, esc_blk = 0;
     int dcd = 0;
@@ -972,11 +967,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         if (pend_b && (!(JD_ABL & 16) || ent == 0x7FFFFFFFu)) rec_top[-int(pblk)] = prec; \
         pend_b = false;                                                  \
     } while (0)
-    // Warm-up and writing share one symbol loop: while warm, a lane follows the symbols only (its
-    // slot count, block count and MCU count stay 0, errors are ignored) until the first MCU
-    // boundary at/after warm_to, where the piece starts.
-    uint32_t pos = W.start;                          // == R.bit(): the stream bit of the next symbol
-    uint32_t wm = warm ? 0u : 64u, wm2 = wm << 1;    // emit masks: 0 while warm
+    uint32_t pos = W.start;  // == R.bit(): the stream bit of the next symbol
     while (true) {
         const uintptr_t na = wa + kWin;
         u32x4 nx[win_loads(kWin)];
@@ -1001,10 +992,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             const int v1 = s1 - ((int(lo) >> 16) ^ (s1 >> 31));
             uint32_t zn = z + __builtin_amdgcn_ubfe(hi, 5u, 7u);
             uint32_t L = __builtin_amdgcn_ubfe(lo, kLoL1Shift, 5u);
-            // a slot is written for every symbol; a stored coefficient (E1, zn < 64, not warm:
-            // bit 6 of lo & ~zn & wm) advances ent
+            // a slot is written for every symbol; a stored coefficient (E1, zn < 64: bit 6 of
+            // lo & ~zn) advances ent
             ring16[ent & 15u] = uint16_t((uint32_t(v1) << 6) | zn);
-            ent += (lo & ~zn & wm) >> 6;
+            ent += (lo & ~zn & 64u) >> 6;
             if (JD_DC_BFI) {  // dcd = DC ? v1 : dcd as one bit-field select on the sign-extended DC
                               // flag (bit 5); asm: the compiler turns it back into and + cmp + cndmask
                 const int m = __builtin_amdgcn_sbfe(int(lo), 5u, 1u);
@@ -1017,7 +1008,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             const bool pr = (lo & kLoPair) && zn < 63u;
             const uint32_t zn2 = zn + __builtin_amdgcn_ubfe(hi, 12u, 7u);
             ring16[ent & 15u] = uint16_t((uint32_t(int(hi) >> 23) << 6) | zn2);
-            ent += pr ? (lo & ~(zn2 << 1) & wm2) >> 7 : 0u;
+            ent += pr ? (lo & ~(zn2 << 1) & 128u) >> 7 : 0u;
             L += pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : 0u;
             zn = pr ? zn2 : zn;
             // A rare entry consumes nothing in the common path above (L = 0, no emit, no pair,
@@ -1036,7 +1027,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 // EOB / ZRL / run-size (parser.cpp:114-134)
                 zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
                 L = e & 31u;
-                const bool emit = (e & ~zn & wm) != 0;  // kEntEmit is bit 6: zn < 64, not warm
+                const bool emit = (e & ~zn & 64u) != 0;  // kEntEmit is bit 6: zn < 64
                 dcd = (e & kEntDc) ? val : dcd;
                 // the escaped value goes to the next slot unconditionally (a free slot, overwritten
                 // by the next entry unless the value needed it)
@@ -1045,7 +1036,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 ring16[(ent + 1u) & 15u] = uint16_t(val);
                 esc_blk |= (emit && big) ? 1u : 0u;
                 ent += emit ? (big ? 2u : 1u) : 0u;
-                if ((e & kEntBad) && !warm) {  // the next MCU end takes the branch below
+                if (e & kEntBad) {  // the next MCU end takes the branch below
                     errs = 1u;
                     thr = 0u;
                 }
@@ -1055,12 +1046,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             const bool fin = zn >= 63u;
             prec = fin ? block_rec(ent - ent_blk, dcd, esc_blk) : prec;
             pblk = fin ? blk : pblk;
-            pend_b = pend_b || (fin && !warm);
+            pend_b = pend_b || fin;
             if ((it & 1u) == 0u) {
                 JD_FLUSH_Q();
                 JD_FLUSH_B();
             }
-            blk += (fin && !warm) ? 1u : 0u;
+            blk += fin ? 1u : 0u;
             ent_blk = fin ? ent : ent_blk;
             esc_blk = fin ? 0u : esc_blk;
             z = fin ? 0u : zn;
@@ -1068,24 +1059,14 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             // (a stalled rare lane keeps its table: its symbol, DC or AC, is still ahead)
             tab = (rare && !rare_now) ? tab : lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
             // MCU end: the common case only counts; the branch is taken at the next threshold
-            // (piece start while warm, piece end, data end, checkpoint) or after an error
+            // (piece end, data end, checkpoint) or after an error
             const bool mend = b3 == bpm3;
             b3 = mend ? 0u : b3;
             tab = mend ? tab_dc0 : tab;
-            mcus += (mend && !warm) ? 1u : 0u;
+            mcus += mend ? 1u : 0u;
             if (JD_PSTAT) st_mend_w += __any(mend && pos >= thr) ? 1u : 0u;
             if (mend && pos >= thr) {
                 const uint32_t consumed = pos;
-                if (KIND == kSpec && warm) {  // synchronised (or assumed so): the piece starts here
-                    warm = false;
-                    wm = 64u;
-                    wm2 = 128u;
-                    m_start = m_end = consumed;
-                    next_cp = consumed + cp_bits;
-                    thr = min(min(W.stop_at, end_thr), next_cp);
-                    if (consumed + 8 > sbits) active = false;
-                    continue;
-                }
                 if (errs || consumed > sbits) {  // an error in this MCU
                     emcu = min(emcu, mcus - 1u);
                     errs = 0;
@@ -1121,10 +1102,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         JD_FLUSH_B();
         if (active && R.bit() > sbits) {  // past the data
             m_end = R.bit();
-            emcu = min(emcu, warm ? 0u : mcus);
+            emcu = min(emcu, mcus);
             active = false;
         }
-        if (active && !warm && (ent + 1u) / 2u + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
+        if (active && (ent + 1u) / 2u + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
             m_end = R.bit();
             emcu = min(emcu, mcus);
             active = false;
@@ -1159,6 +1140,83 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     }
 }
 
+// Warm-up of a speculative piece (k_piece, before its writing walk): from `start` in the guessed
+// state (first block of an MCU, its DC symbol next) follow the symbols only -- no entries,
+// records, counts or errors -- to the first MCU boundary at/after warm_to, where the piece's
+// writing walk (walk_piece) starts.  The loop is the writing walk's decode without its
+// bookkeeping (about half its instructions); a lane that synchronises early idles until the
+// wave's last one has (the separate loop measured 7 % faster than warming up inside the writing
+// walk, a separate kernel for it slower: its boundary costs the two batches' overlap).
+// Returns that boundary, or kNoPiece with `end` = the bit at which the walk ran past the data.
+__device__ __forceinline__ uint32_t sync_piece(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
+                                               uint32_t* row, uint32_t start, uint32_t warm_to, bool active,
+                                               uint32_t& end) {
+    const uintptr_t a_start = S.data + (start >> 3);
+    uintptr_t wa = a_start & ~uintptr_t(15);
+#pragma unroll
+    for (int q = 0; q < win_loads(kWin); q++) {
+        const u32x4 v = win_load(wa, q, S.last);
+        JD_ROW_FILL(row, v, q);
+    }
+    BitRow R;
+    R.init(row, uint32_t(a_start & 15) * 8 + (start & 7u), start);
+    const uint32_t bpm3 = 3u * S.bpm;
+    const uint32_t lbase = lds_addr(s_lutw);
+    const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
+    uint32_t z = 0, b3 = 0, tab = tab_dc0, pos = start, res = kNoPiece;
+    end = 0;
+    while (true) {
+        const uintptr_t na = wa + kWin;
+        u32x4 nx[win_loads(kWin)];
+#pragma unroll
+        for (int q = 0; q < win_loads(kWin); q++) nx[q] = win_load(na, q, S.last);
+        uint32_t it = 0;
+        while (active && R.in_window()) {
+            it++;
+            const uint32_t peek = R.peek();
+            const u32x2 E = lut_fast(tab, peek);
+            const uint32_t lo = E.x, hi = E.y;
+            uint32_t zn = z + __builtin_amdgcn_ubfe(hi, 5u, 7u);
+            uint32_t L = __builtin_amdgcn_ubfe(lo, kLoL1Shift, 5u);
+            const bool pr = (lo & kLoPair) && zn < 63u;
+            L += pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : 0u;
+            zn = pr ? zn + __builtin_amdgcn_ubfe(hi, 12u, 7u) : zn;
+            // rare entries as in walk_piece: deferred to every kRareEvery-th iteration
+            const bool rare = (lo & kLoRare) != 0;
+            const bool rare_now = (it & (kRareEvery - 1u)) == kRareEvery - 1u || __ballot(!rare) == 0;
+            if (rare && rare_now) {
+                uint32_t e = hi >> kRareShift;
+                if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
+                zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
+                L = e & 31u;
+            }
+            R.skip(L, row);
+            pos += L;
+            const bool fin = zn >= 63u;
+            z = fin ? 0u : zn;
+            b3 += fin ? 3u : 0u;
+            tab = (rare && !rare_now) ? tab : lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
+            const bool mend = b3 == bpm3;
+            b3 = mend ? 0u : b3;
+            tab = mend ? tab_dc0 : tab;
+            if (mend && pos >= warm_to) {
+                res = pos;
+                active = false;
+            }
+        }
+        if (active && R.bit() > S.bits) {  // past the data before a boundary
+            end = R.bit();
+            active = false;
+        }
+        if (__ballot(active) == 0) break;  // wave-uniform
+#pragma unroll
+        for (int q = 0; q < win_loads(kWin); q++) JD_ROW_FILL(row, nx[q], q);
+        R.template next_window<kWin>();
+        wa = na;
+    }
+    return res;
+}
+
 __device__ __forceinline__ void table_slots(const TableSet& ts, const SegInfo& S, uint32_t& dcp, uint32_t& acp) {
     dcp = acp = 0;  // 3-bit table slot per MCU block
     for (uint32_t q = 0; q < S.bpm && q < 10; q++) {
@@ -1185,8 +1243,8 @@ __device__ __forceinline__ uint32_t piece_stop(const PieceGeo& P) {
     return (P.j + 1 == P.npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(P.j + 1) * P.plen, 0xFFFFFFFEu));
 }
 
-// Lane per piece slot: the speculative walk (warm-up, then the writing walk into the piece's own
-// region).  Piece 0 of an interval starts at bit 0 in the true state.
+// Lane per piece slot: the speculative walk -- for a piece j > 0 first the warm-up (sync_piece,
+// every lane of the wave together), then the writing walk into the piece's own region.  Piece 0 of an interval starts at bit 0 in the true state.
 // NT = kPieceThreads, or 64 for batches with few pieces (one small image: a few 512-lane
 // workgroups would leave all but a few CUs idle; 64-lane ones spread the same lanes over 8x as
 // many CUs, each staging its own table copy).
@@ -1214,10 +1272,19 @@ __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
     table_slots(ts, S, dcp, acp);
     PWalk W;
     // piece j > 0 synchronises from piece_overlap bits before its nominal start (from bit 0,
-    // exactly, when that is closer)
+    // exactly, when that is closer) to the first MCU boundary at/after it
     const uint64_t pstart = uint64_t(P.j) * P.plen;
-    W.warm_to = (P.j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
-    W.start = (pstart <= b.piece_overlap) ? 0u : min(uint32_t(pstart - b.piece_overlap), W.warm_to);
+    const uint32_t warm_to = (P.j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
+    W.start = (pstart <= b.piece_overlap) ? 0u : min(uint32_t(pstart - b.piece_overlap), warm_to);
+    bool live = valid;
+    uint32_t sync_end = 0;
+    const bool spec = valid && P.j != 0;
+    const uint32_t m = sync_piece(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp,
+                                  s_rows + threadIdx.x * row_words(kWin), W.start, warm_to, spec, sync_end);
+    if (spec) {
+        live = m != kNoPiece;
+        W.start = live ? m : 0u;
+    }
     W.stop_at = piece_stop(P);
     W.reg = S.eimg + P.own;
     W.rw = P.rw;
@@ -1225,9 +1292,14 @@ __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     const uint32_t none[kCpMax] = {};
     walk_piece<kSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWin),
-                      s_rows + NT * row_words(kWin) + threadIdx.x * kRingWords, valid, W, cp,
+                      s_rows + NT * row_words(kWin) + threadIdx.x * kRingWords, live, W, cp,
                       max(1u, P.plen / kCpMax), none);
     if (!valid) return;
+    if (!live) {  // as a warm-up that runs past the data: no piece, an error at its first MCU
+        W.m_start = kNoPiece;
+        W.m_end = sync_end;
+        W.emcu = 0u;
+    }
     b.piece_bit[u] = (P.j == 0) ? 0u : W.m_start;
     b.piece_end[u] = W.m_end;
     b.piece_nmcu[u] = W.mcus;
@@ -1263,7 +1335,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
     for (int c = 0; c < kCpMax; c++) cpb[c] = (need && uint32_t(c) < ncp) ? cp[c].bit : 0xFFFFFFFFu;
     PWalk W;
     W.stats = nullptr;
-    W.start = W.warm_to = expect;
+    W.start = expect;
     W.stop_at = piece_stop(P);
     W.reg = S.eimg + base;
     W.rw = P.rw;
