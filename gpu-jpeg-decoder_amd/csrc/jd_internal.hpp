@@ -68,7 +68,7 @@ JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
 //   hi  bits 0..4   w1   magnitude bits still to extract (0 when the index resolves the value)
 //       bits 5..11  adv1 advance of z by the first symbol (DC 0, AC run + 1, ZRL 16, EOB 64)
 //       bits 12..18 adv2 the same for the second symbol
-//       bits 19..22 L2   bits of the second symbol (code + magnitude, within the index)
+//       bits 19..22 L12  bits of the pair, L1 + the second symbol's code + magnitude (<= kLutBits)
 //       bits 23..31 v2   int9: its value (|v2| <= 255: its magnitude has at most 8 bits)
 //   Codes longer than kLutBits take the canonical slow path:
 //   lim[l]     : left-justified 16-bit limit; a code has length l iff peek16 < lim[l] (and not

@@ -745,7 +745,7 @@ constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte alig
 constexpr int kRedoThreads = 64;
 static_assert(kPieceThreads % kRedoThreads == 0, "a redo workgroup lies inside one piece workgroup");
 constexpr size_t kRedoLds = size_t(kRedoThreads) * (row_words(kWin) + kRingWords) * 4;
-static_assert((kRedoThreads * row_words(kWin) * 4) % 16 == 0, "redo rings must start 16-byte aligned");
+static_assert((kRedoThreads * row_words(kWin) * 4) % 32 == 0, "redo rings must start 32-byte aligned (ring_put)");
 size_t piece_lds_bytes(uint32_t max_slots, int nt) {
     return size_t(max_slots) * sizeof(HuffLut) + size_t(nt) * (row_words(kWin) + kRingWords) * 4 + JD_EXTRA_LDS;
 }
@@ -754,44 +754,54 @@ size_t piece_lds_bytes(uint32_t max_slots, int nt) {
 #define JD_SMALL_PIECE_LANES 16384
 #endif
 constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
-static_assert((kPieceThreads * row_words(kWin) * 4) % 16 == 0, "rings must start 16-byte aligned");
+static_assert((kPieceThreads * row_words(kWin) * 4) % 32 == 0 && (64 * row_words(kWin) * 4) % 32 == 0 && sizeof(HuffLut) % 32 == 0 && kRingWords == 8,
+              "rings must start 32-byte aligned (ring_put)");
 
 typedef const __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return uint32_t(size_t((lds_u32*)p)); }
 
 // Stream reader over a lane's LDS row of big-endian words.  A and B are the words under the read
 // position and s = 32 - (bits of A consumed), 0..31 (s = 0: A is used up, the next symbol starts
-// at B), so the next 32 stream bits are alignbit(A, B, s).  nextw = row[rp] is the word after B,
-// read one symbol ahead; wb places row[0] in the interval: bit of the next symbol =
-// rp * 32 + wb - s.  A symbol advances the reader by at most 31 bits, so by at most one word.
+// at B), so the next 32 stream bits are alignbit(A, B, s).  nextw is the word after B, read one
+// symbol ahead from rp, its LDS byte address; wb places the row in the interval: bit of the next
+// symbol = rp * 8 + wb - s.  A symbol advances the reader by at most 31 bits, so by at most one
+// word.  skip() takes the word step from the sign of s - L alone: v_bfi selects with it as the
+// mask and rp moves by -4 x it (one v_mad_i32_i24), no compare.
+__device__ __forceinline__ uint32_t bfi_sel(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b, m = 0 / ~0
+    uint32_t r = b;
+    asm("v_bfi_b32 %0, %1, %2, %0" : "+v"(r) : "v"(m), "v"(a));
+    return r;
+}
 struct BitRow {
-    uint32_t A, B, nextw;
-    int s, rp, wb;
+    uint32_t A, B, nextw, rp, lim, wb;
+    int s;
     __device__ __forceinline__ void init(const uint32_t* row, uint32_t off, uint32_t start) {
-        const uint32_t w0 = off >> 5, o = off & 31u;
+        const uint32_t w0 = off >> 5, o = off & 31u, base = lds_addr(row);
         A = o ? row[w0] : 0u;
         B = row[w0 + (o ? 1u : 0u)];
-        rp = int(w0 + (o ? 2u : 1u));
-        nextw = row[rp];
+        const uint32_t r = w0 + (o ? 2u : 1u);
+        nextw = row[r];
+        rp = base + 4u * r;
+        lim = base + uint32_t(kWin);  // the window's last refill word: kWin / 4
         s = int((32u - o) & 31u);
-        wb = int(start) - int(off) - 32;
+        wb = start - off - 32u - 8u * base;  // modulo 2^32
     }
     __device__ __forceinline__ uint32_t peek() const { return __builtin_amdgcn_alignbit(A, B, uint32_t(s)); }
-    __device__ __forceinline__ void skip(uint32_t L, const uint32_t* row) {
+    __device__ __forceinline__ void skip(uint32_t L) {
         s -= int(L);
-        const bool need = s < 0;
-        s &= 31;  // s + 32 when negative (L <= 31)
-        A = need ? B : A;
-        B = need ? nextw : B;
-        rp += need ? 1 : 0;
-        nextw = row[rp];
+        const int m = s >> 31;  // ~0: B becomes A (L <= 31)
+        s &= 31;                // s + 32 when negative
+        A = bfi_sel(uint32_t(m), B, A);
+        B = bfi_sel(uint32_t(m), nextw, B);
+        asm("v_mad_i32_i24 %0, %1, -4, %0" : "+v"(rp) : "v"(m));  // rp += 4 when m = ~0
+        nextw = *(const __attribute__((address_space(3))) uint32_t*)size_t(rp);
     }
-    __device__ __forceinline__ uint32_t bit() const { return uint32_t((rp << 5) + wb - s); }
-    __device__ __forceinline__ bool in_window() const { return rp <= kWin / 4; }
+    __device__ __forceinline__ uint32_t bit() const { return rp * 8u + wb - uint32_t(s); }
+    __device__ __forceinline__ bool in_window() const { return rp <= lim; }
     template <int WIN>
     __device__ __forceinline__ void next_window() {
-        rp -= WIN / 4;
-        wb += WIN * 8;
+        rp -= uint32_t(WIN);
+        wb += uint32_t(WIN * 8);
     }
 };
 
@@ -850,9 +860,22 @@ struct TabSpace<true> {
 };
 
 // Block record in a piece's region: escape flag << 23 | AC-entry slot count (<= 126) << 16 | the
-// 16-bit DC difference (a DC size is <= 15 bits, jd_internal.hpp lut_entry).
-__device__ __forceinline__ uint32_t block_rec(uint32_t cnt, int dc, uint32_t esc) {
-    return (esc ? (1u << 23) : 0u) | (min(cnt, 127u) << 16) | (uint32_t(dc) & 0xFFFFu);
+// 16-bit DC difference (a DC size is <= 15 bits, jd_internal.hpp lut_entry).  esc: 0 or 1 << 23;
+// cnt2 = 2 x the slot count.  A block stores at most 63 coefficients (each at a zig-zag index
+// < 64, strictly increasing), of at most two slots each, so the count fits its 7 bits.
+__device__ __forceinline__ uint32_t block_rec(uint32_t cnt2, int dc, uint32_t esc) {
+    return ((cnt2 << 15) | esc) | (uint32_t(dc) & 0xFFFFu);
+}
+// A 16-bit slot into a lane's ring of 16 (ringb 32-byte aligned, ent2 = 2 x the slot count).
+__device__ __forceinline__ void ring_put(uint32_t ringb, uint32_t ent2, uint32_t v) {
+    *(__attribute__((address_space(3))) uint16_t*)size_t(ringb | (ent2 & 30u)) = uint16_t(v);
+}
+// Whether x != 0 in every lane of the wave that is executing this: one v_cmp into an SGPR pair,
+// compared with exec (a ballot of a bool re-derives the compare; asm keeps it one instruction).
+__device__ __forceinline__ bool all_lanes_nz(uint32_t x) {
+    uint64_t m;
+    asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(m) : "v"(x));
+    return m == __builtin_amdgcn_read_exec();
 }
 // A 16-bit AC entry: value << 6 | zig-zag index for |value| <= 511; else an escape (0x8000 | zz)
 // followed by the value itself (jd_internal.hpp).
@@ -921,7 +944,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     const TabT tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
     uint32_t* const reg = W.reg;
     uint32_t* const rec_top = W.reg + (W.rw - 1u);  // block record k at rec_top[-k]
-    uint16_t* const ring16 = reinterpret_cast<uint16_t*>(ring);
+    const uint32_t ringb = lds_addr(ring);  // 32-byte aligned: slot address = ringb | (ent2 & 30)
     uint32_t z = 0, b3 = 0;
     TabT tab = tab_dc0;
     bool active = active_in;
@@ -940,14 +963,15 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     }
     uint32_t thr = min(min(W.stop_at, end_thr), nxt0);
     uint32_t mcus = 0, emcu = kNoError, errs = 0;
-    uint32_t ent = 0, ent_blk = 0, blk = 0, esc_blk = 0;
+    // ent2 / ent_blk2: 2 x the slot counts (the ring's byte offsets); esc_blk: the record's escape bit
+    uint32_t ent2 = 0, ent_blk2 = 0, blk = 0, esc_blk = 0;
     int dcd = 0;
     // AC entries are 16-bit slots (an escaped value takes two).  Stores are deferred and issued
     // every other loop iteration, so that one store instruction carries many lanes.  An iteration
     // emits at most two slots (a pair of AC symbols, or one escaped value: pairs never escape), and
     // a block takes at least two iterations (its DC symbol never pairs), so flushing one quad (8
     // slots) and one block record every two iterations keeps fewer than 16 slots pending: one ring
-    // of two quads and one pending record suffice.  Slots go to the ring at ent & 15 (a symbol that emits nothing
+    // of two quads and one pending record suffice.  Slots go to the ring at slot ent & 15 (a symbol that emits nothing
     // writes the next free slot without advancing, so it is overwritten); a flush stores the
     // completed quad fq straight from the ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
@@ -956,15 +980,15 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     bool pend_b = false;
 #define JD_FLUSH_Q()                                                                                   \
     do {                                                                                               \
-        if (fq < (ent >> 3)) {                                                                         \
-            if (!(JD_ABL & 8) || ent == 0x7FFFFFFFu)                                                   \
+        if (fq < (ent2 >> 4)) {                                                                        \
+            if (!(JD_ABL & 8) || ent2 == 0x7FFFFFFFu)                                                  \
                 st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u))); \
             fq++;                                                                                      \
         }                                                                                              \
     } while (0)
 #define JD_FLUSH_B()                                                     \
     do {                                                                 \
-        if (pend_b && (!(JD_ABL & 16) || ent == 0x7FFFFFFFu)) rec_top[-int(pblk)] = prec; \
+        if (pend_b && (!(JD_ABL & 16) || ent2 == 0x7FFFFFFFu)) rec_top[-int(pblk)] = prec; \
         pend_b = false;                                                  \
     } while (0)
     uint32_t pos = W.start;  // == R.bit(): the stream bit of the next symbol
@@ -994,8 +1018,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             uint32_t L = __builtin_amdgcn_ubfe(lo, kLoL1Shift, 5u);
             // a slot is written for every symbol; a stored coefficient (E1, zn < 64: bit 6 of
             // lo & ~zn) advances ent
-            ring16[ent & 15u] = uint16_t((uint32_t(v1) << 6) | zn);
-            ent += (lo & ~zn & 64u) >> 6;
+            ring_put(ringb, ent2, (uint32_t(v1) << 6) | zn);
+            uint32_t e1 = __builtin_amdgcn_ubfe(lo & ~zn, 6u, 1u);
+            asm("" : "+v"(e1));  // keeps bfe + lshl_add (not lshr + and + add)
+            ent2 += e1 << 1;
             if (JD_DC_BFI) {  // dcd = DC ? v1 : dcd as one bit-field select on the sign-extended DC
                               // flag (bit 5); asm: the compiler turns it back into and + cmp + cndmask
                 const int m = __builtin_amdgcn_sbfe(int(lo), 5u, 1u);
@@ -1004,12 +1030,15 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 dcd = (lo & kLoDc) ? v1 : dcd;
             }
             // the second symbol of a pair, when the first left the block open (its slot goes to
-            // the next free position either way; E2 is bit 7 of lo)
+            // the next free position either way).  It stores a coefficient iff E2 (bit 7 of lo,
+            // pairs only) and zn2 < 64: a first symbol that closed the block (zn >= 63, never EOB:
+            // EOB does not pair) leaves zn2 >= 64, so the test needs no `pr`.  hi[19:22] is the
+            // pair's total length L1 + L2.
             const bool pr = (lo & kLoPair) && zn < 63u;
             const uint32_t zn2 = zn + __builtin_amdgcn_ubfe(hi, 12u, 7u);
-            ring16[ent & 15u] = uint16_t((uint32_t(int(hi) >> 23) << 6) | zn2);
-            ent += pr ? (lo & ~(zn2 << 1) & 128u) >> 7 : 0u;
-            L += pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : 0u;
+            ring_put(ringb, ent2, (uint32_t(int(hi) >> 23) << 6) | zn2);
+            ent2 += ((lo & kLoE2) && zn2 < 64u) ? 2u : 0u;
+            L = pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : L;
             zn = pr ? zn2 : zn;
             // A rare entry consumes nothing in the common path above (L = 0, no emit, no pair,
             // zn = z): it is resolved in this one-sided branch, taken only every kRareEvery-th
@@ -1017,9 +1046,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             // rare entry since (they stall in place meanwhile).
             // (also as soon as every lane still in this window round is stalled: the round would
             // otherwise idle until the period comes round)
-            const bool rare = (lo & kLoRare) != 0;
-            const bool rare_now = (it & (kRareEvery - 1u)) == kRareEvery - 1u || __ballot(!rare) == 0 ||
-                                  (kRareCount && __popcll(__ballot(rare)) >= kRareCount);  // wave-uniform
+            uint32_t rl = lo & kLoRare;
+            asm("" : "+v"(rl));  // one v_and for both compares
+            const bool rare = rl != 0;
+            // (| of ints, not ||: the asm compare stays unconditional, in the loop's block)
+            const bool rare_now = (int((it & (kRareEvery - 1u)) == kRareEvery - 1u) | int(all_lanes_nz(rl)) |
+                                   int(kRareCount && __popcll(__ballot(rare)) >= kRareCount)) != 0;  // wave-uniform
             if (rare && rare_now) {  // codes longer than the index, escaped magnitudes, corrupt codes
                 uint32_t e = hi >> kRareShift;
                 if ((e & 31u) == 0) e = huff_slow(TS::at(tab), peek);
@@ -1032,19 +1064,19 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 // the escaped value goes to the next slot unconditionally (a free slot, overwritten
                 // by the next entry unless the value needed it)
                 const bool big = entry_big(val);
-                ring16[ent & 15u] = uint16_t(entry16(val, zn, big));
-                ring16[(ent + 1u) & 15u] = uint16_t(val);
-                esc_blk |= (emit && big) ? 1u : 0u;
-                ent += emit ? (big ? 2u : 1u) : 0u;
+                ring_put(ringb, ent2, entry16(val, zn, big));
+                ring_put(ringb, ent2 + 2u, uint32_t(val));
+                esc_blk |= (emit && big) ? (1u << 23) : 0u;
+                ent2 += emit ? (big ? 4u : 2u) : 0u;
                 if (e & kEntBad) {  // the next MCU end takes the branch below
                     errs = 1u;
                     thr = 0u;
                 }
             }
-            R.skip(L, row);
+            R.skip(L);
             pos += L;
             const bool fin = zn >= 63u;
-            prec = fin ? block_rec(ent - ent_blk, dcd, esc_blk) : prec;
+            prec = fin ? block_rec(ent2 - ent_blk2, dcd, esc_blk) : prec;
             pblk = fin ? blk : pblk;
             pend_b = pend_b || fin;
             if ((it & 1u) == 0u) {
@@ -1052,7 +1084,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 JD_FLUSH_B();
             }
             blk += fin ? 1u : 0u;
-            ent_blk = fin ? ent : ent_blk;
+            ent_blk2 = fin ? ent2 : ent_blk2;
             esc_blk = fin ? 0u : esc_blk;
             z = fin ? 0u : zn;
             b3 += fin ? 3u : 0u;
@@ -1077,7 +1109,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                     active = false;
                 } else if (KIND == kSpec) {
                     if (consumed >= next_cp && ncp < uint32_t(kCpMax)) {
-                        cp[ncp] = CpRec{consumed, mcus, ent, 0u};
+                        cp[ncp] = CpRec{consumed, mcus, ent2 >> 1, 0u};
                         ncp++;
                         next_cp = (ncp < uint32_t(kCpMax)) ? consumed + cp_bits : 0xFFFFFFFFu;
                     }
@@ -1105,7 +1137,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             emcu = min(emcu, mcus);
             active = false;
         }
-        if (active && (ent + 1u) / 2u + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
+        if (active && (ent2 + 2u) / 4u + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
             m_end = R.bit();
             emcu = min(emcu, mcus);
             active = false;
@@ -1123,12 +1155,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     }
 #undef JD_FLUSH_Q
 #undef JD_FLUSH_B
-    if (ent & 7u)  // the last, partial quad (every complete one is stored; the region has room for all of it)
+    if (ent2 & 15u)  // the last, partial quad (every complete one is stored; the region has room for all of it)
         st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)));
     W.m_start = m_start;
     W.m_end = m_end;
     W.mcus = mcus;
-    W.ents = ent;
+    W.ents = ent2 >> 1;
     W.emcu = emcu;
     W.ncp = ncp;
     W.join = join;
@@ -1179,18 +1211,20 @@ __device__ __forceinline__ uint32_t sync_piece(const SegInfo& S, const uint32_t*
             uint32_t zn = z + __builtin_amdgcn_ubfe(hi, 5u, 7u);
             uint32_t L = __builtin_amdgcn_ubfe(lo, kLoL1Shift, 5u);
             const bool pr = (lo & kLoPair) && zn < 63u;
-            L += pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : 0u;
+            L = pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : L;  // the pair's L1 + L2
             zn = pr ? zn + __builtin_amdgcn_ubfe(hi, 12u, 7u) : zn;
             // rare entries as in walk_piece: deferred to every kRareEvery-th iteration
-            const bool rare = (lo & kLoRare) != 0;
-            const bool rare_now = (it & (kRareEvery - 1u)) == kRareEvery - 1u || __ballot(!rare) == 0;
+            uint32_t rl = lo & kLoRare;
+            asm("" : "+v"(rl));
+            const bool rare = rl != 0;
+            const bool rare_now = (int((it & (kRareEvery - 1u)) == kRareEvery - 1u) | int(all_lanes_nz(rl))) != 0;
             if (rare && rare_now) {
                 uint32_t e = hi >> kRareShift;
                 if ((e & 31u) == 0) e = huff_slow(lut_at(tab), peek);
                 zn = z + __builtin_amdgcn_ubfe(e, 8u, 7u);
                 L = e & 31u;
             }
-            R.skip(L, row);
+            R.skip(L);
             pos += L;
             const bool fin = zn >= 63u;
             z = fin ? 0u : zn;
@@ -1250,7 +1284,7 @@ __device__ __forceinline__ uint32_t piece_stop(const PieceGeo& P) {
 // many CUs, each staging its own table copy).
 template <int NT>
 __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * NT) / kPieceThreads]];
@@ -1366,7 +1400,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
 // round keeps its end when it joins its speculative walk, and otherwise k_chain notices.
 __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
     JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];  // the lanes' rows and rings only
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
     const uint32_t u = blockIdx.x * kRedoThreads + threadIdx.x;
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
@@ -1517,7 +1551,7 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
 // LDS under the other batch's k_idct_color (1.1 ms instead of 0.02 in a kernel trace).
 __global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
     JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];  // the lanes' rows and rings only
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
     const uint32_t li = blockIdx.x * kRedoThreads + threadIdx.x;
     uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;

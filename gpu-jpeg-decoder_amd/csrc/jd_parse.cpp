@@ -223,7 +223,7 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
         const uint32_t adv2 = sym2 == 0u ? 64u : (sym2 >> 4) + 1u;
         const int v2 = value_at(idx, L1 + l2, sz2);
         lo |= kLoPair | (sz2 ? kLoE2 : 0u);
-        hi |= (adv2 << 12) | (L2 << 19) | ((uint32_t(v2) & 511u) << 23);
+        hi |= (adv2 << 12) | ((L1 + L2) << 19) | ((uint32_t(v2) & 511u) << 23);  // the pair's length
     }
     return true;
 }
