@@ -824,6 +824,36 @@ __device__ __forceinline__ u32x4 win_load(uintptr_t a, int q, uintptr_t last) {
         }                                                                   \
     } while (0)
 
+// The next G windows of a lane's stream (G * kWin bytes + the row overlap), loaded together once
+// every G window rounds and copied into the LDS row one window per round.  A lane's 128-byte line
+// is then fetched in one go instead of once per 32-byte round: with ~32 K lanes per XCD streaming
+// their own pieces, a line read round by round is often evicted from L2 between two rounds.
+#ifndef JD_WIN_GROUP
+#define JD_WIN_GROUP 4
+#endif
+constexpr int kWinGroup = JD_WIN_GROUP;
+static_assert(kWin == 32 && kRowOverlap == 8, "WinGroup assumes 32-byte windows with an 8-byte overlap");
+template <int G>
+struct WinGroup {
+    u32x4 v[2 * G + 1];
+    __device__ __forceinline__ void load(uintptr_t a, uintptr_t last) {
+#pragma unroll
+        for (int q = 0; q < 2 * G; q++) v[q] = load16(a + 16 * q, last);
+        const uintptr_t c = a + 32 * G;
+        const u32x2 t = *reinterpret_cast<const __attribute__((address_space(1))) u32x2*>(c < last ? c : last);
+        v[2 * G] = u32x4{t.x, t.y, 0u, 0u};
+    }
+    // the group's next window into the row, then the rest moves down one window (constant register
+    // indices throughout: a window index would put the group in scratch memory)
+    __device__ __forceinline__ void fill_next(uint32_t* row) {
+        JD_ROW_FILL(row, v[0], 0);
+        JD_ROW_FILL(row, v[1], 1);
+        JD_ROW_FILL(row, v[2], 2);
+#pragma unroll
+        for (int q = 0; q + 2 < 2 * G + 1; q++) v[q] = v[q + 2];
+    }
+};
+
 // Decoder state per symbol: z = coefficient index of the last symbol (DC: 0), b3 = 3 x block
 // within the MCU, tab = LDS byte offset of the next symbol's table (DC table of the block after a
 // block ends, else the block's AC table).
@@ -992,11 +1022,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         pend_b = false;                                                  \
     } while (0)
     uint32_t pos = W.start;  // == R.bit(): the stream bit of the next symbol
+    // (re-walks are short and run few lanes: one window ahead keeps their registers down)
+    constexpr int kGroup = KIND == kSpec ? kWinGroup : 1;
+    WinGroup<kGroup> nx;
+    uint32_t gi = 0;  // window round within the group, wave-uniform
     while (true) {
-        const uintptr_t na = wa + kWin;
-        u32x4 nx[win_loads(kWin)];
-#pragma unroll
-        for (int q = 0; q < win_loads(kWin); q++) nx[q] = win_load(na, q, S.last);
+        if (gi == 0) nx.load(wa + kWin, S.last);
         uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
         while (active && R.in_window()) {
             it++;
@@ -1148,10 +1179,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             st_rounds++;
         }
         if (__ballot(active) == 0) break;  // wave-uniform
-#pragma unroll
-        for (int q = 0; q < win_loads(kWin); q++) JD_ROW_FILL(row, nx[q], q);
+        nx.fill_next(row);
+        gi = __builtin_amdgcn_readfirstlane(gi + 1u == uint32_t(kGroup) ? 0u : gi + 1u);
         R.template next_window<kWin>();
-        wa = na;
+        wa += kWin;
     }
 #undef JD_FLUSH_Q
 #undef JD_FLUSH_B
@@ -1197,11 +1228,10 @@ __device__ __forceinline__ uint32_t sync_piece(const SegInfo& S, const uint32_t*
     const uint32_t tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
     uint32_t z = 0, b3 = 0, tab = tab_dc0, pos = start, res = kNoPiece;
     end = 0;
+    WinGroup<kWinGroup> nx;
+    uint32_t gi = 0;  // window round within the group, wave-uniform
     while (true) {
-        const uintptr_t na = wa + kWin;
-        u32x4 nx[win_loads(kWin)];
-#pragma unroll
-        for (int q = 0; q < win_loads(kWin); q++) nx[q] = win_load(na, q, S.last);
+        if (gi == 0) nx.load(wa + kWin, S.last);
         uint32_t it = 0;
         while (active && R.in_window()) {
             it++;
@@ -1243,10 +1273,10 @@ __device__ __forceinline__ uint32_t sync_piece(const SegInfo& S, const uint32_t*
             active = false;
         }
         if (__ballot(active) == 0) break;  // wave-uniform
-#pragma unroll
-        for (int q = 0; q < win_loads(kWin); q++) JD_ROW_FILL(row, nx[q], q);
+        nx.fill_next(row);
+        gi = __builtin_amdgcn_readfirstlane(gi + 1u == uint32_t(kWinGroup) ? 0u : gi + 1u);
         R.template next_window<kWin>();
-        wa = na;
+        wa += kWin;
     }
     return res;
 }
