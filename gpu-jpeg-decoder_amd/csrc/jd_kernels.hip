@@ -2217,17 +2217,25 @@ struct ChromaTerms {
 // below 2^31).  G's quotient by a multiply-high on n offset to [0, 2^29) (below), its remainder
 // exact in integers.  Equal to the integer definitions above for every (cb, cr) in [-256, 255]^2
 // (tests/test_oracle.py::test_chroma_terms_exhaustive, and the GPU's all-2^27 test_color_exhaustive).
+// a * k + c as one v_mad_i32_i24 whatever the compiler knows of a's range (k in an SGPR: the
+// compiler otherwise falls back to v_mul_lo_u32 / v_mad_u64_u32 for values whose 24-bit range it
+// lost across basic blocks, e.g. the filtered chroma of k_colour_fancy).  |a| < 2^23.
+__device__ __forceinline__ int mad24(int a, int k, int c) {
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
+    return r;
+}
 __device__ __forceinline__ ChromaTerms chroma_terms(int cb, int cr) {
     ChromaTerms t;
-    t.r = (__mul24(cr, 91881) + (128 << 16)) >> 16;
-    t.b = (__mul24(cb, 58065) + (128 << 15) + 32) >> 15;
+    t.r = mad24(cr, 91881, 128 << 16) >> 16;
+    t.b = mad24(cb, 58065, (128 << 15) + 32) >> 15;
     // n' = n + 271 * 587000 is in [0, 2^29): floor(n' / 587000) = mulhi(n', M) >> 19 with
     // M = ceil(2^51 / 587000) for every n' of the domain (checked exhaustively), two integer
     // instructions instead of the float convert / multiply / floor / convert
     constexpr int kOff = 271 * 587000;
-    const uint32_t np = uint32_t(__mul24(cb, 202008) + __mul24(cr, 419198) + kOff);
+    const uint32_t np = uint32_t(mad24(cb, 202008, mad24(cr, 419198, kOff)));
     const uint32_t qp = __umulhi(np, 3836115526u) >> 19;  // q + 271
-    const int rem = int(np) - __mul24(int(qp), 587000);
+    const int rem = mad24(int(qp), -587000, int(np));
     const bool nz = np != uint32_t(kOff);
     t.exact = nz && (rem < 64 || rem > 587000 - 64);
     t.g = nz ? 127 + 271 - int(qp) : 128;
@@ -2306,6 +2314,11 @@ __device__ __forceinline__ void pack24(const uint32_t (&rgb)[8][3], uint32_t (&w
     }
 }
 
+// Pixel (x, y) of an RGB image of row pitch W3 = 3 W bytes: one 32 x 32 -> 64-bit multiply-add for
+// the row (the form (size_t(y) * W + x) * 3 costs three of them), x * 3 as a 24-bit multiply.
+__device__ __forceinline__ uint8_t* rgb_at(uint8_t* out, uint32_t y, uint32_t W3, uint32_t x) {
+    return out + size_t(y) * W3 + __umul24(x, 3u);
+}
 // n <= 8 pixels (24 bytes when n == 8) of a row: 8-byte stores when aligned, else words/bytes
 __device__ __forceinline__ void store24(uint8_t* dst, const uint32_t (&w)[6], uint32_t n) {
     const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
@@ -2868,7 +2881,7 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
     const uint32_t lg_mw = TM_::lg_mw(im), lg_mh = TM_::lg_mh(im);
     const uint32_t gpr = (TM << lg_mw) >> 3;  // 8-pixel groups per tile row
     const uint32_t th = 1u << lg_mh;
-    const uint32_t W = im.width, H = im.height;
+    const uint32_t W = im.width, H = im.height, W3 = 3u * W;  // W3 < 2^18
     const uint32_t x_tile = m0 << lg_mw, y_tile = r0 << lg_mh;
     const uint32_t shx1 = TM_::shx(im, 1), shy1 = TM_::shy(im, 1), shx2 = TM_::shx(im, 2), shy2 = TM_::shy(im, 2);
     const uint32_t cmode = nc == 1 ? 3u : (shx1 == shx2 ? shx1 : 4u);
@@ -2946,8 +2959,9 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         if (w0[0] == 0x12345678u && w1[3] == 0x9abcdef0u)
 #endif
         {
-            store24(out + (size_t(y) * W + x) * 3, w0, min(8u, W - x));
-            if (pair && y + 1 < H) store24(out + (size_t(y + 1) * W + x) * 3, w1, min(8u, W - x));
+            uint8_t* const p0 = rgb_at(out, y, W3, x);
+            store24(p0, w0, min(8u, W - x));
+            if (pair && y + 1 < H) store24(p0 + W3, w1, min(8u, W - x));
         }
     }
     if (halves && lane < 2u * nrem) {
@@ -2959,8 +2973,9 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             uint32_t w0[3], w1[3];
             colour4x2(s_pl, pbase[0] + py * ppitch[0] + gx, ppitch[0], pbase[1] + (py >> 1) * ppitch[1] + (gx >> 1),
                       pbase[2] + (py >> 1) * ppitch[2] + (gx >> 1), w0, w1);
-            store12(out + (size_t(y) * W + x) * 3, w0, min(4u, W - x));
-            if (y + 1 < H) store12(out + (size_t(y + 1) * W + x) * 3, w1, min(4u, W - x));
+            uint8_t* const p0 = rgb_at(out, y, W3, x);
+            store12(p0, w0, min(4u, W - x));
+            if (y + 1 < H) store12(p0 + W3, w1, min(4u, W - x));
         }
     }
     return true;
@@ -3150,24 +3165,27 @@ __device__ __forceinline__ void fancy_row8(const FancyWin& P, uint32_t gx, uint3
             const int far = (y & 1) ? min(rr + 1, int(P.ch) - 1) : max(rr - 1, 0);
             const int16_t* frow = P.row(far);
             const uint2 f = *reinterpret_cast<const uint2*>(frow + (i0 - P.c0));
-            C[0] = 3 * C[0] + frow[lo];
-            C[1] = 3 * C[1] + s16(f.x, 0);
-            C[2] = 3 * C[2] + s16(f.x, 1);
-            C[3] = 3 * C[3] + s16(f.y, 0);
-            C[4] = 3 * C[4] + s16(f.y, 1);
-            C[5] = 3 * C[5] + frow[hi];
+            C[0] = mad24(C[0], 3, frow[lo]);
+            C[1] = mad24(C[1], 3, s16(f.x, 0));
+            C[2] = mad24(C[2], 3, s16(f.x, 1));
+            C[3] = mad24(C[3], 3, s16(f.y, 0));
+            C[4] = mad24(C[4], 3, s16(f.y, 1));
+            C[5] = mad24(C[5], 3, frow[hi]);
         }
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) {  // pixels 2k (even: sample i0 + k and its left) and 2k + 1 (odd: its right)
         const int i = i0 + k, c = C[k + 1];
         const bool first = i == 0, last = uint32_t(i) + 1 >= P.cw;
+        // the image's edge column is its own neighbour (libjpeg's edge cases: (4c + 8) >> 4 and
+        // (4c + 7) >> 4 for h2v2; c itself for h2v1, where (3c + c + 1) >> 2 = c as well)
+        const int left = first ? c : C[k], right = last ? c : C[k + 2];
         if (MODE == 1) {
-            v[2 * k] = first ? (4 * c + 8) >> 4 : (3 * c + C[k] + 8) >> 4;
-            v[2 * k + 1] = last ? (4 * c + 7) >> 4 : (3 * c + C[k + 2] + 7) >> 4;
+            v[2 * k] = mad24(c, 3, left + 8) >> 4;
+            v[2 * k + 1] = mad24(c, 3, right + 7) >> 4;
         } else {
-            v[2 * k] = first ? c : (3 * c + C[k] + 1) >> 2;
-            v[2 * k + 1] = last ? c : (3 * c + C[k + 2] + 2) >> 2;
+            v[2 * k] = mad24(c, 3, left + 1) >> 2;
+            v[2 * k + 1] = mad24(c, 3, right + 2) >> 2;
         }
     }
 }
@@ -3180,11 +3198,6 @@ __device__ __forceinline__ void fancy_colour8(const FancyWin (&P)[3], uint32_t g
     int cb[8], cr[8];
     fancy_row8<MODE>(P[1], gx, y, cb);
     fancy_row8<MODE>(P[2], gx, y, cr);
-#pragma unroll
-    for (int j = 0; j < 8; j++) {  // filtered samples stay in [-256, 255]: say so, so that
-        cb[j] = int(int16_t(cb[j]));  // chroma_terms' products are 24-bit multiplies
-        cr[j] = int(int16_t(cr[j]));
-    }
     uint32_t TR[4], TG[4], TB[4], ex = 0;
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -3344,7 +3357,7 @@ __global__ __launch_bounds__(kFancyThreads, JD_FANCY_LB) void k_colour_fancy(Bat
                 }
                 pack24(rgb, w);
             }
-            store24(reinterpret_cast<uint8_t*>(im.rgb) + (size_t(y) * W + gx) * 3, w, min(8u, W - gx));
+            store24(rgb_at(reinterpret_cast<uint8_t*>(im.rgb), y, 3u * W, gx), w, min(8u, W - gx));
         }
         if (!next) break;
         __syncthreads();  // every read of this band's windows is done
