@@ -2367,17 +2367,33 @@ __device__ __forceinline__ void colour16(const int (&Y0)[8], const int (&Y1)[8],
 
 // Packed colour (the common case): two pixels per 32-bit word as int16 halves, exactly the
 // integer terms above: R = clamp(y + t.r), B = clamp(y + t.b), G = clamp(y + t.g) with
-// v_pk_add / v_pk_max / v_pk_min (3 VALU per two pixels and channel), then v_perm byte shuffles
+// v_pk_add_u16 + v_sat_pk_u8_i16 (2 VALU per two pixels and channel), then v_perm byte shuffles
 // into RGB order.  Taken when no chroma sample of the wave's lane-step needs the reference's
 // double-precision G (ChromaTerms::exact, about 2e-4 of the samples).
-// clamp(y + t, 0, 255) of two int16 lanes, as two bytes in the low half (v_sat_pk_u8_i16)
-__device__ __forceinline__ uint32_t pk_add_sat_u8(uint32_t y, uint32_t t) {
-    const s16x2 r = __builtin_bit_cast(s16x2, y) + __builtin_bit_cast(s16x2, t);  // |y + t| < 2^15
+__device__ __forceinline__ uint32_t pair16(int lo, int hi) { return __builtin_amdgcn_perm(uint32_t(hi), uint32_t(lo), 0x05040100u); }
+// y + t of two int16 lanes; LO: t's low half serves both lanes (op_sel_hi), for the pixel pairs that
+// share one chroma sample, so no duplicated pair is built
+template <bool LO>
+__device__ __forceinline__ uint32_t pk_add16(uint32_t y, uint32_t t) {
+    uint32_t s;
+    if (LO) asm("v_pk_add_u16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(s) : "v"(y), "v"(t));
+    else asm("v_pk_add_u16 %0, %1, %2" : "=v"(s) : "v"(y), "v"(t));
+    return s;
+}
+// clamp(y + t, 0, 255) of the two lanes as bytes 0, 1 (bytes 2, 3 zero)
+template <bool LO>
+__device__ __forceinline__ uint32_t pk_sat_add(uint32_t y, uint32_t t) {
     uint32_t o;
-    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(o) : "v"(__builtin_bit_cast(uint32_t, r)));
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(o) : "v"(pk_add16<LO>(y, t)));
     return o;
 }
-__device__ __forceinline__ uint32_t pair16(int lo, int hi) { return __builtin_amdgcn_perm(uint32_t(hi), uint32_t(lo), 0x05040100u); }
+// the same as bytes 2, 3 of lo2, whose bytes 0, 1 are kept (SDWA destination: no v_perm to merge)
+template <bool LO>
+__device__ __forceinline__ uint32_t pk_sat_add_hi(uint32_t lo2, uint32_t y, uint32_t t) {
+    asm("v_sat_pk_u8_i16_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD" : "+v"(lo2)
+        : "v"(pk_add16<LO>(y, t)));
+    return lo2;
+}
 
 // Terms of the 8 >> SH chroma samples under 8 pixels as per-word pairs (word u = pixels 2u, 2u+1).
 // Returns the mask of samples (bit u) whose G needs the reference's double-precision path.
@@ -2398,10 +2414,15 @@ __device__ __forceinline__ uint32_t terms_words(const int16_t* s_pl, uint32_t cb
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const int a = SH == 0 ? 2 * w : (SH == 1 ? w : w >> 1);  // sample of the word's pixels
-        const int c = SH == 0 ? 2 * w + 1 : a;
-        TR[w] = pair16(t[a].r, t[c].r);
-        TG[w] = pair16(t[a].g, t[c].g);
-        TB[w] = pair16(t[a].b, t[c].b);
+        if (SH == 0) {
+            TR[w] = pair16(t[a].r, t[2 * w + 1].r);
+            TG[w] = pair16(t[a].g, t[2 * w + 1].g);
+            TB[w] = pair16(t[a].b, t[2 * w + 1].b);
+        } else {  // one sample under both pixels: the term in the low half (row_rgb_packed<true>)
+            TR[w] = uint32_t(t[a].r);
+            TG[w] = uint32_t(t[a].g);
+            TB[w] = uint32_t(t[a].b);
+        }
     }
     return ex;
 }
@@ -2425,24 +2446,26 @@ __device__ __forceinline__ void fix_g_exact(const uint4& Yq, const int16_t* s_pl
 }
 
 // 8 pixels of one row: Y as 4 words of int16 pairs -> 24 RGB bytes in 6 words (pack24's order):
-// per pixel pair and channel one packed add and one saturating pack to bytes, then byte shuffles.
+// per pixel pair and channel one packed add and one saturating pack to bytes (G's straight into
+// the high half of R's word), then byte shuffles.  LO: terms in the words' low halves (a pixel
+// pair on one chroma sample, terms_words<SH >= 1>), else one term per pixel (int16 pairs).
+template <bool LO>
 __device__ __forceinline__ void row_rgb_packed(const uint4& Yq, const uint32_t (&TR)[4], const uint32_t (&TG)[4],
                                                const uint32_t (&TB)[4], uint32_t (&w)[6]) {
     const uint32_t Y[4] = {Yq.x, Yq.y, Yq.z, Yq.w};
-    uint32_t RG[4], B[4];  // RG: r0 g0 r1 g1; B: b0 b1 in the low half
+    uint32_t RG[4], B[4];  // RG: r0 r1 g0 g1; B: b0 b1 in the low half
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-        const uint32_t r = pk_add_sat_u8(Y[u], TR[u]), g = pk_add_sat_u8(Y[u], TG[u]);
-        B[u] = pk_add_sat_u8(Y[u], TB[u]);
-        RG[u] = __builtin_amdgcn_perm(g, r, 0x05010400u);
+        RG[u] = pk_sat_add_hi<LO>(pk_sat_add<LO>(Y[u], TR[u]), Y[u], TG[u]);
+        B[u] = pk_sat_add<LO>(Y[u], TB[u]);
     }
     // perm(hi, lo, sel): selector bytes 0-3 take lo's bytes, 4-7 hi's, 0x0c a zero byte
-    w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x02040100u);                                            // r0 g0 b0 r1
-    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0503u), 0x05040100u);  // g1 b1 r2 g2
-    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x05030204u);                                            // b2 r3 g3 b3
-    w[3] = __builtin_amdgcn_perm(B[2], RG[2], 0x02040100u);                                            // r4 g4 b4 r5
-    w[4] = __builtin_amdgcn_perm(RG[3], __builtin_amdgcn_perm(B[2], RG[2], 0x0c0c0503u), 0x05040100u);  // g5 b5 r6 g6
-    w[5] = __builtin_amdgcn_perm(B[3], RG[3], 0x05030204u);                                            // b6 r7 g7 b7
+    w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x01040200u);                                            // r0 g0 b0 r1
+    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0503u), 0x06040100u);  // g1 b1 r2 g2
+    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x05030104u);                                            // b2 r3 g3 b3
+    w[3] = __builtin_amdgcn_perm(B[2], RG[2], 0x01040200u);                                            // r4 g4 b4 r5
+    w[4] = __builtin_amdgcn_perm(RG[3], __builtin_amdgcn_perm(B[2], RG[2], 0x0c0c0503u), 0x06040100u);  // g5 b5 r6 g6
+    w[5] = __builtin_amdgcn_perm(B[3], RG[3], 0x05030104u);                                            // b6 r7 g7 b7
 }
 
 // The 4:2:0 tail step: 4 pixels of two rows that share their two chroma samples (both chroma
@@ -2451,16 +2474,15 @@ __device__ __forceinline__ void row_rgb_packed(const uint4& Yq, const uint32_t (
 __device__ __forceinline__ void rgb4_packed(const uint2& Yq, const uint32_t (&TR)[2], const uint32_t (&TG)[2],
                                             const uint32_t (&TB)[2], uint32_t (&w)[3]) {
     const uint32_t Y[2] = {Yq.x, Yq.y};
-    uint32_t RG[2], B[2];
+    uint32_t RG[2], B[2];  // (terms in the low halves: both pixels of a word share their sample)
 #pragma unroll
     for (int u = 0; u < 2; u++) {
-        const uint32_t r = pk_add_sat_u8(Y[u], TR[u]), g = pk_add_sat_u8(Y[u], TG[u]);
-        B[u] = pk_add_sat_u8(Y[u], TB[u]);
-        RG[u] = __builtin_amdgcn_perm(g, r, 0x05010400u);
+        RG[u] = pk_sat_add_hi<true>(pk_sat_add<true>(Y[u], TR[u]), Y[u], TG[u]);
+        B[u] = pk_sat_add<true>(Y[u], TB[u]);
     }
-    w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x02040100u);                                            // r0 g0 b0 r1
-    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0503u), 0x05040100u);  // g1 b1 r2 g2
-    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x05030204u);                                            // b2 r3 g3 b3
+    w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x01040200u);                                            // r0 g0 b0 r1
+    w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0503u), 0x06040100u);  // g1 b1 r2 g2
+    w[2] = __builtin_amdgcn_perm(B[1], RG[1], 0x05030104u);                                            // b2 r3 g3 b3
 }
 __device__ __forceinline__ void fix_g4_exact(const uint2& Yq, const int (&cb)[2], const int (&cr)[2], uint32_t exmask,
                                              uint32_t (&w)[3]) {
@@ -2497,9 +2519,9 @@ __device__ __forceinline__ void colour4x2(const int16_t* s_pl, uint32_t yoff, ui
     const int cb[2] = {int(int16_t(cbw & 0xFFFFu)), int32_t(cbw) >> 16};
     const int cr[2] = {int(int16_t(crw & 0xFFFFu)), int32_t(crw) >> 16};
     const ChromaTerms t0 = chroma_terms(cb[0], cr[0]), t1 = chroma_terms(cb[1], cr[1]);
-    const uint32_t TR[2] = {pair16(t0.r, t0.r), pair16(t1.r, t1.r)};
-    const uint32_t TG[2] = {pair16(t0.g, t0.g), pair16(t1.g, t1.g)};
-    const uint32_t TB[2] = {pair16(t0.b, t0.b), pair16(t1.b, t1.b)};
+    const uint32_t TR[2] = {uint32_t(t0.r), uint32_t(t1.r)};
+    const uint32_t TG[2] = {uint32_t(t0.g), uint32_t(t1.g)};
+    const uint32_t TB[2] = {uint32_t(t0.b), uint32_t(t1.b)};
     const uint32_t ex = (t0.exact ? 1u : 0u) | (t1.exact ? 2u : 0u);
     const uint2 Y0 = *reinterpret_cast<const uint2*>(s_pl + yoff), Y1 = *reinterpret_cast<const uint2*>(s_pl + yoff + ypitch);
     rgb4_packed(Y0, TR, TG, TB, w0);
@@ -2919,11 +2941,13 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
                 default: ex = terms_words<2>(s_pl, cboff, croff, TR, TG, TB); break;
             }
             const uint4 Y0q = *reinterpret_cast<const uint4*>(s_pl + yoff);
-            row_rgb_packed(Y0q, TR, TG, TB, w0);
+            if (cmode == 0u) row_rgb_packed<false>(Y0q, TR, TG, TB, w0);
+            else row_rgb_packed<true>(Y0q, TR, TG, TB, w0);
             uint4 Y1q = make_uint4(0, 0, 0, 0);
             if (pair) {
                 Y1q = *reinterpret_cast<const uint4*>(s_pl + yoff + ppitch[0]);
-                row_rgb_packed(Y1q, TR, TG, TB, w1);
+                if (cmode == 0u) row_rgb_packed<false>(Y1q, TR, TG, TB, w1);  // (h1v2 chroma)
+                else row_rgb_packed<true>(Y1q, TR, TG, TB, w1);
             }
             if (__any(ex != 0u)) {  // uniform over the lanes in this step
                 switch (cmode) {
@@ -3208,7 +3232,7 @@ __device__ __forceinline__ void fancy_colour8(const FancyWin (&P)[3], uint32_t g
         TG[u] = pair16(t0.g, t1.g);
         TB[u] = pair16(t0.b, t1.b);
     }
-    row_rgb_packed(Yq, TR, TG, TB, w);
+    row_rgb_packed<false>(Yq, TR, TG, TB, w);
     if (__any(ex != 0u)) {
         const uint32_t Y[4] = {Yq.x, Yq.y, Yq.z, Yq.w};
 #pragma unroll

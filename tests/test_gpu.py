@@ -113,6 +113,9 @@ def test_pipelined_batches(decoder, golden):
     (1920, 1080, "4:4:4", 0, 0, 90),
     (1280, 720, "4:2:2", 0, 7, 75),
     (3840, 2160, "4:2:0", 1, 0, 90),   # BASELINE config 3 shape
+    (1920, 1080, "4:4:0", 1, 0, 90),   # vertically subsampled chroma only: row pairs, per-pixel terms
+    (333, 217, "4:4:0", 0, 0, 50),
+    (333, 217, "4:2:2", 0, 3, 50),
 ])
 def test_full_size_vs_oracle(decoder, w, h, ss, rows, blocks, q):
     data = jd_synth.encode(jd_synth.synth_pixels(w, h, 42), q, ss, rows, blocks)
