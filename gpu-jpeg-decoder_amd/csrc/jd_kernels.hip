@@ -2842,8 +2842,11 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             const uint32_t hc = TM_::h(im, comp), vc = TM_::v(im, comp);
             const uint32_t t = bb - TM_::cb0(im, comp);
             const uint32_t tyb = t >> __builtin_ctz(hc), txb = t - tyb * hc;  // hc in {1, 2, 4}
+            // (the plane pitch in a local: the stores below may alias the descriptor as far as the
+            // compiler knows, and it would reload im.mcux after each of them)
+            const uint32_t ppc = im.mcux * hc * 8;
             int16_t* dst = reinterpret_cast<int16_t*>(im.planes) + fancy_plane_off(im, comp) +
-                           size_t(((r0 + mr) * vc + tyb) * 8) * (im.mcux * hc * 8) + ((m0 + mi) * hc + txb) * 8;
+                           size_t(((r0 + mr) * vc + tyb) * 8) * ppc + ((m0 + mi) * hc + txb) * 8;
 #pragma unroll
             for (int r = 0; r < 8; r++) {
                 uint4 q;  // one v_perm per int16 pair
@@ -2851,7 +2854,8 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
                 q.y = pair16(blk[8 * r + 2], blk[8 * r + 3]);
                 q.z = pair16(blk[8 * r + 4], blk[8 * r + 5]);
                 q.w = pair16(blk[8 * r + 6], blk[8 * r + 7]);
-                *gptr(reinterpret_cast<u32x4*>(dst + size_t(r) * (im.mcux * hc * 8))) = u32x4{q.x, q.y, q.z, q.w};
+                *gptr(reinterpret_cast<u32x4*>(dst)) = u32x4{q.x, q.y, q.z, q.w};
+                dst += ppc;
             }
         }
         return true;
