@@ -829,28 +829,28 @@ __device__ __forceinline__ u32x4 win_load(uintptr_t a, int q, uintptr_t last) {
 // is then fetched in one go instead of once per 32-byte round: with ~32 K lanes per XCD streaming
 // their own pieces, a line read round by round is often evicted from L2 between two rounds.
 #ifndef JD_WIN_GROUP
-#define JD_WIN_GROUP 4
+#define JD_WIN_GROUP (128 / JD_WIN_PIECE)  // 128 bytes of a lane's stream per group
 #endif
 constexpr int kWinGroup = JD_WIN_GROUP;
-static_assert(kWin == 32 && kRowOverlap == 8, "WinGroup assumes 32-byte windows with an 8-byte overlap");
+static_assert(kWin % 16 == 0 && kRowOverlap == 8, "WinGroup: whole 16-byte loads per window, an 8-byte overlap");
 template <int G>
 struct WinGroup {
-    u32x4 v[2 * G + 1];
+    static constexpr int L = kWin / 16;  // 16-byte loads per window
+    u32x4 v[L * G + 1];
     __device__ __forceinline__ void load(uintptr_t a, uintptr_t last) {
 #pragma unroll
-        for (int q = 0; q < 2 * G; q++) v[q] = load16(a + 16 * q, last);
-        const uintptr_t c = a + 32 * G;
+        for (int q = 0; q < L * G; q++) v[q] = load16(a + 16 * q, last);
+        const uintptr_t c = a + kWin * G;
         const u32x2 t = *reinterpret_cast<const __attribute__((address_space(1))) u32x2*>(c < last ? c : last);
-        v[2 * G] = u32x4{t.x, t.y, 0u, 0u};
+        v[L * G] = u32x4{t.x, t.y, 0u, 0u};
     }
     // the group's next window into the row, then the rest moves down one window (constant register
     // indices throughout: a window index would put the group in scratch memory)
     __device__ __forceinline__ void fill_next(uint32_t* row) {
-        JD_ROW_FILL(row, v[0], 0);
-        JD_ROW_FILL(row, v[1], 1);
-        JD_ROW_FILL(row, v[2], 2);
 #pragma unroll
-        for (int q = 0; q + 2 < 2 * G + 1; q++) v[q] = v[q + 2];
+        for (int q = 0; q <= L; q++) JD_ROW_FILL(row, v[q], q);  // q == L: the overlap (first 8 bytes)
+#pragma unroll
+        for (int q = 0; q + L < L * G + 1; q++) v[q] = v[q + L];
     }
 };
 
