@@ -979,9 +979,15 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     TabT tab = tab_dc0;
     bool active = active_in;
     uint32_t m_start = W.start, m_end = W.start;
-    if (W.start + 8 > sbits) active = false;  // starts at the data end: empty
+    if (W.start >= sbits) active = false;  // starts at the data end: empty
     uint32_t next_cp = W.start + cp_bits, ncp = 0, join = 0;
-    // an MCU end at/after end_thr leaves fewer than 8 bits: the data end (padding before RSTn/EOI)
+    // The last byte: an MCU end at/after end_thr leaves fewer than 8 bits, which are padding (1-bits
+    // before RSTn / EOI) or, where an MCU can be that short (a grayscale block: DC "00" + EOB
+    // "1010"), one more MCU.  From there every MCU end takes the slow branch, and m_end (unused until
+    // the walk ends) holds where the current MCU began: m_end >= end_thr marks this tail.  If the MCU
+    // fails (a bad code, or bits past the data) it was padding -- padding never completes an MCU, no
+    // Huffman code being all 1-bits -- and the piece ends at m_end without an error (the oracle
+    // decodes exactly the interval's MCUs and skips the padding).
     const uint32_t end_thr = sbits >= 8u ? sbits - 7u : 0u;
     // the next bit at which an MCU end needs the slow branch: the next of piece end, data end,
     // checkpoint (0 after an error)
@@ -1130,14 +1136,22 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             if (JD_PSTAT) st_mend_w += __any(mend && pos >= thr) ? 1u : 0u;
             if (mend && pos >= thr) {
                 const uint32_t consumed = pos;
-                if (errs || consumed > sbits) {  // an error in this MCU
-                    emcu = min(emcu, mcus - 1u);
-                    errs = 0;
-                }
+                const bool fail = errs || consumed > sbits;
+                errs = 0;
                 uint32_t nxt = 0xFFFFFFFFu;
-                if (consumed >= W.stop_at || consumed >= end_thr) {  // the piece ends here
+                if (fail && m_end >= end_thr) {  // an MCU begun in the last byte: padding, not an MCU
+                    mcus--;
+                    active = false;
+                } else if (fail) {  // an error in this MCU
+                    emcu = min(emcu, mcus - 1u);
+                }
+                if (!active) {
+                    // (rolled back)
+                } else if (consumed >= W.stop_at || consumed >= sbits) {  // the piece ends here
                     m_end = consumed;
                     active = false;
+                } else if (consumed >= end_thr) {  // the last byte (thr stays <= the next MCU end)
+                    m_end = consumed;
                 } else if (KIND == kSpec) {
                     if (consumed >= next_cp && ncp < uint32_t(kCpMax)) {
                         cp[ncp] = CpRec{consumed, mcus, ent2 >> 1, 0u};
@@ -1164,8 +1178,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         JD_FLUSH_Q();
         JD_FLUSH_B();
         if (active && R.bit() > sbits) {  // past the data
-            m_end = R.bit();
-            emcu = min(emcu, mcus);
+            if (m_end < end_thr) {  // (else in an MCU begun in the last byte, at m_end: padding)
+                m_end = R.bit();
+                emcu = min(emcu, mcus);
+            }
             active = false;
         }
         if (active && (ent2 + 2u) / 4u + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
@@ -1461,7 +1477,10 @@ __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
 // The MCUs piece j contributes, given its first MCU m0 (the interval has nmcu_seg): a piece before
 // the last one that matters takes all it walked, error-free; the last takes the rest, which it must
 // have walked error-free — exactly, unless the interval is the scan's last, whose trailing bytes
-// are ignored (the oracle stops after the frame's MCUs).
+// are ignored (the oracle stops after the frame's MCUs).  The last piece of an interval that ends
+// at an RSTn walks to the data end: an error anywhere in it, even after its last counted MCU,
+// means bytes were left before the marker (the walk ran into them), which the oracle reports as
+// a corrupt restart (br_restart finds no marker at the byte-aligned position).
 __device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_t m0, uint32_t nmcu_seg, bool last,
                                                bool final_seg, bool& bad) {
     if (!last) {
@@ -1469,7 +1488,7 @@ __device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_
         return pm;
     }
     const uint32_t take = nmcu_seg >= m0 ? nmcu_seg - m0 : 0u;
-    bad |= m0 > nmcu_seg || (final_seg ? pm < take : pm != take) || em < take;
+    bad |= m0 > nmcu_seg || (final_seg ? pm < take || em < take : pm != take || em != kNoError);
     return min(take, pm);
 }
 

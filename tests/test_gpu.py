@@ -309,6 +309,51 @@ def _cut_interval(jpeg, seg, nmcu):
     return bytes(out)
 
 
+# Bit flips in the entropy data of images with restart intervals that leave whole bytes between an
+# interval's last MCU and its RSTn (found by tools/parity_sweep.py): the oracle's restart finds no
+# marker at the byte-aligned position (status CORRUPT); the interval's last piece must not accept an
+# error after its last counted MCU (jd_kernels.hip piece_take).
+@pytest.mark.parametrize("params", [
+    {"seed": 11004573, "w": 133, "h": 12, "ss": "4:4:4", "q": 50, "rows": 0, "blocks": 2, "flips": 1},
+    {"seed": 11002742, "w": 119, "h": 34, "ss": "4:2:2", "q": 90, "rows": 0, "blocks": 2, "flips": 3},
+    {"seed": 11005497, "w": 36, "h": 238, "ss": "4:2:0", "q": 95, "rows": 2, "blocks": 0, "flips": 3},
+    {"seed": 11006876, "w": 35, "h": 157, "ss": "4:4:0", "q": 90, "rows": 0, "blocks": 10, "flips": 3},
+    {"seed": 11009965, "w": 28, "h": 100, "ss": "4:4:0", "q": 100, "rows": 0, "blocks": 2, "flips": 1},
+    {"seed": 11000078, "w": 22, "h": 250, "ss": "4:4:0", "q": 90, "rows": 0, "blocks": 5, "flips": 2},
+])
+def test_bytes_left_before_rst_is_corrupt(decoder, params):
+    import parity_sweep
+
+    data = parity_sweep.make_image(params)
+    st, ref = jdoracle.decode(data)
+    assert st == jdamd.JD_ERR_CORRUPT
+    out, status = decoder.decode_batch([data])
+    assert status == [st]
+    clean = parity_sweep.make_image(dict(params, flips=0))  # the unflipped image decodes
+    st0, ref0 = jdoracle.decode(clean)
+    out0, status0 = decoder.decode_batch([clean])
+    assert st0 == 0 and status0 == [0] and np.array_equal(out0[0], ref0)
+
+
+# Grayscale images whose last MCU (one block: DC "00" + EOB "1010", 6 bits) lies inside the last
+# byte of the entropy data or of a restart interval (found by tools/parity_sweep.py): the walk must
+# decode it instead of taking the byte for padding (jd_kernels.hip walk_piece, mbeg).
+@pytest.mark.parametrize("params", [
+    {"seed": 12011017, "w": 73, "h": 193, "ss": "gray", "q": 75, "rows": 0, "blocks": 0, "flips": 0},
+    {"seed": 12020118, "w": 385, "h": 225, "ss": "gray", "q": 50, "rows": 3, "blocks": 0, "flips": 1},
+    {"seed": 12072936, "w": 281, "h": 83, "ss": "gray", "q": 35, "rows": 3, "blocks": 0, "flips": 0},
+    {"seed": 12083853, "w": 274, "h": 106, "ss": "gray", "q": 20, "rows": 0, "blocks": 0, "flips": 0},
+])
+def test_mcu_inside_the_last_byte(decoder, params):
+    import parity_sweep
+
+    data = parity_sweep.make_image(params)
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    out, status = decoder.decode_batch([data])
+    assert status == [0] and np.array_equal(out[0], ref)
+
+
 @pytest.mark.parametrize("w,h,ss,q,rst", [(8, 8, "gray", 90, 0), (16, 16, "4:2:0", 50, 0), (24, 16, "4:4:4", 95, 0),
                                           (64, 48, "4:2:2", 75, 0), (32, 32, "4:2:0", 90, 1), (40, 16, "4:4:4", 75, 2),
                                           (256, 256, "gray", 90, 0), (128, 128, "4:2:0", 75, 0)])
