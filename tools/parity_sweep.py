@@ -6,7 +6,8 @@ Batches of synthetic JPEGs with random size (1 .. 2000 x 1 .. 1200, mostly small
 (4:4:4 / 4:2:2 / 4:2:0 / 4:4:0 / grayscale), quality (20 .. 100), restart interval (none, MCU rows,
 MCU counts) and, for about a fifth of them, bit flips in the entropy-coded data, are decoded in one
 batch call on the GPU through each entropy-decode path of the library (default, "sync": 1024-bit
-pieces with most speculative starts failing, "lanes": one lane per restart interval) and compared
+pieces with most speculative starts failing, "lanes": one lane per restart interval, "full": the
+full-batch piece geometry whatever the batch size; --fancy: with libjpeg fancy upsampling) and compared
 with the oracle (oracle/jdoracle.c via oracle/jdoracle.py, in a process pool): per-image status, and
 the pixels when the oracle decodes the image.  Any difference is written to --out with the image's
 parameters and the run exits non-zero.  The oracle is the checker only; nothing here is timed.
@@ -50,11 +51,15 @@ def make_image(args):
     return data
 
 
-def oracle_digest(data):
+def oracle_digest(data, fancy=False):
     import jdoracle
 
-    st, ref = jdoracle.decode(data)
+    st, ref = jdoracle.decode(data, fancy=fancy)
     return st, (hashlib.sha256(ref.tobytes()).hexdigest() if st == 0 else None)
+
+
+def oracle_digest_fancy(data):
+    return oracle_digest(data, True)
 
 
 def draw(rng, seed):
@@ -78,14 +83,15 @@ def main():
     ap.add_argument("--batch", type=int, default=96)
     ap.add_argument("--workers", type=int, default=12)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
+    ap.add_argument("--fancy", action="store_true", help="libjpeg fancy upsampling (its oracle: jdoracle fancy=True)")
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
-    paths = ["auto", "sync", "lanes"]
+    paths = ["auto", "sync", "lanes", "full"]
     # the workers come from a fork server started (and the pool filled) before this process
     # initialises the GPU: no worker is a fork of a process holding a HIP context
     pool = ProcessPoolExecutor(a.workers, mp_context=multiprocessing.get_context("forkserver"))
     list(pool.map(time.sleep, [0.2] * a.workers))
-    decs = {p: jdamd.Decoder(0, path=p) for p in paths}
+    decs = {p: jdamd.Decoder(0, path=p, fancy=a.fancy) for p in paths}
     t_end = time.time() + 60 * a.minutes
     n_img = n_ok = n_bad_status = 0
     fails = []
@@ -98,7 +104,7 @@ def main():
                 params.append(draw(rng, seed))
                 seed += 1
             datas = list(pool.map(make_image, params, chunksize=4))
-            ref = list(pool.map(oracle_digest, datas, chunksize=4))
+            ref = list(pool.map(oracle_digest_fancy if a.fancy else oracle_digest, datas, chunksize=4))
             path = paths[it % len(paths)]
             outs, status = decs[path].decode_batch(datas)
             for p, d, o, s, (st, dig) in zip(params, datas, outs, status, ref):
@@ -118,7 +124,7 @@ def main():
     for d in decs.values():
         d.close()
     res = {"images": n_img, "decoded_equal_or_checked": n_ok, "corrupt_status_checked": n_bad_status,
-           "batches": it, "mismatches": fails, "seed": a.seed, "minutes": a.minutes}
+           "batches": it, "mismatches": fails, "seed": a.seed, "minutes": a.minutes, "fancy": a.fancy, "paths": paths}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
