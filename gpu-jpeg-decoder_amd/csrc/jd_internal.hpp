@@ -25,23 +25,27 @@ constexpr int kLutSize = 1 << kLutBits;
 
 // Symbol entry of the rare path (32 bits; jd_kernels.hip huff_slow / the piece walks' rare branch):
 //     bits 0..4   L    bits the symbol consumes, code + magnitude (0: code longer than kLutBits)
+//     bit  5      sz16 DC size 16 (the sz field then 0)
 //     bit  6      emit AC coefficient stored (size != 0)
 //     bits 8..14  adv  advance of the coefficient index z (the last position decoded, DC = 0):
 //                      DC 0, AC run + 1 (ZRL 16), EOB 64.  A block ends when z + adv >= 63, and
 //                      a coefficient lands at z + adv unless that is past 63 (parser.cpp:120-131:
 //                      its magnitude bits are consumed, the value dropped, the block ends)
 //     bit  15     dc   DC symbol
-//     bits 16..19 sz   magnitude bits (DC: symbol, AC: symbol & 15; a DC size above 15 is corrupt)
+//     bits 16..19 sz   magnitude bits (DC: symbol, AC: symbol & 15; a DC size above 16 is corrupt)
 //     bit  7      bad  corrupt code (slow path only)
 //   The coefficient is EXTEND(the last sz of the L bits).
-constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 7;
+constexpr uint32_t kEntEmit = 1u << 6, kEntDc = 1u << 15, kEntBad = 1u << 7, kEntSz16 = 1u << 5;
 
-// Entry of a code of length l for symbol sym; 0 when it cannot be represented (l + sz > 31 or a
-// DC size beyond 15 bits: corrupt for 8-bit baseline, whose DC sizes are <= 11).
+// Entry of a code of length l for symbol sym; 0 when it cannot be represented: l + sz > 31 (a DC
+// size 16 behind a 16-bit code), or a DC size beyond 16 bits.  Baseline DC sizes are <= 11, but
+// the reference reads a DC size as it comes (parser.cpp:106-108, 16 bits into a uint16_t) and the
+// oracle takes up to 16 (jdoracle.c decode_block): a size-16 difference spans +-65535 (a block
+// record's DC field has 17 bits, jd_kernels.hip block_rec).
 JD_HD inline uint32_t lut_entry(uint32_t l, uint32_t sym, bool is_dc) {
     const uint32_t sz = is_dc ? sym : (sym & 15u);
-    if (sz > 15u || l + sz > 31u || l == 0u) return 0u;
-    if (is_dc) return (l + sz) | kEntDc | (sz << 16);
+    if (sz > 16u || l + sz > 31u || l == 0u) return 0u;
+    if (is_dc) return (l + sz) | kEntDc | ((sz & 15u) << 16) | ((sz >> 4) << 5);
     const uint32_t adv = sym == 0u ? 64u : (sym >> 4) + 1u;
     return (l + sz) | (sz ? kEntEmit : 0u) | (adv << 8) | (sz << 16);
 }
@@ -200,15 +204,22 @@ constexpr int kCpRecords = kCpMax + 1;
 
 // Speculative-walk checkpoints, kCpRecords per piece slot: kCpMax checkpoints, then the totals.
 //   checkpoint: {bit of an MCU boundary, MCUs and AC entries written up to it (entries = offset in
-//                the piece's region), 0}
-//   totals:     {end, MCUs, AC entries, MCUs before the first error (kNoError: none)}
+//                the piece's region), the walk's MCU index of its first error between the previous
+//                checkpoint (or the start) and this one (kNoError: none)}
+//   totals:     {end, MCUs, AC entries, first error after the last checkpoint}
+// (piece_join: tail << 24 | checkpoints << 16, tail = the walk's MCUs begun in the data's last byte)
 // A re-walk from the true start that reaches a checkpoint's bit at an MCU boundary is in the
 // speculative walk's state there, so it joins it: the piece is then the re-walk's blocks followed
-// by the speculative walk's blocks from that checkpoint on (two segments, k_gather).
+// by the speculative walk's blocks from that checkpoint on (two segments, k_gather), and its first
+// error is the re-walk's or the speculative walk's first after that checkpoint (the speculative
+// walk's first error overall may lie before, in bits it decoded out of sync).
 struct alignas(16) CpRec {
     uint32_t bit, mcus, ents, flags;
 };
 constexpr uint32_t kNoError = 0xFFFFFFFFu;
+// piece_emcu: the MCUs before the piece's first error, or, >= kTailErr, no error and kNoError - it
+// of its MCUs began in the data's last byte (an interval ending at RSTn may end before them: k_chain)
+constexpr uint32_t kTailErr = kNoError - 15u;
 
 // Per-piece output region (image-relative AC-entry slots): AC entries ascend from its start, one
 // 32-bit record per block (AC-entry count << 16 | 16-bit DC difference) descends from its end.  A

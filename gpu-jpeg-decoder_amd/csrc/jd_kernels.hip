@@ -517,7 +517,7 @@ __device__ __forceinline__ uint32_t huff_slow(const uint32_t* lutw, uint32_t pee
 
 // EXTEND (utils/stream.cpp:44-52) of the last sz bits of the L bits at the top of peek.
 __device__ __forceinline__ int huff_value(uint32_t peek, uint32_t e) {
-    const uint32_t L = e & 31u, sz = __builtin_amdgcn_ubfe(e, 16u, 4u);
+    const uint32_t L = e & 31u, sz = __builtin_amdgcn_ubfe(e, 16u, 4u) | ((e & kEntSz16) >> 1);
     const uint32_t mag = __builtin_amdgcn_ubfe(peek, 32u - L, sz);  // width 0 -> 0
     const uint32_t half = (1u << sz) >> 1;
     return int(mag) - (mag < half ? int(2 * half - 1) : 0);
@@ -889,13 +889,18 @@ struct TabSpace<true> {
     static __device__ __forceinline__ const uint32_t* at(T tab) { return reinterpret_cast<const uint32_t*>(tab); }
 };
 
-// Block record in a piece's region: escape flag << 23 | AC-entry slot count (<= 126) << 16 | the
-// 16-bit DC difference (a DC size is <= 15 bits, jd_internal.hpp lut_entry).  esc: 0 or 1 << 23;
-// cnt2 = 2 x the slot count.  A block stores at most 63 coefficients (each at a zig-zag index
-// < 64, strictly increasing), of at most two slots each, so the count fits its 7 bits.
+// Block record in a piece's region: AC-entry slot count (<= 126) << 18 | escape flag << 17 | the
+// DC difference, 17-bit two's complement (a DC size is <= 16 bits, jd_internal.hpp lut_entry: the
+// difference lies within +-65535).  esc: 0 or kRecEsc; cnt2 = 2 x the slot count.  A block stores
+// at most 63 coefficients (each at a zig-zag index < 64, strictly increasing), of at most two slots
+// each, so the count fits its 7 bits.
+constexpr uint32_t kRecEsc = 1u << 17;
 __device__ __forceinline__ uint32_t block_rec(uint32_t cnt2, int dc, uint32_t esc) {
-    return ((cnt2 << 15) | esc) | (uint32_t(dc) & 0xFFFFu);
+    return ((cnt2 << 17) | esc) | (uint32_t(dc) & 0x1FFFFu);
 }
+__device__ __forceinline__ uint32_t record_cnt(uint32_t r) { return r >> 18; }
+__device__ __forceinline__ bool record_esc(uint32_t r) { return (r & kRecEsc) != 0; }
+__device__ __forceinline__ int record_dc(uint32_t r) { return int32_t(r << 15) >> 15; }
 // A 16-bit slot into a lane's ring of 16 (ringb 32-byte aligned, ent2 = 2 x the slot count).
 __device__ __forceinline__ void ring_put(uint32_t ringb, uint32_t ent2, uint32_t v) {
     *(__attribute__((address_space(3))) uint16_t*)size_t(ringb | (ent2 & 30u)) = uint16_t(v);
@@ -929,9 +934,13 @@ struct PWalk {
     uint32_t start, stop_at;
     uint32_t* reg;
     uint32_t rw;
-    uint32_t m_start, m_end, mcus, ents, emcu, ncp, join;
+    uint32_t m_start, m_end, mcus, ents, emcu, ncp, join, tail;
     unsigned long long* stats;  // JD_PSTAT builds
 };
+
+__device__ __forceinline__ uint32_t piece_emcu_code(uint32_t emcu, uint32_t tail) {
+    return emcu != kNoError ? emcu : kNoError - min(tail, kNoError - kTailErr);
+}
 constexpr int kSpec = 0, kRedo = 1;
 
 #ifndef JD_NT
@@ -998,6 +1007,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
         for (int c = 0; c < kCpMax; c++) nxt0 = (cpb[c] > W.start) ? min(nxt0, cpb[c]) : nxt0;
     }
     uint32_t thr = min(min(W.stop_at, end_thr), nxt0);
+    // errs: bit 0, an error in the current MCU; bits 1..: MCUs completed that began in the last byte
     uint32_t mcus = 0, emcu = kNoError, errs = 0;
     // ent2 / ent_blk2: 2 x the slot counts (the ring's byte offsets); esc_blk: the record's escape bit
     uint32_t ent2 = 0, ent_blk2 = 0, blk = 0, esc_blk = 0;
@@ -1103,10 +1113,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 const bool big = entry_big(val);
                 ring_put(ringb, ent2, entry16(val, zn, big));
                 ring_put(ringb, ent2 + 2u, uint32_t(val));
-                esc_blk |= (emit && big) ? (1u << 23) : 0u;
+                esc_blk |= (emit && big) ? kRecEsc : 0u;
                 ent2 += emit ? (big ? 4u : 2u) : 0u;
                 if (e & kEntBad) {  // the next MCU end takes the branch below
-                    errs = 1u;
+                    errs |= 1u;
                     thr = 0u;
                 }
             }
@@ -1136,14 +1146,16 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             if (JD_PSTAT) st_mend_w += __any(mend && pos >= thr) ? 1u : 0u;
             if (mend && pos >= thr) {
                 const uint32_t consumed = pos;
-                const bool fail = errs || consumed > sbits;
-                errs = 0;
+                const bool fail = (errs & 1u) || consumed > sbits;
+                errs &= ~1u;
                 uint32_t nxt = 0xFFFFFFFFu;
                 if (fail && m_end >= end_thr) {  // an MCU begun in the last byte: padding, not an MCU
                     mcus--;
                     active = false;
                 } else if (fail) {  // an error in this MCU
                     emcu = min(emcu, mcus - 1u);
+                } else if (m_end >= end_thr) {  // an MCU begun in the last byte, complete
+                    errs += 2u;
                 }
                 if (!active) {
                     // (rolled back)
@@ -1154,7 +1166,8 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                     m_end = consumed;
                 } else if (KIND == kSpec) {
                     if (consumed >= next_cp && ncp < uint32_t(kCpMax)) {
-                        cp[ncp] = CpRec{consumed, mcus, ent2 >> 1, 0u};
+                        cp[ncp] = CpRec{consumed, mcus, ent2 >> 1, emcu};  // the segment before it
+                        emcu = kNoError;
                         ncp++;
                         next_cp = (ncp < uint32_t(kCpMax)) ? consumed + cp_bits : 0xFFFFFFFFu;
                     }
@@ -1211,6 +1224,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     W.emcu = emcu;
     W.ncp = ncp;
     W.join = join;
+    W.tail = errs >> 1;
     if (JD_PSTAT && KIND == kSpec && W.stats) {
         const uint32_t v[10] = {st_wit, 0u, wave_sum_u32(st_lit), 0u, wave_sum_u32(st_rare),
                                 wave_max_u32(st_rare_w), st_rounds, 1u, wave_max_u32(st_mend_w), wave_sum_u32(st_sym)};
@@ -1384,10 +1398,15 @@ __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
     b.piece_end[u] = W.m_end;
     b.piece_nmcu[u] = W.mcus;
     b.piece_nent[u] = W.ents;
-    b.piece_emcu[u] = W.emcu;
+    // W.emcu: the first error after the last checkpoint; each checkpoint holds its segment's
+    uint32_t emcu = W.emcu;
+#pragma unroll
+    for (int k = 0; k < kCpMax; k++)
+        if (uint32_t(k) < W.ncp) emcu = min(emcu, cp[k].flags);
+    b.piece_emcu[u] = piece_emcu_code(emcu, W.tail);
     b.piece_abase[u] = P.own;
     b.piece_amcu[u] = W.mcus;
-    b.piece_join[u] = W.ncp << 16;
+    b.piece_join[u] = (min(W.tail, 255u) << 24) | (W.ncp << 16);
     cp[kCpMax] = CpRec{W.m_end, W.mcus, W.ents, W.emcu};
 }
 
@@ -1400,11 +1419,13 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
                                uint32_t expect, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp, uint32_t* row,
                                uint32_t* ring, bool need) {
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
-    uint32_t ncp = 0, base = P.own;
+    uint32_t ncp = 0, base = P.own, stail = 0;
     CpRec tot{0u, 0u, 0u, kNoError};
     uint32_t cpb[kCpMax];
     if (need) {
-        ncp = b.piece_join[u] >> 16;
+        const uint32_t pj = b.piece_join[u];  // k_piece's: tail << 24 | checkpoints << 16
+        ncp = (pj >> 16) & 0xFFu;
+        stail = pj >> 24;
         tot = cp[kCpMax];
         const uint32_t img = b.seg_img[s];
         const uint32_t a = b.no_pool ? 0xFFFFFFFFu : atomicAdd(&b.img_pool[img], P.rw);
@@ -1421,19 +1442,26 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
     W.rw = P.rw;
     walk_piece<kRedo, GL>(S, s_lutw, dcp, acp, row, ring, need, W, cp, 0xFFFFFFFFu, cpb);
     if (!need) return 0;
-    uint32_t end = W.m_end, mcus = W.mcus, ents = W.ents, emcu = W.emcu;
-    if (W.join) {
+    uint32_t end = W.m_end, mcus = W.mcus, ents = W.ents, emcu = W.emcu, tail = W.tail;
+    if (W.join) {  // (checkpoints lie before the last byte: the tail, if any, is the speculative walk's)
         const CpRec c = cp[W.join - 1];
         end = tot.bit;
         mcus += tot.mcus - c.mcus;
         ents += tot.ents - c.ents;
-        if (tot.flags != kNoError && tot.flags >= c.mcus) emcu = min(emcu, W.mcus + (tot.flags - c.mcus));
+        tail = stail;
+        // the speculative walk's first error after the joined checkpoint: in the segments of the
+        // checkpoints after it (each holds the one before it), or after the last (the totals')
+        uint32_t e = tot.flags;
+#pragma unroll
+        for (int k = 0; k < kCpMax; k++)
+            if (uint32_t(k) >= W.join && uint32_t(k) < ncp) e = min(e, cp[k].flags);
+        if (e != kNoError) emcu = min(emcu, W.mcus + (e - c.mcus));
     }
     b.piece_bit[u] = expect;
     b.piece_end[u] = end;
     b.piece_nmcu[u] = mcus;
     b.piece_nent[u] = ents;
-    b.piece_emcu[u] = emcu;
+    b.piece_emcu[u] = piece_emcu_code(emcu, tail);
     b.piece_abase[u] = base;
     b.piece_amcu[u] = W.mcus;
     b.piece_join[u] = (ncp << 16) | W.join;
@@ -1480,15 +1508,23 @@ __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
 // are ignored (the oracle stops after the frame's MCUs).  The last piece of an interval that ends
 // at an RSTn walks to the data end: an error anywhere in it, even after its last counted MCU,
 // means bytes were left before the marker (the walk ran into them), which the oracle reports as
-// a corrupt restart (br_restart finds no marker at the byte-aligned position).
+// a corrupt restart (br_restart finds no marker at the byte-aligned position).  Except for MCUs
+// that began in the data's last byte (em's tail count, piece_emcu_code): where the interval's last
+// MCU ends in that byte, its leftover bits -- not padding, in a corrupt stream -- may complete
+// another short MCU, which the oracle, having decoded the interval's count, never reads; the count
+// is then right if it lies between the MCUs before the tail and all of them.  (Only the interval's
+// last piece can hold them, unless a piece boundary falls in that byte: such a piece's tail MCUs
+// count in full.)
 __device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_t m0, uint32_t nmcu_seg, bool last,
                                                bool final_seg, bool& bad) {
+    const bool err = em < kTailErr;
     if (!last) {
-        bad |= em != kNoError;
+        bad |= err;
         return pm;
     }
     const uint32_t take = nmcu_seg >= m0 ? nmcu_seg - m0 : 0u;
-    bad |= m0 > nmcu_seg || (final_seg ? pm < take || em < take : pm != take || em != kNoError);
+    const uint32_t tail = err ? 0u : kNoError - em;
+    bad |= m0 > nmcu_seg || (final_seg ? pm < take || em < take : pm < take || pm - tail > take || err);
     return min(take, pm);
 }
 
@@ -1679,10 +1715,10 @@ __device__ __forceinline__ uint32_t gather_rows(BlockInfo* out, const uint32_t* 
 #pragma unroll
         for (int i = 0; i < kGatherLoads; i++) {
             const uint32_t k = k0 + t + 16u * i;
-            const uint32_t cnt = (r[i] >> 16) & 127u;
+            const uint32_t cnt = record_cnt(r[i]);
             const uint32_t incl = uint32_t(row_scan_dpp(int(cnt)));
             if (k < n && (!(JD_ABL & 32) || run == 0x7FFFFFFFu))
-                out[k] = BlockInfo{run + incl - cnt, pack_cnt_dc(cnt, int(int16_t(r[i] & 0xFFFFu)), r[i] >> 23)};
+                out[k] = BlockInfo{run + incl - cnt, pack_cnt_dc(cnt, record_dc(r[i]), record_esc(r[i]))};
             run += uint32_t(__shfl(int(incl), int(last), 64));
         }
     }

@@ -354,19 +354,82 @@ def test_mcu_inside_the_last_byte(decoder, params):
     assert status == [0] and np.array_equal(out[0], ref)
 
 
+# Corrupt streams found by tools/parity_sweep.py, through every piece geometry:
+#  - 16033655: a flip leaves an interval's last MCU ending in its last byte, and the leftover bits
+#    complete one more (short, grayscale) MCU, which the oracle never reads (it decodes the
+#    interval's count, then finds RSTn): status 0 (jd_kernels.hip piece_take, the tail count);
+#  - 16038946: on 1024-bit pieces, a piece re-walked from its true start joins its speculative
+#    walk, which had hit a garbage code before synchronising and a real one after the joined
+#    checkpoint: the real one must count (status corrupt; redo_piece, per-checkpoint errors);
+#  - 16045274: a flip turns the chroma DC table's first symbol into 16 (DC size 16, decoded by the
+#    reference and the oracle: jd_internal.hpp lut_entry).
+@pytest.mark.parametrize("params", [
+    {"seed": 16033655, "w": 74, "h": 179, "ss": "gray", "q": 35, "rows": 0, "blocks": 2, "flips": 1},
+    {"seed": 16038946, "w": 366, "h": 10, "ss": "gray", "q": 100, "rows": 0, "blocks": 0, "flips": 1},
+    {"seed": 16045274, "w": 11, "h": 68, "ss": "4:4:4", "q": 90, "rows": 0, "blocks": 0, "flips": 3},
+])
+def test_sweep_cases_every_path(params):
+    import parity_sweep
+
+    data = parity_sweep.make_image(params)
+    st, ref = jdoracle.decode(data)
+    for path in ("auto", "sync", "lanes", "full"):
+        dec = jdamd.Decoder(0, path=path)
+        try:
+            out, status = dec.decode_batch([data])
+        finally:
+            dec.close()
+        assert status == [st], path
+        if st == 0:
+            assert np.array_equal(out[0], ref), path
+
+
+def _dht_values_offset(data, tc, th):
+    """Byte offset of the symbol values of DHT table (tc, th) in a JPEG."""
+    i = 2
+    while i + 4 <= len(data):
+        m, L = data[i + 1], (data[i + 2] << 8) | data[i + 3]
+        if m == 0xC4:
+            q = i + 4
+            while q < i + 2 + L:
+                tot = sum(data[q + 1:q + 17])
+                if (data[q] >> 4, data[q] & 15) == (tc, th):
+                    return q + 17
+                q += 17 + tot
+        if m == 0xDA:
+            break
+        i += 2 + L
+    raise ValueError("no such table")
+
+
 @pytest.mark.parametrize("w,h,ss,q,rst", [(8, 8, "gray", 90, 0), (16, 16, "4:2:0", 50, 0), (24, 16, "4:4:4", 95, 0),
                                           (64, 48, "4:2:2", 75, 0), (32, 32, "4:2:0", 90, 1), (40, 16, "4:4:4", 75, 2),
-                                          (256, 256, "gray", 90, 0), (128, 128, "4:2:0", 75, 0)])
+                                          (256, 256, "gray", 90, 0), (128, 128, "4:2:0", 75, 0),
+                                          (64, 32, "gray", 75, "dc16"), (48, 32, "4:2:0", 50, "dc16"),
+                                          (40, 16, "4:4:4", 90, "dc16r2")])
 def test_random_entropy_data_vs_oracle(decoder, w, h, ss, q, rst):
     """Random entropy-coded bytes behind valid headers: every symbol the tables allow, in any
     order (runs past index 63, ZRL, codes longer than the LUT, magnitudes whose dequantised values
     need the exact IDCT form, paired and unpaired lookups).  Status (decoded or not) and pixels
     must match the oracle, image by image, in one batch.  rst > 0: restart intervals of rst MCUs,
     each its own random bytes followed by the expected RSTn (trailing bytes before an RSTn are
-    corrupt, trailing bytes before EOI are not)."""
-    rng = np.random.default_rng(w * 10007 + h * 101 + q + rst)
+    corrupt, trailing bytes before EOI are not).
+    "dc16[rN]": luma DC symbols rewritten to DC sizes 16, 12, 15 and (the longest code) 17 (beyond
+    baseline's 11: the reference reads up to 16 magnitude bits, parser.cpp:106-108, the oracle
+    flags a size above 16, jdoracle.c decode_block; 16 gives differences of +-32768..65535,
+    jd_kernels.hip block_rec's 17-bit DC), restart intervals of N MCUs with "rN"."""
+    dcs = isinstance(rst, str)
+    if dcs:
+        rst = int(rst[5:]) if len(rst) > 4 else 0
+    rng = np.random.default_rng(w * 10007 + h * 101 + q + rst + (7 if dcs else 0))
     hdr = jd_synth.encode(jd_synth.synth_pixels(w, h, 1, ss == "gray"), q, "4:4:4" if ss == "gray" else ss,
                           restart_blocks=rst)
+    if dcs:  # the standard luma DC table: codes 00, 010, 011, ..., 111111110 for symbols 0 .. 11
+        hdr = bytearray(hdr)
+        o = _dht_values_offset(hdr, 0, 0)
+        hdr[o:o + 3] = bytes([16, 12, 15])
+        hdr[o + 11] = 17
+        hdr = bytes(hdr)
     hd = jdamd.parse(hdr)
     head = hdr[:hd.ecs_offset]
     nseg = -(-hd.mcux * hd.mcuy // rst) if rst else 1

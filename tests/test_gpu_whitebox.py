@@ -79,8 +79,8 @@ def test_intervals_and_piece_starts(sync_decoder, name):
             own = int(sent[s]) + j * rw
             if int(pab[u]) != own and int(pab[u]) < own + rw:
                 errs.append(f"seg {s} piece {j}: region {int(pab[u])} overlaps own {own}")
-            if (int(pjoin[u]) & 0xFFFF) > (int(pjoin[u]) >> 16):
-                errs.append(f"seg {s} piece {j}: joined checkpoint {int(pjoin[u]) & 0xFFFF} of {int(pjoin[u]) >> 16}")
+            if (int(pjoin[u]) & 0xFFFF) > ((int(pjoin[u]) >> 16) & 0xFF):
+                errs.append(f"seg {s} piece {j}: joined checkpoint {int(pjoin[u]) & 0xFFFF} of {(int(pjoin[u]) >> 16) & 0xFF}")
             nm += int(pnm[u])
         if nm != len(seg["starts"]) - 1:
             errs.append(f"seg {s}: MCUs gpu {nm} want {len(seg['starts']) - 1}")
@@ -92,7 +92,8 @@ def test_intervals_and_piece_starts(sync_decoder, name):
 @pytest.mark.parametrize("name", CASES)
 def test_scan_checkpoints(sync_decoder, name):
     """Checkpoints (k_piece) sit on true MCU boundaries with the MCU and AC-entry counts from the
-    piece start, for every piece whose speculative start synchronised (the join relies on both)."""
+    piece start, for every piece whose speculative start synchronised (the join relies on both),
+    and record no error in the segment before them (kNoError; the images are valid)."""
     data = _load(name)
     try:
         sync_decoder.decode(data)
@@ -109,7 +110,7 @@ def test_scan_checkpoints(sync_decoder, name):
         starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
         for j in range(int(nsub[s])):
             u = int(ssb[s]) + j
-            ncp = int(pjoin[u]) >> 16
+            ncp = (int(pjoin[u]) >> 16) & 0xFF  # (tail count << 24 | checkpoints << 16)
             assert ncp <= 8
             b0 = int(pbit[u])
             if b0 not in starts or ncp == 0:
@@ -117,7 +118,7 @@ def test_scan_checkpoints(sync_decoder, name):
             m0, e0 = starts[b0]
             for c in range(ncp):
                 bit, mcus, ents, err = (int(x) for x in cp[u, c])
-                if bit in starts and (starts[bit][0] - m0, starts[bit][1] - e0) == (mcus, ents) and err == 0:
+                if bit in starts and (starts[bit][0] - m0, starts[bit][1] - e0) == (mcus, ents) and err == 0xFFFFFFFF:
                     checked += 1
                 else:
                     bad += 1
