@@ -229,8 +229,16 @@ constexpr uint32_t kTailErr = kNoError - 15u;
 // straddles the piece's end (<= 10 blocks x 64) and one window round past the data end (<= 272), see
 // jd_kernels.hip walk_piece, whose region guard stops a walk (as an error) before it could overrun.
 constexpr uint32_t kRegionSlack = 1040;
+// Entry quads are stored in pairs (32 bytes, one HBM write granule) into 32-byte aligned regions:
+// a lane's region line stays open for ~60 walk iterations and is written back piecemeal when the
+// L2 (4 MB per XCD, ~32 K lanes each streaming into their own lines) evicts it, each 16-byte quad
+// costing a 32-byte write (C2: k_piece WRITE_SIZE 3.98 -> 2.30 GB per launch).
+#ifndef JD_ENT_PAIR
+#define JD_ENT_PAIR 1
+#endif
+constexpr uint32_t kRegionAlign = JD_ENT_PAIR ? 8u : 4u;  // words
 JD_HD inline uint32_t region_words(uint32_t plen, uint32_t div = 2u) {
-    return ((plen + div - 1u) / div + kRegionSlack + 3u) & ~3u;
+    return ((plen + div - 1u) / div + kRegionSlack + kRegionAlign - 1u) & ~(kRegionAlign - 1u);
 }
 
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile

@@ -737,6 +737,13 @@ constexpr uint32_t kRoundItems = (kWin * 8 + 31) / 2 + 4;
 static_assert(kRegionSlack >= 640 + kRoundItems + 2, "region slack: straddling MCU + one round past the data");
 
 constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte aligned)
+// Block records staged four at a time in a per-lane LDS ring and stored as one 16-byte quad (a
+// record at a time, 4 bytes, each store became its own write-back: 1.1 GB written for 0.2 GB of
+// records on C2).  16 bytes per lane is what two 512-lane workgroups per CU leave with 4 tables.
+#ifndef JD_REC_RING
+#define JD_REC_RING 1
+#endif
+constexpr int kRecRingWords = JD_REC_RING ? 4 : 0;
 #ifndef JD_EXTRA_LDS
 #define JD_EXTRA_LDS 0  // experiment builds: extra dynamic LDS per piece workgroup (lowers occupancy)
 #endif
@@ -744,10 +751,11 @@ constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte alig
 // batch's k_piece / k_idct_color waves instead of waiting for a whole CU's LDS.
 constexpr int kRedoThreads = 64;
 static_assert(kPieceThreads % kRedoThreads == 0, "a redo workgroup lies inside one piece workgroup");
-constexpr size_t kRedoLds = size_t(kRedoThreads) * (row_words(kWin) + kRingWords) * 4;
+constexpr size_t kRedoLds = size_t(kRedoThreads) * (row_words(kWin) + kRingWords + kRecRingWords) * 4;
 static_assert((kRedoThreads * row_words(kWin) * 4) % 32 == 0, "redo rings must start 32-byte aligned (ring_put)");
 size_t piece_lds_bytes(uint32_t max_slots, int nt) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(nt) * (row_words(kWin) + kRingWords) * 4 + JD_EXTRA_LDS;
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(nt) * (row_words(kWin) + kRingWords + kRecRingWords) * 4 +
+           JD_EXTRA_LDS;
 }
 // Batches with fewer piece lanes than this run k_piece in 64-lane workgroups.
 #ifndef JD_SMALL_PIECE_LANES
@@ -756,6 +764,8 @@ size_t piece_lds_bytes(uint32_t max_slots, int nt) {
 constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
 static_assert((kPieceThreads * row_words(kWin) * 4) % 32 == 0 && (64 * row_words(kWin) * 4) % 32 == 0 && sizeof(HuffLut) % 32 == 0 && kRingWords == 8,
               "rings must start 32-byte aligned (ring_put)");
+static_assert((kPieceThreads * (row_words(kWin) + kRingWords) * 4) % 16 == 0 && (64 * (row_words(kWin) + kRingWords) * 4) % 16 == 0,
+              "record rings must start 16-byte aligned");
 
 typedef const __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return uint32_t(size_t((lds_u32*)p)); }
@@ -964,7 +974,7 @@ __device__ __forceinline__ void st_ent(uint4* p, const uint4& v) {
 
 template <int KIND, bool GL = false>
 __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
-                                           uint32_t* row, uint32_t* ring, bool active_in, PWalk& W, CpRec* cp,
+                                           uint32_t* row, uint32_t* ring, uint32_t* rring, bool active_in, PWalk& W, CpRec* cp,
                                            uint32_t cp_bits, const uint32_t (&cpb)[kCpMax]) {
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
@@ -1022,8 +1032,35 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // completed quad fq straight from the ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
     uint32_t st_wit = 0, st_lit = 0, st_rare = 0, st_rare_w = 0, st_rounds = 0, st_mend_w = 0, st_sym = 0;
+#if JD_REC_RING
+    // block record k goes to ring word 3 - (k & 3), so that the ring reads as the records' memory
+    // order (descending from rec_top); group fr (records 4fr .. 4fr + 3) is stored when complete,
+    // at most one group pending (a block takes >= 2 iterations, a flush comes every other one)
+    const uint32_t rrb = lds_addr(rring);  // 16-byte aligned
+    uint32_t fr = 0;  // record groups stored
+#else
     uint32_t prec = 0, pblk = 0;
     bool pend_b = false;
+#endif
+#if JD_ENT_PAIR
+    // an even quad is held in registers and stored with the odd one after it: 32 contiguous bytes
+    uint4 hq = {0u, 0u, 0u, 0u};
+#define JD_FLUSH_Q()                                                                                   \
+    do {                                                                                               \
+        if (fq < (ent2 >> 4)) {                                                                        \
+            const uint4 q_ = *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u));                   \
+            if (fq & 1u) {                                                                             \
+                if (!(JD_ABL & 8) || ent2 == 0x7FFFFFFFu) {                                            \
+                    st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);                          \
+                    st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), q_);                               \
+                }                                                                                      \
+            } else {                                                                                   \
+                hq = q_;                                                                               \
+            }                                                                                          \
+            fq++;                                                                                      \
+        }                                                                                              \
+    } while (0)
+#else
 #define JD_FLUSH_Q()                                                                                   \
     do {                                                                                               \
         if (fq < (ent2 >> 4)) {                                                                        \
@@ -1032,11 +1069,23 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             fq++;                                                                                      \
         }                                                                                              \
     } while (0)
+#endif
+#if JD_REC_RING
+#define JD_FLUSH_B()                                                                                   \
+    do {                                                                                               \
+        if (fr < (blk >> 2)) {                                                                         \
+            if (!(JD_ABL & 16) || ent2 == 0x7FFFFFFFu)                                                 \
+                st_ent(reinterpret_cast<uint4*>(rec_top - (4u * fr + 3u)), *reinterpret_cast<const uint4*>(rring)); \
+            fr++;                                                                                      \
+        }                                                                                              \
+    } while (0)
+#else
 #define JD_FLUSH_B()                                                     \
     do {                                                                 \
         if (pend_b && (!(JD_ABL & 16) || ent2 == 0x7FFFFFFFu)) rec_top[-int(pblk)] = prec; \
         pend_b = false;                                                  \
     } while (0)
+#endif
     uint32_t pos = W.start;  // == R.bit(): the stream bit of the next symbol
     // (re-walks are short and run few lanes: one window ahead keeps their registers down)
     constexpr int kGroup = KIND == kSpec ? kWinGroup : 1;
@@ -1123,6 +1172,16 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             R.skip(L);
             pos += L;
             const bool fin = zn >= 63u;
+#if JD_REC_RING
+            if (fin)
+                *(__attribute__((address_space(3))) uint32_t*)size_t(rrb | ((~blk & 3u) << 2)) =
+                    block_rec(ent2 - ent_blk2, dcd, esc_blk);
+            blk += fin ? 1u : 0u;
+            if ((it & 1u) == 0u) {
+                JD_FLUSH_Q();
+                JD_FLUSH_B();
+            }
+#else
             prec = fin ? block_rec(ent2 - ent_blk2, dcd, esc_blk) : prec;
             pblk = fin ? blk : pblk;
             pend_b = pend_b || fin;
@@ -1131,6 +1190,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 JD_FLUSH_B();
             }
             blk += fin ? 1u : 0u;
+#endif
             ent_blk2 = fin ? ent2 : ent_blk2;
             esc_blk = fin ? 0u : esc_blk;
             z = fin ? 0u : zn;
@@ -1215,8 +1275,16 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     }
 #undef JD_FLUSH_Q
 #undef JD_FLUSH_B
+#if JD_ENT_PAIR
+    if (fq & 1u) st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);  // a held quad
+#endif
     if (ent2 & 15u)  // the last, partial quad (every complete one is stored; the region has room for all of it)
         st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)));
+#if JD_REC_RING
+    // the last, partial record group (every complete one is stored: the window round's flush)
+    if (!(JD_ABL & 16))
+        for (uint32_t r = 0; r < (blk & 3u); r++) rec_top[-int(4u * fr + r)] = rring[3u - r];
+#endif
     W.m_start = m_start;
     W.m_end = m_end;
     W.mcus = mcus;
@@ -1386,7 +1454,8 @@ __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     const uint32_t none[kCpMax] = {};
     walk_piece<kSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWin),
-                      s_rows + NT * row_words(kWin) + threadIdx.x * kRingWords, live, W, cp,
+                      s_rows + NT * row_words(kWin) + threadIdx.x * kRingWords,
+                      s_rows + NT * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords, live, W, cp,
                       max(1u, P.plen / kCpMax), none);
     if (!valid) return;
     if (!live) {  // as a warm-up that runs past the data: no piece, an error at its first MCU
@@ -1417,7 +1486,7 @@ __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
 template <bool GL>
 __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceGeo& P, uint32_t s, uint32_t u,
                                uint32_t expect, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp, uint32_t* row,
-                               uint32_t* ring, bool need) {
+                               uint32_t* ring, uint32_t* rring, bool need) {
     CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
     uint32_t ncp = 0, base = P.own, stail = 0;
     CpRec tot{0u, 0u, 0u, kNoError};
@@ -1440,7 +1509,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
     W.stop_at = piece_stop(P);
     W.reg = S.eimg + base;
     W.rw = P.rw;
-    walk_piece<kRedo, GL>(S, s_lutw, dcp, acp, row, ring, need, W, cp, 0xFFFFFFFFu, cpb);
+    walk_piece<kRedo, GL>(S, s_lutw, dcp, acp, row, ring, rring, need, W, cp, 0xFFFFFFFFu, cpb);
     if (!need) return 0;
     uint32_t end = W.m_end, mcus = W.mcus, ents = W.ents, emcu = W.emcu, tail = W.tail;
     if (W.join) {  // (checkpoints lie before the last byte: the tail, if any, is the speculative walk's)
@@ -1499,6 +1568,7 @@ __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
     table_slots(ts, S, dcp, acp);
     redo_piece<true>(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
                      s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
+                     s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords,
                      need);
 }
 
@@ -1659,6 +1729,7 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
     table_slots(ts, S, dcp, acp);
     uint32_t* const row = s_rows + threadIdx.x * row_words(kWin);
     uint32_t* const ring = s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords;
+    uint32_t* const rring = s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords;
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const bool final_seg = seg_is_final(b, s);  // trailing bytes after its last MCU are ignored
     bool bad = false, done = false;
@@ -1673,7 +1744,7 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
         uint32_t pend = b.piece_end[u];
         if (b.piece_bit[u] != expect) {  // the start had not synchronised: re-walk from the truth
             const PieceGeo P = piece_geo(b, S, s, u);
-            pend = redo_piece<true>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, true);
+            pend = redo_piece<true>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, rring, true);
         }
         const uint32_t pm = b.piece_nmcu[u], em = b.piece_emcu[u];
         const bool last = j + 1 == n || (final_seg && mcu_run + pm >= nmcu_seg);

@@ -533,7 +533,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             d.sub_cap = uint32_t(piece_slots(d.len - d.ecs_off, d.nseg, P.piece_bits));
             d.entry_base = entry_cursor;
             d.entry_cap = uint32_t(entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces, d.rw_div));
-            entry_cursor += align_up(size_t(d.entry_cap), 4);
+            entry_cursor += align_up(size_t(d.entry_cap), kRegionAlign);
             sub += d.sub_cap;
             for (uint32_t k = 0; k < d.nseg; k++) P.chain_seg.push_back(d.seg_base + k);
         }

@@ -30,7 +30,7 @@ pytestmark = pytest.mark.gpu
 def region_words(plen, div=2):
     """jd_internal.hpp region_words: one piece's AC-entry region in 32-bit words (div: the image's
     jd_plan.cpp region_divisor; 4 for the Annex K tables, tests/test_sanitize.py)."""
-    return ((plen + div - 1) // div + 1040 + 3) & ~3
+    return ((plen + div - 1) // div + 1040 + 7) & ~7  # kRegionAlign: 8 words
 
 
 def entry_words(data, h, piece_bits=16384, spare=None, div=2):

@@ -63,7 +63,7 @@ def test_intervals_and_piece_starts(sync_decoder, name):
             errs.append(f"seg {s}: pieces gpu {nsub[s]} want {want_n}")
             continue
         plen = -(-seg["bits"] // want_n)
-        rw = ((plen + div - 1) // div + 1040 + 3) // 4 * 4  # jd_internal.hpp region_words
+        rw = ((plen + div - 1) // div + 1040 + 7) // 8 * 8  # jd_internal.hpp region_words (kRegionAlign 8)
         starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
         nm = 0
         for j in range(want_n):
