@@ -237,8 +237,14 @@ def gather_counters(local, world: int):
 # ---------------------------------------------------------------------------------------------
 # measurement helpers
 # ---------------------------------------------------------------------------------------------
+def _profile_order(path: str):
+    """Run tags go r03a .. r03z, r03aa .. : newer = longer, then later in the alphabet."""
+    tag = os.path.basename(path).split("_")[0]
+    return tag[:3], len(tag), tag
+
+
 def newest_profile(pattern: str, config: str, kernel: str):
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=_profile_order, reverse=True):
         with open(f) as fh:
             t = json.load(fh)
         if t.get("config") == config and kernel in t.get("kernels", {}):
