@@ -4,7 +4,9 @@
 
 Batches of synthetic JPEGs with random size (1 .. 2000 x 1 .. 1200, mostly small), sampling layout
 (4:4:4 / 4:2:2 / 4:2:0 / 4:4:0 / grayscale), quality (20 .. 100), restart interval (none, MCU rows,
-MCU counts) and, for about a fifth of them, bit flips in the entropy-coded data, are decoded in one
+MCU counts), encoder (tools/jdenc.c with the Annex K tables, or Pillow with its standard or its
+optimised per-image Huffman tables; Pillow has no 4:4:0) and, for about a fifth of them, bit flips in
+the entropy-coded data, are decoded in one
 batch call on the GPU through each entropy-decode path of the library (default, "sync": 1024-bit
 pieces with most speculative starts failing, "lanes": one lane per restart interval, "full": the
 full-batch piece geometry whatever the batch size; --fancy: with libjpeg fancy upsampling) and compared
@@ -39,7 +41,9 @@ def make_image(args):
     p = args
     gray = p["ss"] == "gray"
     px = jd_synth.synth_pixels(p["w"], p["h"], p["seed"], gray)
-    data = jd_synth.encode(px, p["q"], "4:4:4" if gray else p["ss"], p["rows"], p["blocks"])
+    enc = p.get("enc", "jdenc")  # jdenc | pil | pil-opt
+    data = jd_synth.encode(px, p["q"], "4:4:4" if gray else p["ss"], p["rows"], p["blocks"],
+                           optimize=enc == "pil-opt", encoder="jdenc" if enc == "jdenc" else "pil")
     if p["flips"]:
         rng = np.random.default_rng(p["seed"] ^ 0x5EED)
         d = bytearray(data)
@@ -62,15 +66,19 @@ def oracle_digest_fancy(data):
     return oracle_digest(data, True)
 
 
-def draw(rng, seed):
+def draw(rng, seed, pil=False):
     small = rng.random() < 0.85
     w = int(rng.integers(1, 400 if small else 2001))
     h = int(rng.integers(1, 300 if small else 1201))
     r = rng.random()
     rows, blocks = (0, 0) if r < 0.4 else ((int(rng.integers(1, 4)), 0) if r < 0.7 else (0, int(rng.integers(1, 12))))
-    return {"seed": int(seed), "w": w, "h": h, "ss": LAYOUTS[int(rng.integers(0, len(LAYOUTS)))],
-            "q": int(rng.choice([20, 35, 50, 75, 90, 95, 100])), "rows": rows, "blocks": blocks,
-            "flips": int(rng.integers(1, 4)) if rng.random() < 0.2 else 0}
+    d = {"seed": int(seed), "w": w, "h": h, "ss": LAYOUTS[int(rng.integers(0, len(LAYOUTS)))],
+         "q": int(rng.choice([20, 35, 50, 75, 90, 95, 100])), "rows": rows, "blocks": blocks,
+         "flips": int(rng.integers(1, 4)) if rng.random() < 0.2 else 0}
+    if pil:
+        e = rng.random()
+        d["enc"] = "jdenc" if e < 0.6 or d["ss"] == "4:4:0" else ("pil" if e < 0.75 else "pil-opt")
+    return d
 
 
 def main():
@@ -84,6 +92,7 @@ def main():
     ap.add_argument("--workers", type=int, default=12)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
     ap.add_argument("--fancy", action="store_true", help="libjpeg fancy upsampling (its oracle: jdoracle fancy=True)")
+    ap.add_argument("--pil", action="store_true", help="also Pillow-encoded images (standard and optimised tables)")
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
     paths = ["auto", "sync", "lanes", "full"]
@@ -101,7 +110,7 @@ def main():
         while time.time() < t_end and len(fails) < 20:
             params = []
             for _ in range(a.batch):
-                params.append(draw(rng, seed))
+                params.append(draw(rng, seed, a.pil))
                 seed += 1
             datas = list(pool.map(make_image, params, chunksize=4))
             ref = list(pool.map(oracle_digest_fancy if a.fancy else oracle_digest, datas, chunksize=4))
@@ -124,7 +133,8 @@ def main():
     for d in decs.values():
         d.close()
     res = {"images": n_img, "decoded_equal_or_checked": n_ok, "corrupt_status_checked": n_bad_status,
-           "batches": it, "mismatches": fails, "seed": a.seed, "minutes": a.minutes, "fancy": a.fancy, "paths": paths}
+           "batches": it, "mismatches": fails, "seed": a.seed, "minutes": a.minutes, "fancy": a.fancy, "pil": a.pil,
+           "paths": paths}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
