@@ -1025,11 +1025,13 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // AC entries are 16-bit slots (an escaped value takes two).  Stores are deferred and issued
     // every other loop iteration, so that one store instruction carries many lanes.  An iteration
     // emits at most two slots (a pair of AC symbols, or one escaped value: pairs never escape), and
-    // a block takes at least two iterations (its DC symbol never pairs), so flushing one quad (8
-    // slots) and one block record every two iterations keeps fewer than 16 slots pending: one ring
-    // of two quads and one pending record suffice.  Slots go to the ring at slot ent & 15 (a symbol that emits nothing
-    // writes the next free slot without advancing, so it is overwritten); a flush stores the
-    // completed quad fq straight from the ring.
+    // a block takes at least two iterations (its DC symbol never pairs), so taking one quad (8
+    // slots) every two iterations keeps fewer than 16 slots pending: one ring of two quads
+    // suffices.  Slots go to the ring at slot ent & 15 (a symbol that emits nothing writes the next
+    // free slot without advancing, so it is overwritten).  With JD_ENT_PAIR an even quad is copied
+    // from the ring into registers when complete and stored together with the odd quad after it
+    // (32 bytes: one HBM write granule); block records go four at a time through their own ring
+    // (JD_REC_RING).
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
     uint32_t st_wit = 0, st_lit = 0, st_rare = 0, st_rare_w = 0, st_rounds = 0, st_mend_w = 0, st_sym = 0;
 #if JD_REC_RING
@@ -1038,6 +1040,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // at most one group pending (a block takes >= 2 iterations, a flush comes every other one)
     const uint32_t rrb = lds_addr(rring);  // 16-byte aligned
     uint32_t fr = 0;  // record groups stored
+    uint4* rgp = reinterpret_cast<uint4*>(rec_top - 3u);  // where group fr goes (a pointer stepped down)
 #else
     uint32_t prec = 0, pblk = 0;
     bool pend_b = false;
@@ -1048,14 +1051,13 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
 #define JD_FLUSH_Q()                                                                                   \
     do {                                                                                               \
         if (fq < (ent2 >> 4)) {                                                                        \
-            const uint4 q_ = *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u));                   \
-            if (fq & 1u) {                                                                             \
+            if (fq & 1u) { /* (each branch reads its ring quad at a fixed address) */                   \
                 if (!(JD_ABL & 8) || ent2 == 0x7FFFFFFFu) {                                            \
                     st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);                          \
-                    st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), q_);                               \
+                    st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u)); \
                 }                                                                                      \
             } else {                                                                                   \
-                hq = q_;                                                                               \
+                hq = *reinterpret_cast<const uint4*>(ring);                                            \
             }                                                                                          \
             fq++;                                                                                      \
         }                                                                                              \
@@ -1075,7 +1077,8 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     do {                                                                                               \
         if (fr < (blk >> 2)) {                                                                         \
             if (!(JD_ABL & 16) || ent2 == 0x7FFFFFFFu)                                                 \
-                st_ent(reinterpret_cast<uint4*>(rec_top - (4u * fr + 3u)), *reinterpret_cast<const uint4*>(rring)); \
+                st_ent(rgp, *reinterpret_cast<const uint4*>(rring));                                   \
+            rgp--;                                                                                     \
             fr++;                                                                                      \
         }                                                                                              \
     } while (0)
