@@ -906,7 +906,11 @@ struct TabSpace<true> {
 // each, so the count fits its 7 bits.
 constexpr uint32_t kRecEsc = 1u << 17;
 __device__ __forceinline__ uint32_t block_rec(uint32_t cnt2, int dc, uint32_t esc) {
-    return ((cnt2 << 17) | esc) | (uint32_t(dc) & 0x1FFFFu);
+    // one v_bfi_b32 for the DC field (the compiler's and + or3 cost two; the mask in an SGPR:
+    // VOP3 takes no literal on gfx9)
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x1FFFFu), "v"(dc), "v"((cnt2 << 17) | esc));
+    return r;
 }
 __device__ __forceinline__ uint32_t record_cnt(uint32_t r) { return r >> 18; }
 __device__ __forceinline__ bool record_esc(uint32_t r) { return (r & kRecEsc) != 0; }
@@ -1176,10 +1180,16 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             pos += L;
             const bool fin = zn >= 63u;
 #if JD_REC_RING
-            if (fin)
+            // the block's end: its record to the ring and the per-block counters, in the branch the
+            // record store needs anyway (exec-masked increments instead of select + add outside it)
+            if (fin) {
                 *(__attribute__((address_space(3))) uint32_t*)size_t(rrb | ((~blk & 3u) << 2)) =
                     block_rec(ent2 - ent_blk2, dcd, esc_blk);
-            blk += fin ? 1u : 0u;
+                blk++;
+                b3 += 3u;
+                ent_blk2 = ent2;
+                esc_blk = 0u;
+            }
             if ((it & 1u) == 0u) {
                 JD_FLUSH_Q();
                 JD_FLUSH_B();
@@ -1193,11 +1203,11 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 JD_FLUSH_B();
             }
             blk += fin ? 1u : 0u;
-#endif
             ent_blk2 = fin ? ent2 : ent_blk2;
             esc_blk = fin ? 0u : esc_blk;
-            z = fin ? 0u : zn;
             b3 += fin ? 3u : 0u;
+#endif
+            z = fin ? 0u : zn;
             // (a stalled rare lane keeps its table: its symbol, DC or AC, is still ahead)
             tab = (rare && !rare_now) ? tab : lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
             // MCU end: the common case only counts; the branch is taken at the next threshold
