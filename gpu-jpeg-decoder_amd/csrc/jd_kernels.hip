@@ -1140,7 +1140,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             const bool pr = (lo & kLoPair) && zn < 63u;
             const uint32_t zn2 = zn + __builtin_amdgcn_ubfe(hi, 12u, 7u);
             ring_put(ringb, ent2, (uint32_t(int(hi) >> 23) << 6) | zn2);
-            ent2 += ((lo & kLoE2) && zn2 < 64u) ? 2u : 0u;
+            // E2 (bit 7 of lo) and zn2 < 64 (zn2 <= 127: bit 6 clear) as bit 7 of lo & ~(zn2 << 1)
+            uint32_t zs = zn2 << 1;
+            asm("" : "+v"(zs));  // (else not + shift + and instead of shift + one v_bitop3)
+            uint32_t e2 = __builtin_amdgcn_ubfe(lo & ~zs, 7u, 1u);
+            asm("" : "+v"(e2));  // keeps bfe + lshl_add
+            ent2 += e2 << 1;
             L = pr ? __builtin_amdgcn_ubfe(hi, 19u, 4u) : L;
             zn = pr ? zn2 : zn;
             // A rare entry consumes nothing in the common path above (L = 0, no emit, no pair,
