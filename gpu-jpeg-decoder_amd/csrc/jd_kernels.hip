@@ -744,6 +744,8 @@ constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte alig
 #define JD_REC_RING 1
 #endif
 constexpr int kRecRingWords = JD_REC_RING ? 4 : 0;
+// walk_piece counts blocks in steps of 4 with the ring (its slot address rrb | (~blk & 12): one op)
+constexpr uint32_t kBlkStep = JD_REC_RING ? 4u : 1u;
 #ifndef JD_EXTRA_LDS
 #define JD_EXTRA_LDS 0  // experiment builds: extra dynamic LDS per piece workgroup (lowers occupancy)
 #endif
@@ -901,17 +903,21 @@ struct TabSpace<true> {
 
 // Block record in a piece's region: AC-entry slot count (<= 126) << 18 | escape flag << 17 | the
 // DC difference, 17-bit two's complement (a DC size is <= 16 bits, jd_internal.hpp lut_entry: the
-// difference lies within +-65535).  esc: 0 or kRecEsc; cnt2 = 2 x the slot count.  A block stores
-// at most 63 coefficients (each at a zig-zag index < 64, strictly increasing), of at most two slots
-// each, so the count fits its 7 bits.
+// difference lies within +-65535).  A block stores at most 63 coefficients (each at a zig-zag index
+// < 64, strictly increasing), of at most two slots each, so the count fits its 7 bits.
+// cnt2e = 2 x the slot count + the escape flag: the walks keep slot counts doubled (ent2, always
+// even) and mark a block with an escaped value by making its start ent_blk2 odd and one lower
+// (esc_mark), so that ent2 - ent_blk2 = 2 x count + 1 and its shift puts the flag at bit 17.
 constexpr uint32_t kRecEsc = 1u << 17;
-__device__ __forceinline__ uint32_t block_rec(uint32_t cnt2, int dc, uint32_t esc) {
+__device__ __forceinline__ uint32_t block_rec(uint32_t cnt2e, int dc) {
     // one v_bfi_b32 for the DC field (the compiler's and + or3 cost two; the mask in an SGPR:
     // VOP3 takes no literal on gfx9)
     uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x1FFFFu), "v"(dc), "v"((cnt2 << 17) | esc));
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x1FFFFu), "v"(dc), "v"(cnt2e << 17));
     return r;
 }
+// (idempotent: an already odd start stays as it is)
+__device__ __forceinline__ uint32_t esc_mark(uint32_t ent_blk2) { return (ent_blk2 - 1u) | 1u; }
 __device__ __forceinline__ uint32_t record_cnt(uint32_t r) { return r >> 18; }
 __device__ __forceinline__ bool record_esc(uint32_t r) { return (r & kRecEsc) != 0; }
 __device__ __forceinline__ int record_dc(uint32_t r) { return int32_t(r << 15) >> 15; }
@@ -1023,8 +1029,9 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     uint32_t thr = min(min(W.stop_at, end_thr), nxt0);
     // errs: bit 0, an error in the current MCU; bits 1..: MCUs completed that began in the last byte
     uint32_t mcus = 0, emcu = kNoError, errs = 0;
-    // ent2 / ent_blk2: 2 x the slot counts (the ring's byte offsets); esc_blk: the record's escape bit
-    uint32_t ent2 = 0, ent_blk2 = 0, blk = 0, esc_blk = 0;
+    // ent2 / ent_blk2: 2 x the slot counts (the ring's byte offsets; ent_blk2 odd: the block has an
+    // escaped value, block_rec); blk: blocks x kBlkStep
+    uint32_t ent2 = 0, ent_blk2 = 0, blk = 0;
     int dcd = 0;
     // AC entries are 16-bit slots (an escaped value takes two).  Stores are deferred and issued
     // every other loop iteration, so that one store instruction carries many lanes.  An iteration
@@ -1079,7 +1086,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
 #if JD_REC_RING
 #define JD_FLUSH_B()                                                                                   \
     do {                                                                                               \
-        if (fr < (blk >> 2)) {                                                                         \
+        if (fr < (blk >> 4)) {                                                                         \
             if (!(JD_ABL & 16) || ent2 == 0x7FFFFFFFu)                                                 \
                 st_ent(rgp, *reinterpret_cast<const uint4*>(rring));                                   \
             rgp--;                                                                                     \
@@ -1174,7 +1181,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 const bool big = entry_big(val);
                 ring_put(ringb, ent2, entry16(val, zn, big));
                 ring_put(ringb, ent2 + 2u, uint32_t(val));
-                esc_blk |= (emit && big) ? kRecEsc : 0u;
+                ent_blk2 = (emit && big) ? esc_mark(ent_blk2) : ent_blk2;
                 ent2 += emit ? (big ? 4u : 2u) : 0u;
                 if (e & kEntBad) {  // the next MCU end takes the branch below
                     errs |= 1u;
@@ -1188,19 +1195,18 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             // the block's end: its record to the ring and the per-block counters, in the branch the
             // record store needs anyway (exec-masked increments instead of select + add outside it)
             if (fin) {
-                *(__attribute__((address_space(3))) uint32_t*)size_t(rrb | ((~blk & 3u) << 2)) =
-                    block_rec(ent2 - ent_blk2, dcd, esc_blk);
-                blk++;
+                *(__attribute__((address_space(3))) uint32_t*)size_t(rrb | (~blk & 12u)) =
+                    block_rec(ent2 - ent_blk2, dcd);
+                blk += 4u;
                 b3 += 3u;
                 ent_blk2 = ent2;
-                esc_blk = 0u;
             }
             if ((it & 1u) == 0u) {
                 JD_FLUSH_Q();
                 JD_FLUSH_B();
             }
 #else
-            prec = fin ? block_rec(ent2 - ent_blk2, dcd, esc_blk) : prec;
+            prec = fin ? block_rec(ent2 - ent_blk2, dcd) : prec;
             pblk = fin ? blk : pblk;
             pend_b = pend_b || fin;
             if ((it & 1u) == 0u) {
@@ -1209,7 +1215,6 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             }
             blk += fin ? 1u : 0u;
             ent_blk2 = fin ? ent2 : ent_blk2;
-            esc_blk = fin ? 0u : esc_blk;
             b3 += fin ? 3u : 0u;
 #endif
             z = fin ? 0u : zn;
@@ -1275,7 +1280,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             }
             active = false;
         }
-        if (active && (ent2 + 2u) / 4u + blk + kRoundItems > W.rw) {  // never for a valid stream (region bound)
+        if (active && (ent2 + 2u) / 4u + blk / kBlkStep + kRoundItems > W.rw) {  // never for a valid stream (region bound)
             m_end = R.bit();
             emcu = min(emcu, mcus);
             active = false;
@@ -1301,7 +1306,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
 #if JD_REC_RING
     // the last, partial record group (every complete one is stored: the window round's flush)
     if (!(JD_ABL & 16))
-        for (uint32_t r = 0; r < (blk & 3u); r++) rec_top[-int(4u * fr + r)] = rring[3u - r];
+        for (uint32_t r = 0; r < ((blk >> 2) & 3u); r++) rec_top[-int(4u * fr + r)] = rring[3u - r];
 #endif
     W.m_start = m_start;
     W.m_end = m_end;
