@@ -647,7 +647,11 @@ def main():
             "images_per_s": tot_img / t_max,
             "jpeg_MB_per_s": tot_bytes / t_max / 1e6,
             "ecs_MB_per_s": tot_ecs / t_max / 1e6,
-            "roofline": {"bound": "valu" if vb and vb["busy_frac"] > 0.7 else "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+            # the roof that binds: VALU issue when the committed SQ profile shows the SIMDs busy, HBM
+            # when the byte stream is near its peak, else neither (a latency- / parallelism-bound launch,
+            # e.g. C1's one image on a few CUs)
+            "roofline": {"bound": ("valu" if vb and vb["busy_frac"] > 0.7 else
+                                   "hbm" if achieved / HBM_PEAK_GBS > 0.5 else "latency"), "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,

@@ -5,8 +5,7 @@
 #   2. rocprofv3 --kernel-trace --stats over serialized steps     -> gpurun_out/TAG/<cfg>_stats/
 #      (--no-pipeline: kernels of consecutive batches do not overlap, so the per-kernel averages
 #      compare with the bench line's serialized hipEvent pass)
-#   3. PMC passes, one counter group per run, kernel-trace only: FETCH_SIZE, WRITE_SIZE, and (C2,
-#      C5) the SQ groups of tools/r02_sq.sh                    -> gpurun_out/TAG/<cfg>_{fetch,write,sq}/
+#   3. PMC passes, one counter group per run, kernel-trace only: FETCH_SIZE, WRITE_SIZE, and the SQ groups of tools/r02_sq.sh                    -> gpurun_out/TAG/<cfg>_{fetch,write,sq}/
 # tools/round_summary.py then writes profiles/TAG_*.  Every step has its own time limit; the script
 # stops at the first failure.
 set -e
@@ -29,7 +28,7 @@ for c in $cfgs; do
      python3 $root/bench.py --config $c $short > ${c}_fetch.log 2>&1)
   (cd $out && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d ${c}_write -o p -f csv -- \
      python3 $root/bench.py --config $c $short > ${c}_write.log 2>&1)
-  if [ "$c" = c2 ] || [ "$c" = c5 ]; then
+  if [ "$c" = c2 ] || [ "$c" = c5 ] || [ "$c" = c3 ] || [ "$c" = c1 ]; then
     (cd $out && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU \
        SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d ${c}_sq/p1 -o p -f csv -- \
        python3 $root/bench.py --config $c $short > ${c}_sq1.log 2>&1)
