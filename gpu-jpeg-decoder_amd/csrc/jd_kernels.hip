@@ -2247,6 +2247,9 @@ __device__ __forceinline__ int dot2(uint32_t a, uint32_t k, int c) {
 #ifndef JD_HALVES
 #define JD_HALVES 1
 #endif
+#ifndef JD_HALVES444
+#define JD_HALVES444 1
+#endif
 #ifndef JD_QUAD_SKIP
 #define JD_QUAD_SKIP 1
 #endif
@@ -2620,14 +2623,16 @@ __device__ __forceinline__ void row_rgb_packed(const uint4& Yq, const uint32_t (
 // The 4:2:0 tail step: 4 pixels of two rows that share their two chroma samples (both chroma
 // planes subsampled 2x2).  A 4:2:0 tile of 10 MCUs has 160 8-pixel row-pair groups, two and a half
 // lane-steps: the last half step is done as 64 4-pixel halves, so no lane idles (k_idct_color).
+// LO: terms in the low halves (both pixels of a word share their sample), else one term per pixel
+template <bool LO = true>
 __device__ __forceinline__ void rgb4_packed(const uint2& Yq, const uint32_t (&TR)[2], const uint32_t (&TG)[2],
                                             const uint32_t (&TB)[2], uint32_t (&w)[3]) {
     const uint32_t Y[2] = {Yq.x, Yq.y};
-    uint32_t RG[2], B[2];  // (terms in the low halves: both pixels of a word share their sample)
+    uint32_t RG[2], B[2];
 #pragma unroll
     for (int u = 0; u < 2; u++) {
-        RG[u] = pk_sat_add_hi<true>(pk_sat_add<true>(Y[u], TR[u]), Y[u], TG[u]);
-        B[u] = pk_sat_add<true>(Y[u], TB[u]);
+        RG[u] = pk_sat_add_hi<LO>(pk_sat_add<LO>(Y[u], TR[u]), Y[u], TG[u]);
+        B[u] = pk_sat_add<LO>(Y[u], TB[u]);
     }
     w[0] = __builtin_amdgcn_perm(B[0], RG[0], 0x01040200u);                                            // r0 g0 b0 r1
     w[1] = __builtin_amdgcn_perm(RG[1], __builtin_amdgcn_perm(B[0], RG[0], 0x0c0c0503u), 0x06040100u);  // g1 b1 r2 g2
@@ -2678,6 +2683,40 @@ __device__ __forceinline__ void colour4x2(const int16_t* s_pl, uint32_t yoff, ui
     if (__any(ex != 0u)) {
         fix_g4_exact(Y0, cb, cr, ex, w0);
         fix_g4_exact(Y1, cb, cr, ex, w1);
+    }
+}
+
+// The 4:4:4 tail step: 4 pixels of one row, one chroma sample each.  A 4:4:4 tile of 20 MCUs has
+// 160 8-pixel groups, two and a half lane-steps: the last half step is done as 64 4-pixel halves.
+__device__ __forceinline__ void colour4x1(const int16_t* s_pl, uint32_t yoff, uint32_t cboff, uint32_t croff,
+                                          uint32_t (&w)[3]) {
+    const uint2 cbq = *reinterpret_cast<const uint2*>(s_pl + cboff);
+    const uint2 crq = *reinterpret_cast<const uint2*>(s_pl + croff);
+    const int cb[4] = {int(int16_t(cbq.x & 0xFFFFu)), int32_t(cbq.x) >> 16, int(int16_t(cbq.y & 0xFFFFu)), int32_t(cbq.y) >> 16};
+    const int cr[4] = {int(int16_t(crq.x & 0xFFFFu)), int32_t(crq.x) >> 16, int(int16_t(crq.y & 0xFFFFu)), int32_t(crq.y) >> 16};
+    ChromaTerms t[4];
+    uint32_t ex = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        t[u] = chroma_terms(cb[u], cr[u]);
+        ex |= t[u].exact ? (1u << u) : 0u;
+    }
+    const uint32_t TR[2] = {pair16(t[0].r, t[1].r), pair16(t[2].r, t[3].r)};
+    const uint32_t TG[2] = {pair16(t[0].g, t[1].g), pair16(t[2].g, t[3].g)};
+    const uint32_t TB[2] = {pair16(t[0].b, t[1].b), pair16(t[2].b, t[3].b)};
+    const uint2 Y0 = *reinterpret_cast<const uint2*>(s_pl + yoff);
+    rgb4_packed<false>(Y0, TR, TG, TB, w);
+    if (__any(ex != 0u)) {
+        const uint32_t Y[2] = {Y0.x, Y0.y};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if ((ex >> j) & 1u) {
+                const int y = (j & 1) ? int32_t(Y[j >> 1]) >> 16 : int(int16_t(Y[j >> 1] & 0xFFFFu));
+                const int g = color_g_exact(y, cb[j], cr[j]);
+                const int byte = 3 * j + 1;
+                w[byte >> 2] = (w[byte >> 2] & ~(0xFFu << (8 * (byte & 3)))) | (uint32_t(g) << (8 * (byte & 3)));
+            }
+        }
     }
 }
 
@@ -3072,7 +3111,9 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
     // 4:2:0 (row pairs, chroma subsampled 2x horizontally): when the last lane-step would be at most
     // half full, it is done as 4-pixel halves of the remaining groups (colour4x2) instead
     const uint32_t ngroups = gpr * ngy, nfull = ngroups / kIdctThreads, nrem = ngroups - nfull * kIdctThreads;
-    const bool halves = JD_HALVES && pair && cmode == 1u && nrem != 0u && 2u * nrem <= kIdctThreads;  // wave-uniform
+    // 4:4:4 (per-pixel chroma, single rows) likewise, as 4-pixel halves of one row (colour4x1)
+    const bool halves = JD_HALVES && nrem != 0u && 2u * nrem <= kIdctThreads &&
+                        ((pair && cmode == 1u) || (JD_HALVES444 && !pair && cmode == 0u));  // wave-uniform
     const uint32_t nsteps = halves ? nfull : ~0u;
     for (uint32_t st = 0; gy < ngy && st < nsteps;
          st++, gy += step_y + (gc + step_c >= gpr ? 1u : 0u), gc = gc + step_c >= gpr ? gc + step_c - gpr : gc + step_c) {
@@ -3141,7 +3182,17 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             if (pair && y + 1 < H) store24(p0 + W3, w1, min(8u, W - x));
         }
     }
-    if (halves && lane < 2u * nrem) {
+    if (halves && !pair && lane < 2u * nrem) {  // 4:4:4
+        const uint32_t g = nfull * kIdctThreads + (lane >> 1);
+        const uint32_t py = div_small(g, magic16(gpr)), hc = g - py * gpr;
+        const uint32_t gx = (hc << 3) + ((lane & 1u) << 2);
+        const uint32_t y = y_tile + py, x = x_tile + gx;
+        if (y < H && x < W) {
+            uint32_t w0[3];
+            colour4x1(s_pl, pbase[0] + py * ppitch[0] + gx, pbase[1] + py * ppitch[1] + gx, pbase[2] + py * ppitch[2] + gx, w0);
+            store12(rgb_at(out, y, W3, x), w0, min(4u, W - x));
+        }
+    } else if (halves && lane < 2u * nrem) {
         const uint32_t g = nfull * kIdctThreads + (lane >> 1);
         const uint32_t hy = div_small(g, magic16(gpr)), hc = g - hy * gpr;
         const uint32_t py = hy * 2u, gx = (hc << 3) + ((lane & 1u) << 2);
