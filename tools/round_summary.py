@@ -9,7 +9,7 @@ Per config:
                                        WRITE_SIZE passes, corrected as MI355X_MICROARCH.md's HBM
                                        section prescribes (KiB units; gfx950 FETCH_SIZE counts half
                                        of a 16 B/lane streaming read, so reads are doubled)
-  profiles/TAG_sq_<cfg>.json           SQ counters per kernel (C2, C5): instruction counts, wave-cycle
+  profiles/TAG_sq_<cfg>.json           SQ counters per kernel (every config): instruction counts, wave-cycle
                                        split, clock held (GRBM_GUI_ACTIVE / 8 XCDs / dispatch time)
 Kernel names drop their template arguments (k_idct_color<1> -> k_idct_color; per-launch averages
 over the instances that ran, with the dispatches per batch beside them).  bench.py reads traffic and valu_insts/clock_ghz from these files.
