@@ -2523,6 +2523,31 @@ __device__ __forceinline__ void colour16(const int (&Y0)[8], const int (&Y1)[8],
 // into RGB order.  Taken when no chroma sample of the wave's lane-step needs the reference's
 // double-precision G (ChromaTerms::exact, about 2e-4 of the samples).
 __device__ __forceinline__ uint32_t pair16(int lo, int hi) { return __builtin_amdgcn_perm(uint32_t(hi), uint32_t(lo), 0x05040100u); }
+// The R and B terms of two chroma samples as one int16 pair, straight from their 32-bit multiply-add
+// sums: bits 16..31 of each (one v_perm instead of two shifts and a v_perm; the terms fit int16).
+// R: (91881 cr + 2^23) >> 16; B: (116130 cb + 2^23 + 64) >> 16 = (58065 cb + 2^22 + 32) >> 15
+// (chroma_terms).  JD_TERM_PERM = 0: shift each, then pair16.
+#ifndef JD_TERM_PERM
+#define JD_TERM_PERM 1
+#endif
+__device__ __forceinline__ uint32_t rb_pair(int c0, int c1, int k, int add) {
+    const int x0 = mad24(c0, k, add), x1 = mad24(c1, k, add);
+    return __builtin_amdgcn_perm(uint32_t(x1), uint32_t(x0), 0x07060302u);
+}
+__device__ __forceinline__ uint32_t r_pair(int cr0, int cr1) {
+#if JD_TERM_PERM
+    return rb_pair(cr0, cr1, 91881, 128 << 16);
+#else
+    return pair16(mad24(cr0, 91881, 128 << 16) >> 16, mad24(cr1, 91881, 128 << 16) >> 16);
+#endif
+}
+__device__ __forceinline__ uint32_t b_pair(int cb0, int cb1) {
+#if JD_TERM_PERM
+    return rb_pair(cb0, cb1, 116130, (128 << 16) + 64);
+#else
+    return pair16(mad24(cb0, 58065, (128 << 15) + 32) >> 15, mad24(cb1, 58065, (128 << 15) + 32) >> 15);
+#endif
+}
 // y + t of two int16 lanes; LO: t's low half serves both lanes (op_sel_hi), for the pixel pairs that
 // share one chroma sample, so no duplicated pair is built
 template <bool LO>
@@ -2567,9 +2592,9 @@ __device__ __forceinline__ uint32_t terms_words(const int16_t* s_pl, uint32_t cb
     for (int w = 0; w < 4; w++) {
         const int a = SH == 0 ? 2 * w : (SH == 1 ? w : w >> 1);  // sample of the word's pixels
         if (SH == 0) {
-            TR[w] = pair16(t[a].r, t[2 * w + 1].r);
+            TR[w] = r_pair(cr[a], cr[2 * w + 1]);
             TG[w] = pair16(t[a].g, t[2 * w + 1].g);
-            TB[w] = pair16(t[a].b, t[2 * w + 1].b);
+            TB[w] = b_pair(cb[a], cb[2 * w + 1]);
         } else {  // one sample under both pixels: the term in the low half (row_rgb_packed<true>)
             TR[w] = uint32_t(t[a].r);
             TG[w] = uint32_t(t[a].g);
@@ -2701,9 +2726,9 @@ __device__ __forceinline__ void colour4x1(const int16_t* s_pl, uint32_t yoff, ui
         t[u] = chroma_terms(cb[u], cr[u]);
         ex |= t[u].exact ? (1u << u) : 0u;
     }
-    const uint32_t TR[2] = {pair16(t[0].r, t[1].r), pair16(t[2].r, t[3].r)};
+    const uint32_t TR[2] = {r_pair(cr[0], cr[1]), r_pair(cr[2], cr[3])};
     const uint32_t TG[2] = {pair16(t[0].g, t[1].g), pair16(t[2].g, t[3].g)};
-    const uint32_t TB[2] = {pair16(t[0].b, t[1].b), pair16(t[2].b, t[3].b)};
+    const uint32_t TB[2] = {b_pair(cb[0], cb[1]), b_pair(cb[2], cb[3])};
     const uint2 Y0 = *reinterpret_cast<const uint2*>(s_pl + yoff);
     rgb4_packed<false>(Y0, TR, TG, TB, w);
     if (__any(ex != 0u)) {
