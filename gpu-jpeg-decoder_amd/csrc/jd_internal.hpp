@@ -247,6 +247,15 @@ constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
 #endif
 constexpr int kTileMaxBlocks = JD_TILE_BLOCKS;   // blocks per IDCT/colour tile (one lane each; k_idct_color's LDS)
 
+// k_colour_fancy's workgroup (fancy upsampling): kFancyW x kFancyH-pixel bands, kFancyBands of them
+// stacked vertically (the next band's window is fetched while the current one is coloured).  The
+// host sizes the grid from the same constants (jd_runtime.cpp launch_batch).
+#ifndef JD_FANCY_BANDS
+#define JD_FANCY_BANDS 8
+#endif
+constexpr uint32_t kFancyW = 128, kFancyH = 16, kFancyBands = JD_FANCY_BANDS;
+constexpr uint32_t kFancyRowsPerWg = kFancyH * kFancyBands;
+
 // Per-image status bits written by kernels (atomicOr); host maps them to jd_status.
 constexpr uint32_t kStCorrupt = 1u;     // bad code / overrun / DC range
 constexpr uint32_t kStRstMissing = 2u;  // fewer RST markers than intervals
@@ -331,6 +340,13 @@ struct BatchDev {
     unsigned long long* stamps;   // diagnostic builds (JD_STAMP): 8 s_memtime stamps per IDCT tile, else null
     uint32_t fancy;
     uint32_t max_fancy_wgs;       // k_colour_fancy bands per image: x in bits 0..15, y in 16..31
+    // co-scheduling (jd_runtime.cpp release_tail): k_piece's workgroups count themselves in
+    // piece_started as they start; the last to start writes piece_seq to piece_flag (host-visible),
+    // which tells the host that the whole grid is resident and the previous batch's k_idct_color
+    // may be launched beside it.  piece_flag null: no co-scheduling.
+    uint32_t* piece_started;
+    uint32_t* piece_flag;
+    uint32_t piece_seq;
 };
 
 }  // namespace jd

@@ -1433,11 +1433,20 @@ __device__ __forceinline__ uint32_t piece_stop(const PieceGeo& P) {
 // NT = kPieceThreads, or 64 for batches with few pieces (one small image: a few 512-lane
 // workgroups would leave all but a few CUs idle; 64-lane ones spread the same lanes over 8x as
 // many CUs, each staging its own table copy).
+#ifdef JD_PIECE_VGPRS  // register cap of the walk (co-scheduling: room for an IDCT wave per SIMD)
+#define JD_PIECE_ATTR __attribute__((amdgpu_waves_per_eu(JD_PIECE_VGPRS, JD_PIECE_VGPRS)))
+#else
+#define JD_PIECE_ATTR
+#endif
 template <int NT>
-__global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
+__global__ __launch_bounds__(NT) JD_PIECE_ATTR void k_piece(BatchDev b) {
     extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
+    if (b.piece_flag && threadIdx.x == 0) {  // the grid's last workgroup to start raises the flag
+        const uint32_t n = atomicAdd(b.piece_started, 1u);
+        if (n + 1u == gridDim.x) __hip_atomic_store(b.piece_flag, b.piece_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * NT) / kPieceThreads]];
     stage_luts(b, ts, s_lut, NT);
     __syncthreads();
@@ -3343,7 +3352,7 @@ __global__ __launch_bounds__(kIdctThreads) void k_idct_color_exact(BatchDev b) {
 // bands stacked per workgroup): every component's window of plane samples (the band's rows and
 // columns plus the filter's one-sample halo, 16-byte aligned) is staged in LDS with coalesced
 // 16-byte loads, then thread t colours 8 consecutive pixels of row t / 16 and stores their 24 bytes.
-constexpr uint32_t kFancyW = 128, kFancyH = 16, kFancyThreads = 256;
+constexpr uint32_t kFancyThreads = 256;  // kFancyW x kFancyH bands (jd_internal.hpp)
 constexpr uint32_t kFancyRows = kFancyH + 2, kFancyCols = kFancyW + 16;  // window bound per component
 static_assert((kFancyW / 8) * kFancyH == kFancyThreads, "one 8-pixel group per thread");
 
@@ -3476,15 +3485,11 @@ __device__ __forceinline__ void fancy_colour8(const FancyWin (&P)[3], uint32_t g
     }
 }
 
-// Bands per workgroup (stacked vertically): the next band's window is fetched into registers
-// while the current band is coloured, so a workgroup waits on HBM latency once, not per band.
-#ifndef JD_FANCY_BANDS
-#define JD_FANCY_BANDS 8
-#endif
+// Bands per workgroup (kFancyBands, stacked vertically): the next band's window is fetched into
+// registers while the current band is coloured, so a workgroup waits on HBM latency once, not per band.
 #ifndef JD_FANCY_LB
 #define JD_FANCY_LB 1  // minimum waves per SIMD asked of the compiler (register budget)
 #endif
-constexpr uint32_t kFancyBands = JD_FANCY_BANDS;
 constexpr int kFancyQuadsPerThread = 2;  // window quads per thread and component: 18 x 18 <= 512
 static_assert((kFancyRows * (kFancyCols / 8) + kFancyThreads - 1) / kFancyThreads <= kFancyQuadsPerThread,
               "window quads per thread");

@@ -198,8 +198,13 @@ bool build_lut(const HuffSpec& h, bool is_dc, HuffLut* lut) {
         const uint32_t e1 = l1 ? lut_entry(l1, sym1, is_dc) : 0u;  // 0: longer code (or unrepresentable)
         const uint32_t sz1 = is_dc ? sym1 : (sym1 & 15u);
         if (e1 == 0 || (is_dc ? sz1 > 11u : sz1 >= 10u)) {  // rare: the walks' generic branch
+            // hi bits 0..11 (the width w1 and the first symbol's advance) are clear, so the common
+            // path reads width 0 and advance 0 (a no-op).  The pair fields (adv2 12..18, L12
+            // 19..22, v2 23..31) do hold the rare entry's bits; they are inert because lo carries
+            // neither kLoPair nor kLoE2, which gate every use of them in the walks.
             lo = kLoRare;
-            hi = e1 << kRareShift;  // bits 5..18 clear: the common path's fields read 0 (a no-op)
+            hi = e1 << kRareShift;
+            static_assert((kLoRare & (kLoPair | kLoE2)) == 0u, "a rare lo word never gates the pair fields");
             continue;
         }
         const uint32_t L1 = l1 + sz1, adv1 = (e1 >> 8) & 127u;

@@ -41,12 +41,24 @@ inline uint32_t image_segments(const jd_header& h) {
     return h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
 }
 
+// Piece size of a batch of ecs_bits entropy-coded bits (jd_runtime.cpp build_plan): kPieceBits,
+// halved (down to kMinPieceBits) while the batch would have fewer than kPieceTarget pieces.  It
+// grows with the batch, so an image's own bits give a lower bound for any batch holding it.
+inline uint32_t adaptive_piece_bits(uint64_t ecs_bits) {
+    uint32_t p = kPieceBits;
+    while (p > kMinPieceBits && ecs_bits / p < kPieceTarget) p >>= 1;
+    return p;
+}
+
 // An image's AC-entry offsets are image-relative 32-bit values in 16-bit slot units
-// (BlockInfo::entry_start, k_gather's running offset): its reservation at the shortest pieces must
-// stay below 2^31 words, else the plan rejects it with JD_ERR_CAPACITY.
+// (BlockInfo::entry_start, k_gather's running offset): its reservation must stay below 2^31
+// words, else the plan rejects it with JD_ERR_CAPACITY.  piece_bits: the shortest pieces any
+// batch holding the image can get (adaptive_piece_bits of its own bits, or a forced size); div:
+// its region divisor.
 constexpr uint64_t kMaxImageEntryWords = 0x7FFFFF00ull;
-inline bool image_fits(uint64_t ecs_bytes, const jd_header& h) {
-    return entry_words(ecs_bytes, image_segments(h), kMinPieceBits) <= kMaxImageEntryWords;
+inline bool image_fits(uint64_t ecs_bytes, const jd_header& h, uint32_t piece_bits, int64_t spare_pieces = -1,
+                       uint32_t div = 2u) {
+    return entry_words(ecs_bytes, image_segments(h), piece_bits, spare_pieces, div) <= kMaxImageEntryWords;
 }
 
 // Per image of the plan: what the sequential pass decides (table set, quant slots, bases).

