@@ -189,6 +189,11 @@ constexpr uint64_t kPieceTarget = 65536;    // pieces wanted per batch before sh
 // One workgroup shares one copy of its table set in LDS (four 8.4 KB tables for 4:2:0 + 76 B per
 // lane: two 512-lane workgroups per CU, 16 waves).
 constexpr int kPieceThreads = JD_PIECE_THREADS;
+// Batches with fewer piece lanes than this run k_piece in 64-lane workgroups.
+#ifndef JD_SMALL_PIECE_LANES
+#define JD_SMALL_PIECE_LANES 16384
+#endif
+constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;
@@ -233,10 +238,7 @@ constexpr uint32_t kRegionSlack = 1040;
 // a lane's region line stays open for ~60 walk iterations and is written back piecemeal when the
 // L2 (4 MB per XCD, ~32 K lanes each streaming into their own lines) evicts it, each 16-byte quad
 // costing a 32-byte write (C2: k_piece WRITE_SIZE 3.98 -> 2.30 GB per launch).
-#ifndef JD_ENT_PAIR
-#define JD_ENT_PAIR 1
-#endif
-constexpr uint32_t kRegionAlign = JD_ENT_PAIR ? 8u : 4u;  // words
+constexpr uint32_t kRegionAlign = 8u;  // words
 JD_HD inline uint32_t region_words(uint32_t plen, uint32_t div = 2u) {
     return ((plen + div - 1u) / div + kRegionSlack + kRegionAlign - 1u) & ~(kRegionAlign - 1u);
 }
@@ -340,13 +342,16 @@ struct BatchDev {
     unsigned long long* stamps;   // diagnostic builds (JD_STAMP): 8 s_memtime stamps per IDCT tile, else null
     uint32_t fancy;
     uint32_t max_fancy_wgs;       // k_colour_fancy bands per image: x in bits 0..15, y in 16..31
-    // co-scheduling (jd_runtime.cpp release_tail): k_piece's workgroups count themselves in
-    // piece_started as they start; the last to start writes piece_seq to piece_flag (host-visible),
-    // which tells the host that the whole grid is resident and the previous batch's k_idct_color
-    // may be launched beside it.  piece_flag null: no co-scheduling.
+    // co-scheduling (jd_runtime.cpp release_tails): k_piece's workgroups count themselves in
+    // piece_started as they start; the one that completes the first resident round (piece_round
+    // workgroups: the grid's tail beyond it holds only unused piece slots, which start as slots
+    // free up and exit at once) writes piece_seq to piece_flag (host-visible), which tells the host
+    // that k_piece fills the device and the previous batch's k_idct_color may be launched beside
+    // it.  piece_flag null: no co-scheduling.
     uint32_t* piece_started;
     uint32_t* piece_flag;
     uint32_t piece_seq;
+    uint32_t piece_round;
 };
 
 }  // namespace jd

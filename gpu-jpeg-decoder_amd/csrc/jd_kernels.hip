@@ -488,11 +488,7 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
 __device__ __forceinline__ u32x4 load16(uintptr_t a, uintptr_t last) {
     // clamped to the image's last mapped 16-byte chunk; bytes past an interval's end are never
     // consumed as data, so what a clamped load returns there is irrelevant
-#if JD_NT & 4
-    return __builtin_nontemporal_load(reinterpret_cast<gu32x4*>(a < last ? a : last));
-#else
     return *reinterpret_cast<gu32x4*>(a < last ? a : last);
-#endif
 }
 
 // Codes longer than kLutBits: the canonical limits decide the length (kLutBits+1 plus the number
@@ -699,26 +695,15 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     }
 }
 
-// Bytes a window round advances (the piece walks' LDS rows hold one window plus a 16-byte
-// overlap per lane).
-#ifndef JD_WIN_PIECE
-#define JD_WIN_PIECE 32
-#endif
-constexpr int kWin = JD_WIN_PIECE;
+// Bytes a window round advances (the piece walks' LDS rows hold one window plus an 8-byte
+// overlap per lane; 16-byte windows measured 3 % slower).
+constexpr int kWin = 32;
 // Bytes of the next window a row also holds: a round decodes the symbols whose refill word index
 // is <= kWin / 4, and the last of them reads word kWin / 4 + 1, so 8 bytes suffice.
-#ifndef JD_ROW_OVERLAP
-#define JD_ROW_OVERLAP 8
-#endif
-constexpr int kRowOverlap = JD_ROW_OVERLAP;
-static_assert(kRowOverlap == 8 || kRowOverlap == 16, "row overlap: one 8- or 16-byte load");
+constexpr int kRowOverlap = 8;
 constexpr int win_loads(int win) { return win / 16 + 1; }  // loads per window: win / 16 of 16 bytes + the overlap
 constexpr int row_words(int win) { return 1 + (win + kRowOverlap) / 4; }  // odd pitch (last word unused)
 static_assert(row_words(kWin) % 2 == 1, "row pitch must be odd");
-#ifndef JD_ABL  // experiment builds: 1 skip colour, 2 skip IDCT math, 4 skip the entry scatter, 8 / 16 skip the
-                // piece walk's entry / block-record stores
-#define JD_ABL 0
-#endif
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 // Walk iterations between two executions of the rare-entry branch (a power of two; 1: every
 // iteration).  A rare entry is 0.45 % of lookups on the bench images, but with 64 lanes a quarter
@@ -727,10 +712,6 @@ constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 #define JD_RARE_EVERY 4
 #endif
 constexpr uint32_t kRareEvery = JD_RARE_EVERY;
-#ifndef JD_RARE_COUNT
-#define JD_RARE_COUNT 0  // > 0: also as soon as this many lanes of the wave are stalled on a rare entry
-#endif
-constexpr int kRareCount = JD_RARE_COUNT;
 static_assert((kRareEvery & (kRareEvery - 1u)) == 0u, "kRareEvery: a power of two");
 // items (entries + block records) one window round can add: every item takes >= 2 bits
 constexpr uint32_t kRoundItems = (kWin * 8 + 31) / 2 + 4;
@@ -740,15 +721,9 @@ constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte alig
 // Block records staged four at a time in a per-lane LDS ring and stored as one 16-byte quad (a
 // record at a time, 4 bytes, each store became its own write-back: 1.1 GB written for 0.2 GB of
 // records on C2).  16 bytes per lane is what two 512-lane workgroups per CU leave with 4 tables.
-#ifndef JD_REC_RING
-#define JD_REC_RING 1
-#endif
-constexpr int kRecRingWords = JD_REC_RING ? 4 : 0;
-// walk_piece counts blocks in steps of 4 with the ring (its slot address rrb | (~blk & 12): one op)
-constexpr uint32_t kBlkStep = JD_REC_RING ? 4u : 1u;
-#ifndef JD_EXTRA_LDS
-#define JD_EXTRA_LDS 0  // experiment builds: extra dynamic LDS per piece workgroup (lowers occupancy)
-#endif
+constexpr int kRecRingWords = 4;
+// walk_piece counts blocks in steps of 4 (the record ring's slot address rrb | (~blk & 12): one op)
+constexpr uint32_t kBlkStep = 4u;
 // k_redo: 64-lane workgroups with the tables in global memory, so that they fit beside the other
 // batch's k_piece / k_idct_color waves instead of waiting for a whole CU's LDS.
 constexpr int kRedoThreads = 64;
@@ -756,14 +731,8 @@ static_assert(kPieceThreads % kRedoThreads == 0, "a redo workgroup lies inside o
 constexpr size_t kRedoLds = size_t(kRedoThreads) * (row_words(kWin) + kRingWords + kRecRingWords) * 4;
 static_assert((kRedoThreads * row_words(kWin) * 4) % 32 == 0, "redo rings must start 32-byte aligned (ring_put)");
 size_t piece_lds_bytes(uint32_t max_slots, int nt) {
-    return size_t(max_slots) * sizeof(HuffLut) + size_t(nt) * (row_words(kWin) + kRingWords + kRecRingWords) * 4 +
-           JD_EXTRA_LDS;
+    return size_t(max_slots) * sizeof(HuffLut) + size_t(nt) * (row_words(kWin) + kRingWords + kRecRingWords) * 4;
 }
-// Batches with fewer piece lanes than this run k_piece in 64-lane workgroups.
-#ifndef JD_SMALL_PIECE_LANES
-#define JD_SMALL_PIECE_LANES 16384
-#endif
-constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
 static_assert((kPieceThreads * row_words(kWin) * 4) % 32 == 0 && (64 * row_words(kWin) * 4) % 32 == 0 && sizeof(HuffLut) % 32 == 0 && kRingWords == 8,
               "rings must start 32-byte aligned (ring_put)");
 static_assert((kPieceThreads * (row_words(kWin) + kRingWords) * 4) % 16 == 0 && (64 * (row_words(kWin) + kRingWords) * 4) % 16 == 0,
@@ -840,10 +809,7 @@ __device__ __forceinline__ u32x4 win_load(uintptr_t a, int q, uintptr_t last) {
 // every G window rounds and copied into the LDS row one window per round.  A lane's 128-byte line
 // is then fetched in one go instead of once per 32-byte round: with ~32 K lanes per XCD streaming
 // their own pieces, a line read round by round is often evicted from L2 between two rounds.
-#ifndef JD_WIN_GROUP
-#define JD_WIN_GROUP (128 / JD_WIN_PIECE)  // 128 bytes of a lane's stream per group
-#endif
-constexpr int kWinGroup = JD_WIN_GROUP;
+constexpr int kWinGroup = 128 / kWin;  // 128 bytes of a lane's stream per group (two windows: 1 % slower)
 static_assert(kWin % 16 == 0 && kRowOverlap == 8, "WinGroup: whole 16-byte loads per window, an 8-byte overlap");
 template <int G>
 struct WinGroup {
@@ -963,21 +929,9 @@ __device__ __forceinline__ uint32_t piece_emcu_code(uint32_t emcu, uint32_t tail
 }
 constexpr int kSpec = 0, kRedo = 1;
 
-#ifndef JD_NT
-#define JD_NT 0  // experiment builds: 1 entry stores non-temporal
-#endif
-__device__ __forceinline__ void st_ent(uint4* p, const uint4& v) {
-    if (JD_NT & 1) {
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(p));
-    } else {
-        *p = v;
-    }
-}
+// (non-temporal entry stores measured 3x slower: the lines are written back piecemeal anyway)
+__device__ __forceinline__ void st_ent(uint4* p, const uint4& v) { *p = v; }
 
-#ifndef JD_DC_BFI
-#define JD_DC_BFI 1
-#endif
 #ifndef JD_PSTAT
 #define JD_PSTAT 0  // diagnostic builds: k_piece walk statistics summed into BatchDev::stamps[0..15]
 #endif
@@ -1039,67 +993,39 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // a block takes at least two iterations (its DC symbol never pairs), so taking one quad (8
     // slots) every two iterations keeps fewer than 16 slots pending: one ring of two quads
     // suffices.  Slots go to the ring at slot ent & 15 (a symbol that emits nothing writes the next
-    // free slot without advancing, so it is overwritten).  With JD_ENT_PAIR an even quad is copied
-    // from the ring into registers when complete and stored together with the odd quad after it
-    // (32 bytes: one HBM write granule); block records go four at a time through their own ring
-    // (JD_REC_RING).
+    // free slot without advancing, so it is overwritten).  An even quad is copied from the ring
+    // into registers when complete and stored together with the odd quad after it (32 bytes: one
+    // HBM write granule); block records go four at a time through their own ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
     uint32_t st_wit = 0, st_lit = 0, st_rare = 0, st_rare_w = 0, st_rounds = 0, st_mend_w = 0, st_sym = 0;
-#if JD_REC_RING
     // block record k goes to ring word 3 - (k & 3), so that the ring reads as the records' memory
     // order (descending from rec_top); group fr (records 4fr .. 4fr + 3) is stored when complete,
     // at most one group pending (a block takes >= 2 iterations, a flush comes every other one)
     const uint32_t rrb = lds_addr(rring);  // 16-byte aligned
     uint32_t fr = 0;  // record groups stored
     uint4* rgp = reinterpret_cast<uint4*>(rec_top - 3u);  // where group fr goes (a pointer stepped down)
-#else
-    uint32_t prec = 0, pblk = 0;
-    bool pend_b = false;
-#endif
-#if JD_ENT_PAIR
     // an even quad is held in registers and stored with the odd one after it: 32 contiguous bytes
     uint4 hq = {0u, 0u, 0u, 0u};
 #define JD_FLUSH_Q()                                                                                   \
     do {                                                                                               \
         if (fq < (ent2 >> 4)) {                                                                        \
             if (fq & 1u) { /* (each branch reads its ring quad at a fixed address) */                   \
-                if (!(JD_ABL & 8) || ent2 == 0x7FFFFFFFu) {                                            \
-                    st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);                          \
-                    st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u)); \
-                }                                                                                      \
+                st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);                              \
+                st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u)); \
             } else {                                                                                   \
                 hq = *reinterpret_cast<const uint4*>(ring);                                            \
             }                                                                                          \
             fq++;                                                                                      \
         }                                                                                              \
     } while (0)
-#else
-#define JD_FLUSH_Q()                                                                                   \
-    do {                                                                                               \
-        if (fq < (ent2 >> 4)) {                                                                        \
-            if (!(JD_ABL & 8) || ent2 == 0x7FFFFFFFu)                                                  \
-                st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u))); \
-            fq++;                                                                                      \
-        }                                                                                              \
-    } while (0)
-#endif
-#if JD_REC_RING
 #define JD_FLUSH_B()                                                                                   \
     do {                                                                                               \
         if (fr < (blk >> 4)) {                                                                         \
-            if (!(JD_ABL & 16) || ent2 == 0x7FFFFFFFu)                                                 \
-                st_ent(rgp, *reinterpret_cast<const uint4*>(rring));                                   \
+            st_ent(rgp, *reinterpret_cast<const uint4*>(rring));                                       \
             rgp--;                                                                                     \
             fr++;                                                                                      \
         }                                                                                              \
     } while (0)
-#else
-#define JD_FLUSH_B()                                                     \
-    do {                                                                 \
-        if (pend_b && (!(JD_ABL & 16) || ent2 == 0x7FFFFFFFu)) rec_top[-int(pblk)] = prec; \
-        pend_b = false;                                                  \
-    } while (0)
-#endif
     uint32_t pos = W.start;  // == R.bit(): the stream bit of the next symbol
     // (re-walks are short and run few lanes: one window ahead keeps their registers down)
     constexpr int kGroup = KIND == kSpec ? kWinGroup : 1;
@@ -1132,12 +1058,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             uint32_t e1 = __builtin_amdgcn_ubfe(lo & ~zn, 6u, 1u);
             asm("" : "+v"(e1));  // keeps bfe + lshl_add (not lshr + and + add)
             ent2 += e1 << 1;
-            if (JD_DC_BFI) {  // dcd = DC ? v1 : dcd as one bit-field select on the sign-extended DC
-                              // flag (bit 5); asm: the compiler turns it back into and + cmp + cndmask
+            {  // dcd = DC ? v1 : dcd as one bit-field select on the sign-extended DC flag (bit 5);
+               // asm: the compiler turns it back into and + cmp + cndmask
                 const int m = __builtin_amdgcn_sbfe(int(lo), 5u, 1u);
                 asm("v_bfi_b32 %0, %1, %2, %0" : "+v"(dcd) : "v"(m), "v"(v1));
-            } else {
-                dcd = (lo & kLoDc) ? v1 : dcd;
             }
             // the second symbol of a pair, when the first left the block open (its slot goes to
             // the next free position either way).  It stores a coefficient iff E2 (bit 7 of lo,
@@ -1165,8 +1089,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             asm("" : "+v"(rl));  // one v_and for both compares
             const bool rare = rl != 0;
             // (| of ints, not ||: the asm compare stays unconditional, in the loop's block)
-            const bool rare_now = (int((it & (kRareEvery - 1u)) == kRareEvery - 1u) | int(all_lanes_nz(rl)) |
-                                   int(kRareCount && __popcll(__ballot(rare)) >= kRareCount)) != 0;  // wave-uniform
+            const bool rare_now = (int((it & (kRareEvery - 1u)) == kRareEvery - 1u) | int(all_lanes_nz(rl))) != 0;  // wave-uniform
             if (rare && rare_now) {  // codes longer than the index, escaped magnitudes, corrupt codes
                 uint32_t e = hi >> kRareShift;
                 if ((e & 31u) == 0) e = huff_slow(TS::at(tab), peek);
@@ -1191,7 +1114,6 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             R.skip(L);
             pos += L;
             const bool fin = zn >= 63u;
-#if JD_REC_RING
             // the block's end: its record to the ring and the per-block counters, in the branch the
             // record store needs anyway (exec-masked increments instead of select + add outside it)
             if (fin) {
@@ -1205,18 +1127,6 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 JD_FLUSH_Q();
                 JD_FLUSH_B();
             }
-#else
-            prec = fin ? block_rec(ent2 - ent_blk2, dcd) : prec;
-            pblk = fin ? blk : pblk;
-            pend_b = pend_b || fin;
-            if ((it & 1u) == 0u) {
-                JD_FLUSH_Q();
-                JD_FLUSH_B();
-            }
-            blk += fin ? 1u : 0u;
-            ent_blk2 = fin ? ent2 : ent_blk2;
-            b3 += fin ? 3u : 0u;
-#endif
             z = fin ? 0u : zn;
             // (a stalled rare lane keeps its table: its symbol, DC or AC, is still ahead)
             tab = (rare && !rare_now) ? tab : lbase + __builtin_amdgcn_ubfe(fin ? dcp : acp, b3, 3u) * kLutBytes;
@@ -1298,16 +1208,11 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     }
 #undef JD_FLUSH_Q
 #undef JD_FLUSH_B
-#if JD_ENT_PAIR
     if (fq & 1u) st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);  // a held quad
-#endif
     if (ent2 & 15u)  // the last, partial quad (every complete one is stored; the region has room for all of it)
         st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)));
-#if JD_REC_RING
     // the last, partial record group (every complete one is stored: the window round's flush)
-    if (!(JD_ABL & 16))
-        for (uint32_t r = 0; r < ((blk >> 2) & 3u); r++) rec_top[-int(4u * fr + r)] = rring[3u - r];
-#endif
+    for (uint32_t r = 0; r < ((blk >> 2) & 3u); r++) rec_top[-int(4u * fr + r)] = rring[3u - r];
     W.m_start = m_start;
     W.m_end = m_end;
     W.mcus = mcus;
@@ -1443,9 +1348,13 @@ __global__ __launch_bounds__(NT) JD_PIECE_ATTR void k_piece(BatchDev b) {
     extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    if (b.piece_flag && threadIdx.x == 0) {  // the grid's last workgroup to start raises the flag
+#ifdef JD_PIECE_PRIO  // co-scheduling probe: the walk's waves ahead of co-resident IDCT waves
+    __builtin_amdgcn_s_setprio(JD_PIECE_PRIO);
+#endif
+    if (b.piece_flag && threadIdx.x == 0) {  // the first round's last workgroup to start raises the flag
         const uint32_t n = atomicAdd(b.piece_started, 1u);
-        if (n + 1u == gridDim.x) __hip_atomic_store(b.piece_flag, b.piece_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (n + 1u == min(gridDim.x, b.piece_round))
+            __hip_atomic_store(b.piece_flag, b.piece_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * NT) / kPieceThreads]];
     stage_luts(b, ts, s_lut, NT);
@@ -1813,14 +1722,14 @@ __device__ __forceinline__ uint32_t gather_rows(BlockInfo* out, const uint32_t* 
 #pragma unroll
         for (int i = 0; i < kGatherLoads; i++) {
             const uint32_t k = k0 + t + 16u * i;
-            r[i] = (k < n && !(JD_ABL & 64)) ? rec_top[-int(k)] : 0u;
+            r[i] = (k < n) ? rec_top[-int(k)] : 0u;
         }
 #pragma unroll
         for (int i = 0; i < kGatherLoads; i++) {
             const uint32_t k = k0 + t + 16u * i;
             const uint32_t cnt = record_cnt(r[i]);
             const uint32_t incl = uint32_t(row_scan_dpp(int(cnt)));
-            if (k < n && (!(JD_ABL & 32) || run == 0x7FFFFFFFu))
+            if (k < n)
                 out[k] = BlockInfo{run + incl - cnt, pack_cnt_dc(cnt, record_dc(r[i]), record_esc(r[i]))};
             run += uint32_t(__shfl(int(incl), int(last), 64));
         }
@@ -2237,48 +2146,19 @@ struct ZzOfNat {  // zig-zag index of each natural position (inverse of kNatOfZz
 };
 constexpr ZzOfNat kZzOfNat{};
 constexpr uint32_t pk16(int lo, int hi) { return (uint32_t(lo) & 0xFFFFu) | (uint32_t(hi) << 16); }
-__device__ __forceinline__ int dot2(uint32_t a, uint32_t k, int c) {
-    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, k), c, false);
-}
 // The same as one VOP3P v_dot2_i32_i16 with its own accumulator operand: the builtin compiles to the
 // tied-accumulator v_dot2c form, which costs a v_mov per product to seed the accumulator (64 per
 // block).  k: the constant pair, in an SGPR (the one scalar operand VOP3P allows); the accumulator
 // is the inline constant 0 (dot2_0) or a VGPR (dot2_v).
-#ifndef JD_DOT2_ASM
-#define JD_DOT2_ASM 1
-#endif
-#ifndef JD_PACK_PERM
-#define JD_PACK_PERM 1
-#endif
-#ifndef JD_ZERO_ASM
-#define JD_ZERO_ASM 0  // 1: one hoisted zero quad (asm), 2: lane bound only; both measured slower
-#endif
-#ifndef JD_HALVES
-#define JD_HALVES 1
-#endif
-#ifndef JD_HALVES444
-#define JD_HALVES444 1
-#endif
-#ifndef JD_QUAD_SKIP
-#define JD_QUAD_SKIP 1
-#endif
 __device__ __forceinline__ int dot2_0(uint32_t a, uint32_t k) {
-#if JD_DOT2_ASM
     int r;
     asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "s"(k));
     return r;
-#else
-    return dot2(a, k, 0);
-#endif
 }
 __device__ __forceinline__ int dot2_v(uint32_t a, uint32_t k, int c) {
-#if JD_DOT2_ASM
     int r;
     asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
     return r;
-#else
-    return dot2(a, k, c);
-#endif
 }
 // (natural n_lo, natural n_hi) as one int16 pair from the zig-zag pair words dw
 __device__ __forceinline__ uint32_t nat_pair(const uint32_t (&dw)[32], int n_lo, int n_hi) {
@@ -2348,9 +2228,6 @@ __device__ __forceinline__ uint32_t row_bits(const uint32_t (&dw)[32]) {
     }
     return acc;
 }
-#ifndef JD_IDCT_ZROWS
-#define JD_IDCT_ZROWS 1  // skip the row pass of coefficient row 7 when it is zero across the wave
-#endif
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
 
@@ -2535,28 +2412,13 @@ __device__ __forceinline__ uint32_t pair16(int lo, int hi) { return __builtin_am
 // The R and B terms of two chroma samples as one int16 pair, straight from their 32-bit multiply-add
 // sums: bits 16..31 of each (one v_perm instead of two shifts and a v_perm; the terms fit int16).
 // R: (91881 cr + 2^23) >> 16; B: (116130 cb + 2^23 + 64) >> 16 = (58065 cb + 2^22 + 32) >> 15
-// (chroma_terms).  JD_TERM_PERM = 0: shift each, then pair16.
-#ifndef JD_TERM_PERM
-#define JD_TERM_PERM 1
-#endif
+// (chroma_terms).
 __device__ __forceinline__ uint32_t rb_pair(int c0, int c1, int k, int add) {
     const int x0 = mad24(c0, k, add), x1 = mad24(c1, k, add);
     return __builtin_amdgcn_perm(uint32_t(x1), uint32_t(x0), 0x07060302u);
 }
-__device__ __forceinline__ uint32_t r_pair(int cr0, int cr1) {
-#if JD_TERM_PERM
-    return rb_pair(cr0, cr1, 91881, 128 << 16);
-#else
-    return pair16(mad24(cr0, 91881, 128 << 16) >> 16, mad24(cr1, 91881, 128 << 16) >> 16);
-#endif
-}
-__device__ __forceinline__ uint32_t b_pair(int cb0, int cb1) {
-#if JD_TERM_PERM
-    return rb_pair(cb0, cb1, 116130, (128 << 16) + 64);
-#else
-    return pair16(mad24(cb0, 58065, (128 << 15) + 32) >> 15, mad24(cb1, 58065, (128 << 15) + 32) >> 15);
-#endif
-}
+__device__ __forceinline__ uint32_t r_pair(int cr0, int cr1) { return rb_pair(cr0, cr1, 91881, 128 << 16); }
+__device__ __forceinline__ uint32_t b_pair(int cb0, int cb1) { return rb_pair(cb0, cb1, 116130, (128 << 16) + 64); }
 // y + t of two int16 lanes; LO: t's low half serves both lanes (op_sel_hi), for the pixel pairs that
 // share one chroma sample, so no duplicated pair is built
 template <bool LO>
@@ -2865,15 +2727,21 @@ __device__ __forceinline__ void load_entry_quads(const EntryRange& r, uint4 (&E)
 // Slots of quad index qi (its 4 words in v) to the lane's staging row at their zig-zag positions:
 // int16 zz of the row is at byte 2 zz, swizzled (staging_base): row base ^ (2 zz & 0x7E).
 // value = slot >> 6 (arithmetic), zz = slot & 63 (blocks without escaped values).
+// Per slot one compare against the quad's limit (slot q is the block's when q < lead + cnt - 8 qi,
+// and, in quad 0, q >= lead); both values of a word by one packed arithmetic shift, the high one
+// stored from the word's upper half (ds_write_b16_d16_hi).
 __device__ __forceinline__ void scatter_quad(uint8_t* s_bytes, uint32_t base, const uint4& v, int qi,
                                              const EntryRange& r) {
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const int lim = int(r.lead) + r.cnt - 8 * qi;
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-        const int i = 8 * qi + q - int(r.lead);
-        const uint32_t h = (q & 1) ? (w[q >> 1] >> 16) : (w[q >> 1] & 0xFFFFu);
-        if (i >= 0 && i < r.cnt)
-            *reinterpret_cast<int16_t*>(s_bytes + (base ^ ((h << 1) & 0x7Eu))) = int16_t(int(int16_t(uint16_t(h))) >> 6);
+    for (int d = 0; d < 4; d++) {
+        const s16x2 val = __builtin_bit_cast(s16x2, w[d]) >> short(6);
+        if (2 * d < lim && (qi > 0 || 2 * d >= int(r.lead)))
+            *reinterpret_cast<int16_t*>(s_bytes + (base ^ ((w[d] << 1) & 0x7Eu))) = val.x;
+        if (2 * d + 1 < lim && (qi > 0 || 2 * d + 1 >= int(r.lead)))
+            *reinterpret_cast<int16_t*>(s_bytes + (base ^ ((w[d] >> 15) & 0x7Eu))) = val.y;
     }
 }
 
@@ -2883,7 +2751,6 @@ __device__ __forceinline__ void scatter_quad(uint8_t* s_bytes, uint32_t base, co
 __device__ __forceinline__ void scatter_entries(uint32_t* s_buf, uint32_t base, const EntryRange& r,
                                                 const uint4 (&E)[kPreQuads]) {
     uint8_t* row = reinterpret_cast<uint8_t*>(s_buf);
-#if !(JD_ABL & 4)
     if (__builtin_expect(r.esc, 0)) {
         for (int i = 0; i < r.cnt; i++) {
             const uint32_t h = r.ep[r.lead + i];
@@ -2896,7 +2763,7 @@ __device__ __forceinline__ void scatter_entries(uint32_t* s_buf, uint32_t base, 
     // quads no lane of the wave has are skipped (wave-uniform): their slots would all be masked
 #pragma unroll
     for (int u = 0; u < kPreQuads; u++)
-        if (!JD_QUAD_SKIP || u == 0 || __any(u < r.n4)) scatter_quad(row, base, E[u], u, r);
+        if (u == 0 || __any(u < r.n4)) scatter_quad(row, base, E[u], u, r);
     for (int c = kPreQuads; c < r.n4; c += 4) {
         uint4 v[4];
 #pragma unroll
@@ -2905,7 +2772,6 @@ __device__ __forceinline__ void scatter_entries(uint32_t* s_buf, uint32_t base, 
 #pragma unroll
         for (int u = 0; u < 4; u++) scatter_quad(row, base, v[u], c + u, r);
     }
-#endif
 }
 
 // DC prediction (parser.cpp:106-111): segmented scan of the tile's DC differences onto its entry
@@ -2941,20 +2807,10 @@ __device__ __forceinline__ void stage_quant(const BatchDev& b, const ImgDesc& im
     }
 }
 
-// One zero quad materialised once (the compiler would re-create it with four v_mov per store) and
-// the lane known to be < kIdctThreads (only the last store is predicated).
+// (a zero quad hoisted into one asm-materialised register, and the lane bound given to the
+// compiler, were both measured slower)
 __device__ __forceinline__ void zero_staging(uint32_t* s_buf, uint32_t lane) {
-#if JD_ZERO_ASM == 1
-    __builtin_assume(lane < kIdctThreads);
-    uint32_t z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    const uint4 zq = make_uint4(z, z, z, z);
-#else
-#if JD_ZERO_ASM == 2
-    __builtin_assume(lane < kIdctThreads);
-#endif
     const uint4 zq = make_uint4(0, 0, 0, 0);
-#endif
     uint4* z4 = reinterpret_cast<uint4*>(s_buf);
 #pragma unroll
     for (uint32_t k = 0; k < (kIdctBufWords / 4 + kIdctThreads - 1) / kIdctThreads; k++) {
@@ -3034,15 +2890,9 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
                 dw[4 * p4 + k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, rw[4 * p4 + k]) * __builtin_bit_cast(u16x2, qw[k]));
         }
         dw[0] = __builtin_amdgcn_perm(dw[0], uint32_t(dq0), 0x07060100u);
-#if !(JD_ABL & 2)
-        if (JD_IDCT_ZROWS) {
-            // row 7 is zero across a whole C2 tile in 96 % of tiles: its row pass is skipped by a
-            // wave-uniform branch (a second copy of the IDCT without it made the kernel spill)
-            idct_block_dot2<8>(dw, blk, __all(!have || row_bits<7>(dw) == 0u));
-        } else {
-            idct_block_dot2(dw, blk);
-        }
-#endif
+        // row 7 is zero across a whole C2 tile in 96 % of tiles: its row pass is skipped by a
+        // wave-uniform branch (a second copy of the IDCT without it made the kernel spill)
+        idct_block_dot2<8>(dw, blk, __all(!have || row_bits<7>(dw) == 0u));
     } else {
 #pragma unroll
         for (int p4 = 0; p4 < 8; p4++) {
@@ -3108,17 +2958,10 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             uint4 q;  // one v_perm per int16 pair
-#if JD_PACK_PERM
             q.x = pair16(blk[8 * r + 0], blk[8 * r + 1]);
             q.y = pair16(blk[8 * r + 2], blk[8 * r + 3]);
             q.z = pair16(blk[8 * r + 4], blk[8 * r + 5]);
             q.w = pair16(blk[8 * r + 6], blk[8 * r + 7]);
-#else
-            q.x = (uint32_t(blk[8 * r + 0]) & 0xFFFFu) | (uint32_t(blk[8 * r + 1]) << 16);
-            q.y = (uint32_t(blk[8 * r + 2]) & 0xFFFFu) | (uint32_t(blk[8 * r + 3]) << 16);
-            q.z = (uint32_t(blk[8 * r + 4]) & 0xFFFFu) | (uint32_t(blk[8 * r + 5]) << 16);
-            q.w = (uint32_t(blk[8 * r + 6]) & 0xFFFFu) | (uint32_t(blk[8 * r + 7]) << 16);
-#endif
             *reinterpret_cast<uint4*>(dst + r * pitch) = q;
         }
     }
@@ -3139,15 +2982,12 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
     // lane -> (row group gy, column group gc), advanced by 64 groups per iteration
     const uint32_t step_y = kIdctThreads / gpr, step_c = kIdctThreads - step_y * gpr;
     uint32_t gy = gpr <= 64u ? div_small(lane, magic16(gpr)) : 0u, gc = lane - gy * gpr;
-#if JD_ABL & 1
-    if (lane < 1000) return true;
-#endif
     // 4:2:0 (row pairs, chroma subsampled 2x horizontally): when the last lane-step would be at most
     // half full, it is done as 4-pixel halves of the remaining groups (colour4x2) instead
     const uint32_t ngroups = gpr * ngy, nfull = ngroups / kIdctThreads, nrem = ngroups - nfull * kIdctThreads;
     // 4:4:4 (per-pixel chroma, single rows) likewise, as 4-pixel halves of one row (colour4x1)
-    const bool halves = JD_HALVES && nrem != 0u && 2u * nrem <= kIdctThreads &&
-                        ((pair && cmode == 1u) || (JD_HALVES444 && !pair && cmode == 0u));  // wave-uniform
+    const bool halves = nrem != 0u && 2u * nrem <= kIdctThreads &&
+                        ((pair && cmode == 1u) || (!pair && cmode == 0u));  // wave-uniform
     const uint32_t nsteps = halves ? nfull : ~0u;
     for (uint32_t st = 0; gy < ngy && st < nsteps;
          st++, gy += step_y + (gc + step_c >= gpr ? 1u : 0u), gc = gc + step_c >= gpr ? gc + step_c - gpr : gc + step_c) {
@@ -3207,9 +3047,6 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             }
             pack24(rgb, w0);
         }
-#if JD_ABL & 32
-        if (w0[0] == 0x12345678u && w1[3] == 0x9abcdef0u)
-#endif
         {
             uint8_t* const p0 = rgb_at(out, y, W3, x);
             store24(p0, w0, min(8u, W - x));
@@ -3260,57 +3097,33 @@ __device__ __forceinline__ DcPred load_dcpred(const BatchDev& b, const ImgDesc& 
         if (JD_STAMP && b.stamps && lane == 0) b.stamps[size_t(im.tile_base + tile) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// One wave per kIdctTpw consecutive tiles of an image; grid: tile groups x the batch's images of
-// sampling layout M (b.mode_imgs).  The BlockInfo and DC predictors of all its tiles are loaded up
-// front, so only the first tile waits on the BlockInfo -> entries chain of two dependent HBM round
-// trips (the later tiles' BlockInfo arrives while the first is processed).
-#ifndef JD_TPW
-#define JD_TPW 1
-#endif
-constexpr uint32_t kIdctTpw = JD_TPW;
+// One wave per tile; grid: tiles x the batch's images of sampling layout M (b.mode_imgs).  (Two
+// tiles per wave, the second's BlockInfo loaded up front, took 3.7 instead of 2.9 ms: DESIGN.md §8.)
 template <int M>
 __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
     __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
-    const uint32_t lane = threadIdx.x, img = b.mode_imgs[b.mode_off[M] + blockIdx.y], tile0 = blockIdx.x * kIdctTpw;
+    const uint32_t lane = threadIdx.x, img = b.mode_imgs[b.mode_off[M] + blockIdx.y], tile = blockIdx.x;
     const ImgDesc& im = b.imgs[img];
-    const uint32_t nt = im.tiles_x * im.tiles_y;
-    if (tile0 >= nt) return;
-    BlockInfo bis[kIdctTpw];
-    DcPred dcs[kIdctTpw];
-#pragma unroll
-    for (uint32_t k = 0; k < kIdctTpw; k++) {
-        bis[k] = BlockInfo{0u, 0u};
-        dcs[k] = DcPred{0, 0, 0, 0};
-        if (tile0 + k < nt) {  // wave-uniform
-            const TileGeo G = tile_geo<M>(im, tile0 + k);
-            bis[k] = load_block_info<M>(b, im, G, tile_lane_geo<M>(im, G, lane));
-            dcs[k] = load_dcpred(b, im, tile0 + k);
-        }
-    }
+    if (tile >= im.tiles_x * im.tiles_y) return;
+    const TileGeo G = tile_geo<M>(im, tile);
+    const TileLaneGeo L = tile_lane_geo<M>(im, G, lane);
+    const BlockInfo bi = load_block_info<M>(b, im, G, L);
+    const DcPred dcin = load_dcpred(b, im, tile);
     stage_quant(b, im, s_qz, lane);
-    auto one_tile = [&](uint32_t k, const BlockInfo& bi, const DcPred& dcin) {
-        const uint32_t tile = tile0 + k;
-        JD_STAMP_AT(0);
-        const TileGeo G = tile_geo<M>(im, tile);
-        const TileLaneGeo L = tile_lane_geo<M>(im, G, lane);
-        if (k) __syncthreads();  // the previous tile's plane reads before the zeroing
-        zero_staging(s_buf, lane);
-        const EntryRange R = entry_range(b, im, bi, L.have);
-        uint4 E[kPreQuads];
-        load_entry_quads(R, E);
-        const int dc_pred = tile_dc_predict(G, L, bi, dcin, lane);
-        JD_STAMP_AT(1);
-        __syncthreads();
-        scatter_entries(s_buf, staging_base(lane), R, E);
-        __syncthreads();
-        JD_STAMP_AT(2);
-        idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, R.esc, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
-        JD_STAMP_AT(4);
-    };
-#pragma unroll
-    for (uint32_t k = 0; k < kIdctTpw; k++)
-        if (tile0 + k < nt) one_tile(k, bis[k], dcs[k]);  // wave-uniform; straight-line code per tile
+    JD_STAMP_AT(0);
+    zero_staging(s_buf, lane);
+    const EntryRange R = entry_range(b, im, bi, L.have);
+    uint4 E[kPreQuads];
+    load_entry_quads(R, E);
+    const int dc_pred = tile_dc_predict(G, L, bi, dcin, lane);
+    JD_STAMP_AT(1);
+    __syncthreads();
+    scatter_entries(s_buf, staging_base(lane), R, E);
+    __syncthreads();
+    JD_STAMP_AT(2);
+    idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, R.esc, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
+    JD_STAMP_AT(4);
 }
 
 // The tiles k_idct_color left (grid-stride over the list; empty in practice).
@@ -3773,13 +3586,13 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             if (!b.max_tiles) break;
             // one launch per sampling layout present in the batch (k_idct_color<M> is specialised)
             if (b.mode_cnt[kModeGen])
-                hipLaunchKernelGGL(k_idct_color<kModeGen>, dim3((b.mode_max_tiles[kModeGen] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kModeGen]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kModeGen>, dim3(b.mode_max_tiles[kModeGen], b.mode_cnt[kModeGen]), dim3(kIdctThreads), 0, s, b);
             if (b.mode_cnt[kMode420])
-                hipLaunchKernelGGL(k_idct_color<kMode420>, dim3((b.mode_max_tiles[kMode420] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kMode420]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kMode420>, dim3(b.mode_max_tiles[kMode420], b.mode_cnt[kMode420]), dim3(kIdctThreads), 0, s, b);
             if (b.mode_cnt[kMode422])
-                hipLaunchKernelGGL(k_idct_color<kMode422>, dim3((b.mode_max_tiles[kMode422] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kMode422]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kMode422>, dim3(b.mode_max_tiles[kMode422], b.mode_cnt[kMode422]), dim3(kIdctThreads), 0, s, b);
             if (b.mode_cnt[kMode444])
-                hipLaunchKernelGGL(k_idct_color<kMode444>, dim3((b.mode_max_tiles[kMode444] + kIdctTpw - 1) / kIdctTpw, b.mode_cnt[kMode444]), dim3(kIdctThreads), 0, s, b);
+                hipLaunchKernelGGL(k_idct_color<kMode444>, dim3(b.mode_max_tiles[kMode444], b.mode_cnt[kMode444]), dim3(kIdctThreads), 0, s, b);
             hipLaunchKernelGGL(k_idct_color_exact, dim3(1024), dim3(kIdctThreads), 0, s, b);
             break;
         case 10:

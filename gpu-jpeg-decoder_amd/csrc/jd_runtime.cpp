@@ -904,10 +904,13 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         // co-scheduling: this batch's k_piece tells the host when it is resident (release_tails);
         // only on the slots' own streams (a caller stream serialises the batches anyway)
         pd.gated = ctx->cosched && ctx->piece_flag && s == pd.stream && nsub > 0;
+        const uint32_t round = piece_lanes_resident(huffman_lds_bytes(P.max_slots)) / kPieceThreads;
+        pd.gated = pd.gated && nsub >= kSmallPieceLanes && round > 0;  // (small batches: 64-lane k_piece)
         if (pd.gated) {
             b.piece_started = reinterpret_cast<uint32_t*>(b.counters + 4);
             b.piece_flag = ctx->piece_flag;
             b.piece_seq = pd.seq = ++ctx->piece_seq;
+            b.piece_round = round;
         }
 
         ctx->last = b;

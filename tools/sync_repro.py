@@ -1,4 +1,4 @@
-"""Piece records of one image on the "sync" path (diagnostic for tools/sweep_cases_r03as.json #2)."""
+"""Piece records of one image on the "sync" path (diagnostic for a round-3 parity-sweep case)."""
 import os
 import sys
 
