@@ -342,16 +342,6 @@ struct BatchDev {
     unsigned long long* stamps;   // diagnostic builds (JD_STAMP): 8 s_memtime stamps per IDCT tile, else null
     uint32_t fancy;
     uint32_t max_fancy_wgs;       // k_colour_fancy bands per image: x in bits 0..15, y in 16..31
-    // co-scheduling (jd_runtime.cpp release_tails): k_piece's workgroups count themselves in
-    // piece_started as they start; the one that completes the first resident round (piece_round
-    // workgroups: the grid's tail beyond it holds only unused piece slots, which start as slots
-    // free up and exit at once) writes piece_seq to piece_flag (host-visible), which tells the host
-    // that k_piece fills the device and the previous batch's k_idct_color may be launched beside
-    // it.  piece_flag null: no co-scheduling.
-    uint32_t* piece_started;
-    uint32_t* piece_flag;
-    uint32_t piece_seq;
-    uint32_t piece_round;
 };
 
 }  // namespace jd

@@ -1338,24 +1338,11 @@ __device__ __forceinline__ uint32_t piece_stop(const PieceGeo& P) {
 // NT = kPieceThreads, or 64 for batches with few pieces (one small image: a few 512-lane
 // workgroups would leave all but a few CUs idle; 64-lane ones spread the same lanes over 8x as
 // many CUs, each staging its own table copy).
-#ifdef JD_PIECE_VGPRS  // register cap of the walk (co-scheduling: room for an IDCT wave per SIMD)
-#define JD_PIECE_ATTR __attribute__((amdgpu_waves_per_eu(JD_PIECE_VGPRS, JD_PIECE_VGPRS)))
-#else
-#define JD_PIECE_ATTR
-#endif
 template <int NT>
-__global__ __launch_bounds__(NT) JD_PIECE_ATTR void k_piece(BatchDev b) {
+__global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
     extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-#ifdef JD_PIECE_PRIO  // co-scheduling probe: the walk's waves ahead of co-resident IDCT waves
-    __builtin_amdgcn_s_setprio(JD_PIECE_PRIO);
-#endif
-    if (b.piece_flag && threadIdx.x == 0) {  // the first round's last workgroup to start raises the flag
-        const uint32_t n = atomicAdd(b.piece_started, 1u);
-        if (n + 1u == min(gridDim.x, b.piece_round))
-            __hip_atomic_store(b.piece_flag, b.piece_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * NT) / kPieceThreads]];
     stage_luts(b, ts, s_lut, NT);
     __syncthreads();

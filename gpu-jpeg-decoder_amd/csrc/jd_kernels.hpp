@@ -12,7 +12,6 @@ namespace jd {
 // 5 k_redo, 6 k_chain + k_chain_fix, 7 k_gather (Huffman), 8 k_dc_sum + k_dc_scan,
 // 9 k_idct_color (+ k_idct_color_exact), 10 k_colour_fancy.
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s);
-constexpr int kTailKernel = 9;  // the first kernel of a batch's colour stage (jd_runtime.cpp launch_tail)
 size_t huffman_lds_bytes(uint32_t max_slots);
 // Piece lanes k_piece keeps resident on the device at this dynamic LDS (workgroups per CU x CUs x
 // workgroup size); k_pieceplan fits the batch's pieces to whole rounds of them.

@@ -143,24 +143,12 @@ class Pool {
 
 }  // namespace
 
-// One launched batch whose results are not collected yet (jd_decode_batch_async keeps up to
-// kSlots in flight: the host plans batch k+1 while the GPU decodes batches k and k-1).  Each slot
-// owns its device scratch and, unless the caller names a stream, its own stream, so batch k+1's
-// first kernels run beside batch k's latency-bound tail (re-walks, chain, DC scan).
-// Co-scheduling: an async batch's colour stage (k_idct_color and what follows
-// it, "the tail") is held back until the next batch's k_piece grid is resident, so that the IDCT
-// waves fill the room k_piece leaves on every CU instead of k_piece waiting for the IDCT launch to
-// drain (release_tail).
-constexpr int kMaxSlots = 3;
-
+// One launched batch whose results are not collected yet (jd_decode_batch_async keeps two in
+// flight: the host plans batch k+1 while the GPU decodes batch k).  Each slot owns its device
+// scratch and, unless the caller names a stream, its own stream, so batch k+1's first kernels
+// run beside batch k's latency-bound tail (re-walks, chain, DC scan).
 struct Pending {
     bool active = false;
-    bool tail_pending = false;                  // kernels from k_idct_color on not launched yet
-    bool gated = false;                         // this batch's k_piece raises ctx->piece_flag
-    uint32_t seq = 0;                           // ... to this value
-    hipStream_t tail_stream = nullptr;          // the stream the batch runs on
-    hipEvent_t piece_done = nullptr;            // after k_piece (the gate's fallback)
-    BatchDev b{};                               // the batch's kernel arguments (the tail's launch)
     hipStream_t stream = nullptr;               // this slot's internal stream
     DevBuf d_plan, d_brk, d_blocks, d_entries, d_comp, d_planes, d_stamps;  // device scratch of the batch
     jd_result* results = nullptr;
@@ -204,14 +192,8 @@ struct jd_ctx {
     // staged per slot (Pending::in_host / d_input), so host-input batches pipeline too
     DevBuf output;
 
-    Pending pend[kMaxSlots];
-    int nslots = 2;          // slots in use (JD_SLOTS: 2 or 3)
+    Pending pend[2];
     int slot = 0;  // the slot the next launch uses
-    bool cosched = false;    // JD_COSCHED=1 (with JD_SLOTS=3): hold each async batch's colour stage
-                             // until the next batch's k_piece grid is resident (measured: no gain yet,
-                             // DESIGN.md §4.5)
-    uint32_t* piece_flag = nullptr;  // host-visible (coherent pinned) word k_piece raises (BatchDev::piece_flag)
-    uint32_t piece_seq = 0;
     const void* last_stream = nullptr;  // caller stream of the pending launches (nullptr: the slots' own)
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     int64_t spare_pieces = -1;          // spare re-walk regions per image (JD_SPARE_PIECES; -1: default)
@@ -248,10 +230,8 @@ jd_status hip_fail(jd_ctx* ctx, hipError_t e, const char* what) {
 // Waits for everything this context has in flight: the pending batches (their done events, on
 // the slot streams or a caller stream) and the context stream.  Unlike hipDeviceSynchronize it
 // does not stall the caller's unrelated streams.
-hipError_t release_all_tails(jd_ctx* ctx);
-
 hipError_t quiesce(jd_ctx* ctx) {
-    hipError_t r = release_all_tails(ctx);
+    hipError_t r = hipSuccess;
     for (Pending& pd : ctx->pend)
         if (pd.active) {
             const hipError_t e = hipEventSynchronize(pd.done);
@@ -266,8 +246,6 @@ hipError_t quiesce(jd_ctx* ctx) {
 
 // Makes the context stream wait for the pending batches (jd.h: calls on one context are ordered).
 hipError_t order_after_pending(jd_ctx* ctx) {
-    const hipError_t er = release_all_tails(ctx);
-    if (er != hipSuccess) return er;
     for (Pending& pd : ctx->pend)
         if (pd.active) {
             const hipError_t e = hipStreamWaitEvent(ctx->stream, pd.done, 0);
@@ -609,64 +587,8 @@ hipError_t ensure_pinned(void*& p, size_t& cap, size_t bytes) {
 // Parses nothing (parse_all did), plans items [lo, hi), uploads the plan and launches every kernel
 // on stream s into the context's current pending slot, which it leaves active; finish_batch
 // collects it.
-// The batch's tail: the colour stage (k_idct_color, k_colour_fancy), the status readback and the
-// completion event.
-jd_status launch_tail(jd_ctx* ctx, Pending& pd) {
-    pd.tail_pending = false;
-    hipStream_t s = pd.tail_stream;
-    if (pd.nimg) {
-        for (int k = kTailKernel; k < JD_NUM_KERNELS; k++) {
-            if (pd.timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][0], s));
-            HIPCHK(ctx, launch_kernel(k, pd.b, s));
-            if (pd.timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][1], s));
-        }
-        HIPCHK(ctx, hipMemcpyAsync(pd.host, pd.b.counters, 32, hipMemcpyDeviceToHost, s));
-        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(pd.host) + 32, pd.b.status, pd.nimg * 4, hipMemcpyDeviceToHost, s));
-    }
-    HIPCHK(ctx, hipEventRecord(pd.done, s));
-    return JD_OK;
-}
-
-// Waits (on the host, spinning) until batch `cur`'s k_piece grid is resident: its last workgroup
-// to start raises ctx->piece_flag to cur.seq.  Falls back when k_piece has already finished (or
-// failed) or after a second, so a lost flag only costs the overlap, never a hang.
-void wait_piece_resident(jd_ctx* ctx, Pending& cur) {
-    const volatile uint32_t* f = ctx->piece_flag;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t it = 1;; it++) {
-        if (int32_t(*f - cur.seq) >= 0) return;
-        if ((it & 255u) == 0u) {
-            if (hipEventQuery(cur.piece_done) != hipErrorNotReady) return;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) return;
-        }
-        _mm_pause();
-    }
-}
-
-// Launches the held tails of every slot but `cur`, oldest first; the newest of them (the batch
-// launched just before `cur`) once cur's k_piece is resident, when cur raises the flag.
-jd_status release_tails(jd_ctx* ctx, int cur) {
-    const int n = ctx->nslots;
-    for (int k = 1; k < n; k++) {
-        Pending& pd = ctx->pend[(cur + k) % n];
-        if (!pd.tail_pending) continue;
-        if (k == n - 1 && cur >= 0 && ctx->pend[cur].gated) wait_piece_resident(ctx, ctx->pend[cur]);
-        const jd_status st = launch_tail(ctx, pd);
-        if (st != JD_OK) return st;
-    }
-    return JD_OK;
-}
-
-hipError_t release_all_tails(jd_ctx* ctx) {
-    for (int k = 0; k < ctx->nslots; k++) {  // oldest first
-        Pending& pd = ctx->pend[(ctx->slot + k) % ctx->nslots];
-        if (pd.tail_pending && launch_tail(ctx, pd) != JD_OK) return hipErrorUnknown;
-    }
-    return hipSuccess;
-}
-
 jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result* results, int rgb_on_device,
-                       hipStream_t s, bool defer) {
+                       hipStream_t s) {
     Pending& pd = ctx->pend[ctx->slot];
     if (pd.active) {
         const jd_status fst = finish_batch(ctx, pd);
@@ -799,8 +721,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_chts = put(blob, P.chain_wg_tableset);
         const size_t o_modes = put(blob, P.mode_imgs);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
-        // entries, slow tiles, IDCT queue, k_pieceplan's choice, k_piece workgroups started
-        const size_t o_ctr = put(blob, std::vector<unsigned long long>(6, 0));
+        const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // entries, slow tiles, IDCT queue
         const size_t o_tscur = put(blob, P.ts_slot0);
         const size_t upload = blob.size();
         // device-written scratch after the uploaded part (no initialisation needed)
@@ -901,17 +822,6 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         }
         b.fancy = fancy ? 1u : 0u;
         b.max_fancy_wgs = max_fancy_wgs;
-        // co-scheduling: this batch's k_piece tells the host when it is resident (release_tails);
-        // only on the slots' own streams (a caller stream serialises the batches anyway)
-        pd.gated = ctx->cosched && ctx->piece_flag && s == pd.stream && nsub > 0;
-        const uint32_t round = piece_lanes_resident(huffman_lds_bytes(P.max_slots)) / kPieceThreads;
-        pd.gated = pd.gated && nsub >= kSmallPieceLanes && round > 0;  // (small batches: 64-lane k_piece)
-        if (pd.gated) {
-            b.piece_started = reinterpret_cast<uint32_t*>(b.counters + 4);
-            b.piece_flag = ctx->piece_flag;
-            b.piece_seq = pd.seq = ++ctx->piece_seq;
-            b.piece_round = round;
-        }
 
         ctx->last = b;
         ctx->last_blocks = P.total_blocks;
@@ -925,21 +835,21 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
         const double t_upload = tms();
         rng.reset(new Range("jd_launch"));
-        double t_k[kTailKernel];
-        for (int k = 0; k < kTailKernel; k++) {
+        double t_k[JD_NUM_KERNELS];
+        for (int k = 0; k < JD_NUM_KERNELS; k++) {
             if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][0], s));
             HIPCHK(ctx, launch_kernel(k, b, s));
             if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][1], s));
-            if (k == 4 && pd.gated) HIPCHK(ctx, hipEventRecord(pd.piece_done, s));
             t_k[k] = tms();
         }
         if (ctx->host_timing) {
             std::fprintf(stderr, "host launch returns:");
-            for (int k = 0; k < kTailKernel; k++) std::fprintf(stderr, " %.3f", t_k[k]);
+            for (int k = 0; k < JD_NUM_KERNELS; k++) std::fprintf(stderr, " %.3f", t_k[k]);
             std::fprintf(stderr, "\n");
         }
         HIPCHK(ctx, ensure_pinned(pd.host, pd.host_cap, 32 + size_t(nimg) * 4));
-        pd.b = b;
+        HIPCHK(ctx, hipMemcpyAsync(pd.host, b.counters, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(pd.host) + 32, b.status, nimg * 4, hipMemcpyDeviceToHost, s));
         pd.timing = timing;
         pd.fancy = fancy;
         pd.blocks = double(P.total_blocks);
@@ -971,20 +881,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             pd.host_copies.push_back({reinterpret_cast<uint64_t>(items[i].rgb), out_addr[i],
                                       uint64_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3});
     }
-    if (!nimg) pd.gated = false;
-    pd.tail_stream = s;
-    pd.tail_pending = true;
+    HIPCHK(ctx, hipEventRecord(pd.done, s));
     pd.active = true;
     staging.s = nullptr;  // the slot's done event now covers the copies
-    const int cur = ctx->slot;
-    ctx->slot = (ctx->slot + 1) % ctx->nslots;
-    // the previous batches' held tails: the last one beside this batch's k_piece
-    jd_status st2 = release_tails(ctx, cur);
-    if (st2 != JD_OK) return st2;
-    if (!defer || !pd.gated) {
-        st2 = launch_tail(ctx, pd);
-        if (st2 != JD_OK) return st2;
-    }
+    ctx->slot ^= 1;
     return JD_OK;
 }
 
@@ -992,10 +892,6 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
 // overrides OK), results, host copies of RGB, statistics.
 jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
     if (!pd.active) return JD_OK;
-    if (pd.tail_pending) {
-        const jd_status st = launch_tail(ctx, pd);
-        if (st != JD_OK) return st;
-    }
     pd.active = false;
     Range r("jd_collect");
     const auto tw0 = std::chrono::steady_clock::now();
@@ -1071,9 +967,8 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
 
 // Collects every launched batch, oldest first.
 jd_status finish_all(jd_ctx* ctx) {
-    if (release_all_tails(ctx) != hipSuccess) return hip_fail(ctx, hipErrorUnknown, "release_all_tails");
-    for (int k = 0; k < ctx->nslots; k++) {
-        const jd_status st = finish_batch(ctx, ctx->pend[(ctx->slot + k) % ctx->nslots]);
+    for (int k = 0; k < 2; k++) {
+        const jd_status st = finish_batch(ctx, ctx->pend[(ctx->slot + k) & 1]);
         if (st != JD_OK) return st;
     }
     return JD_OK;
@@ -1139,26 +1034,13 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
         const long long mb = std::strtoll(e, nullptr, 0);
         ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);
     }
-    if (const char* e = std::getenv("JD_COSCHED")) ctx->cosched = std::strtoll(e, nullptr, 0) != 0;
-    if (const char* e = std::getenv("JD_SLOTS")) ctx->nslots = int(std::min<long long>(kMaxSlots, std::max(2ll, std::strtoll(e, nullptr, 0))));
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return JD_ERR_HIP;
     }
-    if (ctx->cosched) {  // the co-scheduling flag: coherent pinned memory the GPU writes and the host polls
-        void* f = nullptr;
-        if (hipHostMalloc(&f, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess) {
-            memset(f, 0, 64);
-            ctx->piece_flag = static_cast<uint32_t*>(f);
-        } else {
-            (void)hipGetLastError();
-            ctx->cosched = false;
-        }
-    }
     for (Pending& pd : ctx->pend) {
         bool ok = hipStreamCreateWithFlags(&pd.stream, hipStreamNonBlocking) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&pd.done, hipEventDisableTiming) == hipSuccess;
-        ok = ok && hipEventCreateWithFlags(&pd.piece_done, hipEventDisableTiming) == hipSuccess;
         for (int k = 0; k < JD_NUM_KERNELS; k++)
             for (int j = 0; j < 2; j++) ok = ok && hipEventCreate(&pd.ev[k][j]) == hipSuccess;
         if (!ok) {
@@ -1185,13 +1067,11 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
         if (pd.host) (void)hipHostFree(pd.host);
         if (pd.plan_host) (void)hipHostFree(pd.plan_host);
         if (pd.done) (void)hipEventDestroy(pd.done);
-        if (pd.piece_done) (void)hipEventDestroy(pd.piece_done);
         for (int k = 0; k < JD_NUM_KERNELS; k++)
             for (int j = 0; j < 2; j++)
                 if (pd.ev[k][j]) (void)hipEventDestroy(pd.ev[k][j]);
     }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    if (ctx->piece_flag) (void)hipHostFree(ctx->piece_flag);
     delete ctx;
     return JD_OK;
 }
@@ -1236,12 +1116,12 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
     for (int lo = 0; lo < n;) {
         const int hi = batch_split(ctx, lo, n, items);
         hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->pend[ctx->slot].stream;
-        jd_status st = launch_batch(ctx, items, lo, hi, results, rgb_on_device, s, async);
+        jd_status st = launch_batch(ctx, items, lo, hi, results, rgb_on_device, s);
         if (st != JD_OK) return st;
-        if (async) {  // collect the oldest launch (its slot is the current one now)
+        if (async) {  // collect the previous launch (its slot is the current one now)
             st = finish_batch(ctx, ctx->pend[ctx->slot]);
         } else {  // collect this sub-batch before the next one reuses the staging and output pools
-            st = finish_batch(ctx, ctx->pend[(ctx->slot + ctx->nslots - 1) % ctx->nslots]);
+            st = finish_batch(ctx, ctx->pend[ctx->slot ^ 1]);
         }
         if (st != JD_OK) return st;
         lo = hi;
