@@ -211,15 +211,15 @@ def gather_matrix(local, world: int):
 
 RANK_FIELDS = ["elapsed_s", "pixels", "images", "ecs_bytes", "jpeg_bytes", "ecs_bytes_per_step",
                "images_per_step", "ms_per_step", "parse_ms", "plan_ms", "stage_ms", "wait_ms", "e2e_ms",
-               "h2d_GB_s"]
+               "h2d_GB_s", "e2e_registered_ms"]
 
 
-def rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, steps, host_ms_step, e2e_ms, h2d_gbs):
+def rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, steps, host_ms_step, e2e_ms, h2d_gbs, reg_ms=0.0):
     """This rank's counter vector for the one all-gather (order: RANK_FIELDS; column 0 = elapsed
     is max-reduced, 1-4 summed)."""
     return [elapsed, pixels * steps, n * steps, ecs * steps, jpeg_bytes * steps, ecs, n,
             elapsed / max(1, steps) * 1e3, host_ms_step.get("parse", 0.0), host_ms_step.get("plan", 0.0),
-            host_ms_step.get("stage_inputs", 0.0), host_ms_step.get("wait", 0.0), e2e_ms, h2d_gbs]
+            host_ms_step.get("stage_inputs", 0.0), host_ms_step.get("wait", 0.0), e2e_ms, h2d_gbs, reg_ms]
 
 
 def per_rank_table(allc, steps):
@@ -455,7 +455,7 @@ def main():
     ap.add_argument("--quality", type=int, default=90)
     ap.add_argument("--cpu-sample", type=int, default=1, help="1: time the CPU baselines, 0: skip")
     ap.add_argument("--verify", type=int, default=1, help="check images {0, n/2, n-1} bit-exact vs the oracle")
-    ap.add_argument("--e2e-steps", type=int, default=8, help="steps of the H2D-inclusive run (0: skip)")
+    ap.add_argument("--e2e-steps", type=int, default=24, help="steps of each H2D-inclusive leg (0: skip; the last batch's kernels after its DMA are ~6 ms of pipeline drain, so few steps understate the rate)")
     ap.add_argument("--copy-peak", type=int, default=1, help="measure an in-run HBM copy peak")
     ap.add_argument("--kernel-steps", type=int, default=3,
                     help="serialized (non-overlapped) steps after the timed region for per-kernel times")
@@ -575,39 +575,83 @@ def main():
     # pipelined like the timed loop (the host stages batch k+1 while the GPU decodes batch k), run
     # by every rank at once so a multi-GPU run shows the shared host's feed rate
     e2e = None
-    e2e_ms = h2d_gbs = 0.0
+    e2e_ms = h2d_gbs = reg_ms = 0.0
     if args.e2e_steps:
-        host_batches = [dec.make_batch(hosts, [None] * n, [rb.data_ptr() + o for o in out_offs]) for rb in rgb_bufs]
-        for k in range(2):
-            dec.decode_prepared(host_batches[k], pipelined=True)
-        dec.wait()
-        dec.reset_stats()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        te = time.perf_counter()
-        for k in range(args.e2e_steps):
-            dec.decode_prepared(host_batches[k & 1], pipelined=True)
-        dec.wait()
-        torch.cuda.synchronize(dev)
-        te = time.perf_counter() - te
-        if any(r.status for b in host_batches for r in b[1]):
-            raise SystemExit("decode failed in the H2D-inclusive run")
-        se = dec.stats()
+        def e2e_leg(batches):
+            """The pipelined timed loop over host-input batches: (seconds, library stats)."""
+            for k in range(2):
+                dec.decode_prepared(batches[k], pipelined=True)
+            dec.wait()
+            dec.reset_stats()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for k in range(args.e2e_steps):
+                dec.decode_prepared(batches[k & 1], pipelined=True)
+            dec.wait()
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter() - t
+            if any(r.status for b in batches for r in b[1]):
+                raise SystemExit("decode failed in the H2D-inclusive run")
+            return t, dec.stats()
+
+        def leg_dict(t, st, dram, note):
+            ms = t / args.e2e_steps * 1e3
+            return {"MPix_s": pixels * args.e2e_steps / t / 1e6, "ms_per_step": ms,
+                    "frac_of_h2d_bound": bound_ms / ms,
+                    "host_ms_per_step": {k: v / args.e2e_steps for k, v in st["host_ms"].items()},
+                    "h2d_registered_bytes_per_step": st["h2d_registered_bytes"] / args.e2e_steps,
+                    "host_dram_bytes_per_step": dram, "note": note}
+
+        def packed(arena):
+            views, o = [], 0
+            for h in hosts:
+                arena[o:o + h.nbytes] = h
+                views.append(arena[o:o + h.nbytes])
+                o += (h.nbytes + 63) // 64 * 64
+            return views
+
+        arena_bytes = sum((h.nbytes + 63) // 64 * 64 for h in hosts)
+        # 1. staged: files in pageable memory, copied by the library's workers into pinned staging
+        te, se = e2e_leg([dec.make_batch(hosts, [None] * n, [rb.data_ptr() + o for o in out_offs]) for rb in rgb_bufs])
+        # 2. registered: the files packed in one caller-owned arena registered with jd_host_register
+        arena = np.empty(arena_bytes, np.uint8)
+        views = packed(arena)
+        t_reg = time.perf_counter()
+        dec.register_host(arena)
+        t_reg = time.perf_counter() - t_reg
+        tr, sr = e2e_leg([dec.make_batch(views, [None] * n, [rb.data_ptr() + o for o in out_offs]) for rb in rgb_bufs])
+        dec.unregister_host(arena)
+        del arena, views
+        # 3. pinned arena: the files read into a jd_host_alloc arena (hipHostMalloc)
+        parena = dec.host_alloc(arena_bytes)
+        pviews = packed(parena)
+        tp, sp = e2e_leg([dec.make_batch(pviews, [None] * n, [rb.data_ptr() + o for o in out_offs]) for rb in rgb_bufs])
+        dec.host_free(parena)
+        del parena, pviews
         e2e_ms = te / args.e2e_steps * 1e3
+        reg_ms = min(tr, tp) / args.e2e_steps * 1e3
         h2d_gbs = pinned_h2d_gbs(int(jpeg_bytes), dev)
         bound_ms = jpeg_bytes / (h2d_gbs * 1e9) * 1e3
-        e2e = {"MPix_s": pixels * args.e2e_steps / te / 1e6, "ms_per_step": e2e_ms,
-               "steps": args.e2e_steps, "pinned_h2d_GB_s": h2d_gbs, "h2d_bound_ms_per_step": bound_ms,
-               "frac_of_h2d_bound": bound_ms / e2e_ms,
-               "host_ms_per_step": {k: v / args.e2e_steps for k, v in se["host_ms"].items()},
-               "note": "per rank; JPEG bytes from pageable host memory, copied by the library's host workers "
-                       "into per-slot pinned staging and uploaded on the slot's stream while the other slot "
-                       "decodes (jd_decode_batch_async); RGB left in HBM"}
+        e2e = leg_dict(te, se, 3 * jpeg_bytes,
+                       "per rank; JPEG bytes from pageable host memory, copied by the library's host workers into "
+                       "per-slot pinned staging and uploaded on the slot's stream while the other slot decodes "
+                       "(jd_decode_batch_async); RGB left in HBM; host DRAM traffic = the staging copy's read + "
+                       "write and the DMA's read")
+        e2e.update({"steps": args.e2e_steps, "pinned_h2d_GB_s": h2d_gbs, "h2d_bound_ms_per_step": bound_ms})
+        e2e["registered"] = dict(leg_dict(tr, sr, jpeg_bytes,
+                                          "the same files packed in one caller-owned arena registered once with "
+                                          "jd_host_register (hipHostRegister): uploaded straight from it by DMA, no "
+                                          "staging copy; host DRAM traffic = the DMA's read"),
+                                 register_ms=t_reg * 1e3)
+        e2e["pinned_arena"] = leg_dict(tp, sp, jpeg_bytes,
+                                       "the same files read into an arena from jd_host_alloc (hipHostMalloc): "
+                                       "uploaded straight from it by DMA, no staging copy")
 
     # one all-gather of per-rank counters (RCCL over xGMI when N > 1): totals for the line, and
     # every rank's step time and host feed (so an 8-GPU run shows whether the host binds)
-    local = torch.tensor(rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, args.steps, host_ms_step, e2e_ms, h2d_gbs),
+    local = torch.tensor(rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, args.steps, host_ms_step, e2e_ms, h2d_gbs, reg_ms),
                          dtype=torch.float64, device=dev if d["backend"] == "nccl" else "cpu")
     allc = gather_matrix(local, world)
     t_max = float(allc[:, 0].max())

@@ -166,6 +166,7 @@ struct Pending {
     size_t in_cap = 0;
     DevBuf d_input;                             // device copy of those inputs
     hipEvent_t done = nullptr;
+    hipEvent_t h2d_done = nullptr;              // after this slot's host-input copies (h2d_after)
     hipEvent_t ev[JD_NUM_KERNELS][2] = {};
     bool timing = false, fancy = false;
     double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0, piece_overlap = 0;
@@ -201,6 +202,15 @@ struct jd_ctx {
     bool fixed_pieces = false;          // JD_FIXED_PIECES: keep the host's piece size (no k_pieceplan)
     size_t stage_chunk = size_t(128) << 20;  // host-input H2D chunk (JD_STAGE_CHUNK_MB; 0: one copy per batch)
     bool stage_nt = true;                     // streaming-store staging copy (JD_STAGE_NT=0: memcpy)
+    // caller-owned host ranges registered with jd_host_register (page-locked, DMA-readable): host
+    // inputs lying in one are uploaded straight from it, without the staging copy
+    std::vector<std::pair<uintptr_t, uintptr_t>> host_regs;  // [begin, end), sorted by begin
+    std::vector<uintptr_t> host_owned;  // the ranges jd_host_alloc allocated (hipHostMalloc)
+    // Host-input copies of consecutive batches run one after the other (JD_H2D_SERIAL=0: as their
+    // streams allow): two batches' DMAs interleaved on the link each took twice as long, delaying
+    // both batches' kernels
+    bool h2d_serial = true;
+    hipEvent_t last_h2d = nullptr;  // the h2d_done event of the batch whose copies were issued last
     jd_stats stats{};
 
     std::vector<ParsedJpeg> parsed;
@@ -587,6 +597,21 @@ hipError_t ensure_pinned(void*& p, size_t& cap, size_t bytes) {
 // Parses nothing (parse_all did), plans items [lo, hi), uploads the plan and launches every kernel
 // on stream s into the context's current pending slot, which it leaves active; finish_batch
 // collects it.
+// The registered range holding address a (index into host_regs), or -1.
+int reg_range(const jd_ctx* ctx, uintptr_t a) {
+    const auto& r = ctx->host_regs;
+    auto it = std::upper_bound(r.begin(), r.end(), a, [](uintptr_t x, const std::pair<uintptr_t, uintptr_t>& y) { return x < y.first; });
+    if (it == r.begin()) return -1;
+    --it;
+    return a < it->second ? int(it - r.begin()) : -1;
+}
+// Whether [p, p + n) lies in one registered range.
+bool host_registered(const jd_ctx* ctx, const uint8_t* p, size_t n) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const int k = reg_range(ctx, a);
+    return k >= 0 && n <= ctx->host_regs[size_t(k)].second - a;
+}
+
 jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result* results, int rgb_on_device,
                        hipStream_t s) {
     Pending& pd = ctx->pend[ctx->slot];
@@ -605,11 +630,58 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     } staging;
     // 1. inputs and outputs on the device
     std::vector<uint64_t> dev_addr(size_t(hi), 0), out_addr(size_t(hi), 0);
-    size_t in_bytes = 0, out_bytes = 0;
+    // Host-memory inputs in a registered range (jd_host_register) are uploaded straight from it,
+    // in spans of neighbouring files (one DMA per span); the others are staged (below).
+    std::vector<int> reg_items;
+    std::vector<char> registered(size_t(hi), 0);
+    if (!ctx->host_regs.empty())
+        for (int i = lo; i < hi; i++)
+            if (ctx->pst[i] == JD_OK && !items[i].jpeg_dev && host_registered(ctx, items[i].jpeg, items[i].len)) {
+                registered[size_t(i)] = 1;
+                reg_items.push_back(i);
+            }
+    struct Span { uintptr_t lo, hi; size_t off; };
+    std::vector<Span> spans;
+    size_t in_bytes = 0, reg_bytes = 0, out_bytes = 0;
+    if (!reg_items.empty()) {
+        std::sort(reg_items.begin(), reg_items.end(), [&](int a, int b) { return items[a].jpeg < items[b].jpeg; });
+        constexpr uintptr_t kSpanGap = uintptr_t(1) << 20;  // a gap up to this is copied along
+        for (int i : reg_items) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(items[i].jpeg), e = a + items[i].len;
+            if (spans.empty() || a > spans.back().hi + kSpanGap || reg_range(ctx, a) != reg_range(ctx, spans.back().lo))
+                spans.push_back({a, e, 0});
+            else
+                spans.back().hi = std::max(spans.back().hi, e);
+        }
+    }
     for (int i = lo; i < hi; i++) {
         if (ctx->pst[i] != JD_OK) continue;
-        if (!items[i].jpeg_dev) in_bytes += align_up(items[i].len + 64, 256);
+        if (!items[i].jpeg_dev && !registered[size_t(i)]) in_bytes += align_up(items[i].len + 64, 256);
         if (!rgb_on_device) out_bytes += align_up(size_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3, 256);
+    }
+    for (Span& sp : spans) {  // after the staged inputs in the slot's device input pool
+        sp.off = in_bytes + reg_bytes;
+        reg_bytes += align_up(size_t(sp.hi - sp.lo) + 64, 256);
+    }
+    if (in_bytes + reg_bytes) HIPCHK(ctx, ensure_dev(ctx, pd.d_input, in_bytes + reg_bytes));
+    if (in_bytes + reg_bytes && ctx->h2d_serial && ctx->last_h2d && ctx->last_h2d != pd.h2d_done)
+        HIPCHK(ctx, hipStreamWaitEvent(s, ctx->last_h2d, 0));
+    if (reg_bytes) {
+        uint8_t* const dbase = static_cast<uint8_t*>(pd.d_input.p);
+        for (const Span& sp : spans)  // (in JD_STAGE_CHUNK_MB pieces, as the staged copies)
+            for (uintptr_t c = sp.lo; c < sp.hi; c += std::min<uintptr_t>(ctx->stage_chunk, sp.hi - c)) {
+                staging.s = s;
+                HIPCHK(ctx, hipMemcpyAsync(dbase + sp.off + (c - sp.lo), reinterpret_cast<const void*>(c),
+                                           std::min<uintptr_t>(ctx->stage_chunk, sp.hi - c), hipMemcpyHostToDevice, s));
+            }
+        size_t k = 0;  // reg_items ascend by address, as the spans do
+        for (int i : reg_items) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(items[i].jpeg);
+            while (a >= spans[k].hi) k++;
+            dev_addr[i] = reinterpret_cast<uint64_t>(dbase) + spans[k].off + (a - spans[k].lo);
+        }
+        ctx->stats.h2d_bytes += double(reg_bytes);
+        ctx->stats.h2d_registered_bytes += double(reg_bytes);
     }
     if (in_bytes) {
         // Host-memory inputs: copied into this slot's pinned staging by the host workers in
@@ -619,14 +691,13 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         // here (collected above).
         Range r("jd_stage_inputs");
         const auto ts0 = std::chrono::steady_clock::now();
-        HIPCHK(ctx, ensure_dev(ctx, pd.d_input, in_bytes));
         HIPCHK(ctx, ensure_pinned(pd.in_host, pd.in_cap, in_bytes));
         struct Piece { const uint8_t* src; size_t off, n; };
         std::vector<Piece> pieces;
         constexpr size_t kStagePiece = size_t(1) << 20;
         size_t off = 0;
         for (int i = lo; i < hi; i++) {
-            if (ctx->pst[i] != JD_OK || items[i].jpeg_dev) continue;
+            if (ctx->pst[i] != JD_OK || items[i].jpeg_dev || registered[size_t(i)]) continue;
             for (size_t k = 0; k < items[i].len; k += kStagePiece)
                 pieces.push_back({items[i].jpeg + k, off + k, std::min(kStagePiece, items[i].len - k)});
             dev_addr[i] = reinterpret_cast<uint64_t>(pd.d_input.p) + off;
@@ -650,6 +721,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         }
         ctx->stats.host_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
         ctx->stats.h2d_bytes += double(in_bytes);
+    }
+    if (in_bytes + reg_bytes && ctx->h2d_serial) {
+        HIPCHK(ctx, hipEventRecord(pd.h2d_done, s));
+        ctx->last_h2d = pd.h2d_done;
     }
     for (int i = lo; i < hi; i++)
         if (ctx->pst[i] == JD_OK && items[i].jpeg_dev) dev_addr[i] = reinterpret_cast<uint64_t>(items[i].jpeg_dev);
@@ -1030,6 +1105,7 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_FIXED_PIECES")) ctx->fixed_pieces = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
     if (const char* e = std::getenv("JD_STAGE_NT")) ctx->stage_nt = std::strtoll(e, nullptr, 0) != 0;
+    if (const char* e = std::getenv("JD_H2D_SERIAL")) ctx->h2d_serial = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_STAGE_CHUNK_MB")) {
         const long long mb = std::strtoll(e, nullptr, 0);
         ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);
@@ -1041,6 +1117,7 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     for (Pending& pd : ctx->pend) {
         bool ok = hipStreamCreateWithFlags(&pd.stream, hipStreamNonBlocking) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&pd.done, hipEventDisableTiming) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&pd.h2d_done, hipEventDisableTiming) == hipSuccess;
         for (int k = 0; k < JD_NUM_KERNELS; k++)
             for (int j = 0; j < 2; j++) ok = ok && hipEventCreate(&pd.ev[k][j]) == hipSuccess;
         if (!ok) {
@@ -1067,14 +1144,71 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
         if (pd.host) (void)hipHostFree(pd.host);
         if (pd.plan_host) (void)hipHostFree(pd.plan_host);
         if (pd.done) (void)hipEventDestroy(pd.done);
+        if (pd.h2d_done) (void)hipEventDestroy(pd.h2d_done);
         for (int k = 0; k < JD_NUM_KERNELS; k++)
             for (int j = 0; j < 2; j++)
                 if (pd.ev[k][j]) (void)hipEventDestroy(pd.ev[k][j]);
+    }
+    for (const auto& r : ctx->host_regs) {
+        void* p = reinterpret_cast<void*>(r.first);
+        if (std::find(ctx->host_owned.begin(), ctx->host_owned.end(), r.first) != ctx->host_owned.end())
+            (void)hipHostFree(p);
+        else
+            (void)hipHostUnregister(p);
     }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return JD_OK;
 }
+
+jd_status jd_host_register(jd_ctx* ctx, void* ptr, size_t bytes) {
+    if (!ctx || !ptr || !bytes) return JD_ERR_INVALID_ARG;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr), e = a + bytes;
+    for (const auto& r : ctx->host_regs)
+        if (a < r.second && r.first < e) return JD_ERR_INVALID_ARG;  // overlaps a registered range
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    ctx->host_regs.insert(std::upper_bound(ctx->host_regs.begin(), ctx->host_regs.end(), std::make_pair(a, e)),
+                          std::make_pair(a, e));
+    return JD_OK;
+}
+
+// Removes a registered (owned = false) or allocated (owned = true) range.
+static jd_status host_release(jd_ctx* ctx, void* ptr, bool owned) {
+    if (!ctx || !ptr) return JD_ERR_INVALID_ARG;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    auto it = std::find_if(ctx->host_regs.begin(), ctx->host_regs.end(),
+                           [&](const std::pair<uintptr_t, uintptr_t>& r) { return r.first == a; });
+    auto ow = std::find(ctx->host_owned.begin(), ctx->host_owned.end(), a);
+    if (it == ctx->host_regs.end() || (ow != ctx->host_owned.end()) != owned) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, quiesce(ctx));  // a launched batch may still be reading it
+    ctx->host_regs.erase(it);
+    if (owned) {
+        ctx->host_owned.erase(ow);
+        HIPCHK(ctx, hipHostFree(ptr));
+    } else {
+        HIPCHK(ctx, hipHostUnregister(ptr));
+    }
+    return JD_OK;
+}
+
+jd_status jd_host_unregister(jd_ctx* ctx, void* ptr) { return host_release(ctx, ptr, false); }
+
+jd_status jd_host_alloc(jd_ctx* ctx, size_t bytes, void** ptr) {
+    if (!ctx || !bytes || !ptr) return JD_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    void* p = nullptr;
+    HIPCHK(ctx, hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    ctx->host_regs.insert(std::upper_bound(ctx->host_regs.begin(), ctx->host_regs.end(), std::make_pair(a, a + bytes)),
+                          std::make_pair(a, a + bytes));
+    ctx->host_owned.push_back(a);
+    *ptr = p;
+    return JD_OK;
+}
+
+jd_status jd_host_free(jd_ctx* ctx, void* ptr) { return host_release(ctx, ptr, true); }
 
 jd_status jd_parse(const uint8_t* jpeg, size_t len, jd_header* hdr) {
     if (!jpeg || !hdr) return JD_ERR_INVALID_ARG;

@@ -33,7 +33,7 @@ JD_FLAG_FORCE_LANES = 4
 JD_FLAG_FANCY_UPSAMPLING = 8
 JD_FLAG_FULL_PIECES = 16
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES, "full": JD_FLAG_FULL_PIECES}
-JD_ABI_VERSION = 5
+JD_ABI_VERSION = 6
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece", "k_redo", "k_chain",
                 "k_gather", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
@@ -73,7 +73,8 @@ class _Stats(ctypes.Structure):
                 ("bytes", ctypes.c_double * JD_NUM_KERNELS), ("batches", ctypes.c_double),
                 ("images", ctypes.c_double), ("pixels", ctypes.c_double), ("ecs_bytes", ctypes.c_double),
                 ("blocks", ctypes.c_double), ("segments", ctypes.c_double), ("subsequences", ctypes.c_double),
-                ("host_ms", ctypes.c_double * 4), ("h2d_bytes", ctypes.c_double)]
+                ("host_ms", ctypes.c_double * 4), ("h2d_bytes", ctypes.c_double),
+                ("h2d_registered_bytes", ctypes.c_double)]
 
 
 # Every symbol include/jd.h and include/jd_test.h declare (checked by tests/test_abi.py).
@@ -82,7 +83,8 @@ EXPORTED_SYMBOLS = [
     "jd_decode_batch_async", "jd_decode_wait", "jd_write_array", "jd_write_ppm", "jd_status_str", "jd_abi_version", "jd_device_alloc", "jd_device_free",
     "jd_memcpy_h2d", "jd_memcpy_d2h", "jd_synchronize", "jd_get_stats", "jd_reset_stats",
     "jd_kernel_name", "jd_test_idct", "jd_test_idct_exact", "jd_test_color", "jd_debug_fetch", "jd_ctx_last_error",
-    "jd_test_copy_peak", "jd_device_bytes",
+    "jd_test_copy_peak", "jd_device_bytes", "jd_host_register", "jd_host_unregister",
+    "jd_host_alloc", "jd_host_free",
 ]
 
 _lib = None
@@ -129,8 +131,15 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         "jd_ctx_last_error": (ctypes.c_char_p, [c_void_p]),
         "jd_device_bytes": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "jd_test_copy_peak": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, ctypes.POINTER(ctypes.c_double)]),
+        "jd_host_register": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "jd_host_unregister": (c_int, [c_void_p, c_void_p]),
+        "jd_host_alloc": (c_int, [c_void_p, c_size_t, ctypes.POINTER(c_void_p)]),
+        "jd_host_free": (c_int, [c_void_p, c_void_p]),
     }
+    experiment = p != LIB_PATH  # an A/B build from an older tree may lack newer entry points
     for name, (res, args) in sig.items():
+        if experiment and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -240,7 +249,7 @@ class Decoder:
         """fancy=True: libjpeg's triangular chroma upsampling instead of replication
         (JD_FLAG_FANCY_UPSAMPLING; an option beyond the reference, see include/jd.h)."""
         self.lib = load_library()
-        if self.lib.jd_abi_version() != JD_ABI_VERSION:
+        if self.lib.jd_abi_version() != JD_ABI_VERSION and not os.environ.get("JDAMD_LIB"):  # (A/B builds may be older)
             raise JDError(JD_ERR_INVALID_ARG, f"libjdamd ABI {self.lib.jd_abi_version()} != {JD_ABI_VERSION}: rebuild")
         self.ctx = ctypes.c_void_p()
         opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path] | (JD_FLAG_FANCY_UPSAMPLING if fancy else 0),
@@ -352,6 +361,35 @@ class Decoder:
         if st != JD_OK:
             raise JDError(st, "jd_decode_wait " + (self.last_error() if st == JD_ERR_HIP else ""))
 
+    def register_host(self, arena: np.ndarray) -> None:
+        """jd_host_register: page-lock a caller-owned input arena (a contiguous numpy array) so that
+        batch items whose bytes lie in it are uploaded straight from it (no staging copy).  The
+        arena must stay alive and unchanged while batches reading it are in flight."""
+        st = self.lib.jd_host_register(self.ctx, arena.ctypes.data, arena.nbytes)
+        if st != JD_OK:
+            raise JDError(st, "jd_host_register " + (self.last_error() if st == JD_ERR_HIP else ""))
+
+    def unregister_host(self, arena: np.ndarray) -> None:
+        """jd_host_unregister (waits for the context's in-flight batches first)."""
+        st = self.lib.jd_host_unregister(self.ctx, arena.ctypes.data)
+        if st != JD_OK:
+            raise JDError(st, "jd_host_unregister " + (self.last_error() if st == JD_ERR_HIP else ""))
+
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """jd_host_alloc: a pinned input arena (hipHostMalloc) owned by the context, as a numpy
+        uint8 array; batch items whose bytes lie in it are uploaded straight from it.  Free it with
+        host_free() (or let close() do it); the array must not be used afterwards."""
+        p = ctypes.c_void_p()
+        st = self.lib.jd_host_alloc(self.ctx, nbytes, ctypes.byref(p))
+        if st != JD_OK:
+            raise JDError(st, "jd_host_alloc " + (self.last_error() if st == JD_ERR_HIP else ""))
+        return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value))
+
+    def host_free(self, arena: np.ndarray) -> None:
+        st = self.lib.jd_host_free(self.ctx, arena.ctypes.data)
+        if st != JD_OK:
+            raise JDError(st, "jd_host_free")
+
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
 
@@ -371,7 +409,7 @@ class Decoder:
             "blocks": s.blocks, "segments": s.segments, "subsequences": s.subsequences,
             "host_ms": {"parse": s.host_ms[0], "plan": s.host_ms[1], "stage_inputs": s.host_ms[2],
                         "wait": s.host_ms[3]},
-            "h2d_bytes": s.h2d_bytes,
+            "h2d_bytes": s.h2d_bytes, "h2d_registered_bytes": s.h2d_registered_bytes,
         }
 
     def device_bytes(self):

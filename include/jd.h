@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define JD_ABI_VERSION 5
+#define JD_ABI_VERSION 6
 
 typedef enum jd_status {
     JD_OK = 0,
@@ -135,11 +135,29 @@ jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* r
  * uploaded by an H2D on that slot's stream, which overlaps the other slot's kernels.
  * results[], the rgb buffers and the jpeg_dev buffers must stay valid until the batch is
  * collected: by the next jd_decode_batch_async / jd_decode_batch call on the context, or by
- * jd_decode_wait; host jpeg buffers only until the call returns. */
+ * jd_decode_wait; host jpeg buffers only until the call returns, unless they lie in a range
+ * registered with jd_host_register (then until the batch is collected). */
 jd_status jd_decode_batch_async(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
                                 void* hip_stream);
 /* Collects every launched batch (fills their results). */
 jd_status jd_decode_wait(jd_ctx* ctx);
+
+/* Registers a caller-owned host range (page-locks it for DMA; hipHostRegister) for inputs: a
+ * batch item whose `jpeg` bytes lie in a registered range and that has no `jpeg_dev` is uploaded
+ * straight from it, neighbouring files in one DMA, without the copy into the context's pinned
+ * staging.  Unlike staged inputs, such bytes are read after jd_decode_batch_async returns: they
+ * must stay unchanged until the batch is collected.  The reference copies each image to the
+ * device inside its host loop (cuda-decoder/src/parser.cu:441-467, driven per image by
+ * benchmark_thoughput/benchmark.cu:49-60); this replaces that copy for callers that keep their
+ * files in one arena.  Ranges may not overlap.  jd_host_unregister waits for the context's
+ * in-flight batches before unlocking; jd_ctx_destroy unregisters what is left. */
+jd_status jd_host_register(jd_ctx* ctx, void* ptr, size_t bytes);
+jd_status jd_host_unregister(jd_ctx* ctx, void* ptr);
+/* The same for an arena the library allocates (hipHostMalloc pinned memory) for the caller to
+ * read its files into: inputs in it are uploaded straight from it.  jd_host_free waits for the
+ * context's in-flight batches before freeing; jd_ctx_destroy frees what is left. */
+jd_status jd_host_alloc(jd_ctx* ctx, size_t bytes, void** ptr);
+jd_status jd_host_free(jd_ctx* ctx, void* ptr);
 
 /* `.array` text writer: "H W\n", then R, G, B planes as space-terminated decimal ints, one plane
  * per line, no trailing newline.  Replaces JPEGParser::write() (cpp-decoder/src/parser.cpp:197-209)
@@ -176,6 +194,7 @@ typedef struct jd_stats {
      * inputs (parallel memcpy into pinned memory + H2D issue), 3 waiting for batches to finish */
     double host_ms[4];
     double h2d_bytes; /* host-memory input bytes uploaded */
+    double h2d_registered_bytes; /* ... of which straight from registered ranges (no staging copy) */
 } jd_stats;
 jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out);
 jd_status jd_reset_stats(jd_ctx* ctx);

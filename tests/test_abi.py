@@ -116,6 +116,12 @@ def test_null_context_calls_are_rejected():
     assert lib.jd_decode(None, b"\xff\xd8", 2, None, 0, ctypes.byref(w), ctypes.byref(h)) == jdamd.JD_ERR_INVALID_ARG
     assert lib.jd_decode_batch(None, None, 1, None, 0, None) == jdamd.JD_ERR_INVALID_ARG
     assert lib.jd_kernel_name(0).decode() == jdamd.KERNEL_NAMES[0]
+    buf = ctypes.create_string_buffer(64)
+    assert lib.jd_host_register(None, buf, 64) == jdamd.JD_ERR_INVALID_ARG
+    assert lib.jd_host_unregister(None, buf) == jdamd.JD_ERR_INVALID_ARG
+    p = ctypes.c_void_p()
+    assert lib.jd_host_alloc(None, 64, ctypes.byref(p)) == jdamd.JD_ERR_INVALID_ARG
+    assert lib.jd_host_free(None, buf) == jdamd.JD_ERR_INVALID_ARG
 
 
 def test_write_ppm_matches_reference_comparator_format():

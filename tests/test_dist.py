@@ -47,7 +47,8 @@ def _worker(rank, world, port, batch, q):
     mat = bench.gather_matrix(torch.tensor([float(rank), float(len(seeds_c5))], dtype=torch.float64), world)
     # the bench's real per-rank vector: rank 1 is host-bound (slow parse + plan, slow e2e leg)
     host = {"parse": 0.5 + 2.0 * rank, "plan": 0.25 + rank, "stage_inputs": 1.0, "wait": 0.1}
-    vec = bench.rank_vector(2.0 + rank, 64 * 48, batch, 1000.0, 1500.0, 10, host, 20.0 + 5 * rank, 50.0 - rank)
+    vec = bench.rank_vector(2.0 + rank, 64 * 48, batch, 1000.0, 1500.0, 10, host, 20.0 + 5 * rank, 50.0 - rank,
+                            12.0 + rank)
     full = bench.gather_matrix(torch.tensor(vec, dtype=torch.float64), world)
     table = bench.per_rank_table(full, 10)
     q.put((rank, d, threads, info, seeds_c2, seeds_c5, digests, t_max, sums, mat.tolist(), table, full.tolist()))
@@ -83,6 +84,7 @@ def test_bench_rank_setup_sharding_and_counter_gather_gloo():
         assert table["parse_ms"] == [0.5, 2.5] and table["plan_ms"] == [0.25, 1.25]
         assert table["stage_ms"] == [1.0, 1.0] and table["wait_ms"] == [0.1, 0.1]
         assert table["e2e_ms"] == [20.0, 25.0] and table["h2d_GB_s"] == [50.0, 49.0]
+        assert table["e2e_registered_ms"] == [12.0, 13.0]
         assert table["host_parse_plan_over_step"] == [round(0.75 / 200.0, 4), round(3.75 / 300.0, 4)]
         assert max(r[0] for r in full) == 3.0 and sum(r[1] for r in full) == 2 * 64 * 48 * 10
     d0, d1 = set(out[0][6]), set(out[1][6])
