@@ -87,3 +87,44 @@ def test_escaped_entries_vs_oracle():
         dec.close()
     assert np.any(esc), "no block used an escaped entry"
     assert np.array_equal(out, ref)
+
+
+@pytest.fixture(scope="module")
+def dense_batch():
+    """the densest streams the region bound allows.  Flat images are all DC-only
+    blocks (Annex K tables: a 2-bit DC code plus a 2-bit chroma EOB, exactly the divisor-4 bound);
+    re-tabled files (tools/jd_retable.py: 4-bit DC, 8-bit AC codes) sit at the divisor's maximum, 8."""
+    import jd_retable
+
+    datas = []
+    for i, (w, h, ss, rr) in enumerate([(1920, 1080, "4:2:0", 0), (1280, 720, "4:4:4", 1), (777, 333, "4:2:2", 0),
+                                        (640, 480, "4:2:0", 2), (1024, 768, "gray", 0)]):
+        gray = ss == "gray"
+        px = np.full((h, w) if gray else (h, w, 3), 37 + 40 * i, np.uint8)
+        datas.append(jd_synth.encode(px, 90, "4:4:4" if gray else ss, rr))
+    for i, (w, h, ss, rr) in enumerate([(1280, 720, "4:2:0", 1), (640, 480, "4:4:4", 0), (333, 251, "4:2:2", 0)]):
+        datas.append(jd_retable.retable(jd_synth.encode(jd_synth.synth_pixels(w, h, 40 + i), 90, ss, rr)))
+    refs = []
+    for d in datas:
+        st, ref = jdoracle.decode(d)
+        assert st == 0
+        refs.append(ref)
+    return datas, refs
+
+
+@pytest.mark.parametrize("path", ["auto", "sync", "lanes", "full"])
+def test_dense_streams_without_spare_regions(monkeypatch, dense_batch, path):
+    """Flat (DC-only) and long-code images on every piece geometry with JD_SPARE_PIECES=0 (re-walks
+    over their own regions): bit-exact, and the re-tabled images planned with region divisor 8."""
+    datas, refs = dense_batch
+    monkeypatch.setenv("JD_SPARE_PIECES", "0")
+    dec = jdamd.Decoder(0, path=path)
+    try:
+        outs, status = dec.decode_batch(datas)
+        assert status == [0] * len(datas)
+        for i, (o, r) in enumerate(zip(outs, refs)):
+            assert np.array_equal(o, r), i
+        assert list(dec.debug_fetch("rw_div")[5:]) == [8, 8, 8]
+        assert list(dec.debug_fetch("rw_div")[:5]) == [4, 4, 4, 4, 4]
+    finally:
+        dec.close()

@@ -102,3 +102,18 @@ def test_region_divisor_of_standard_tables(harness, tmp_path):
     datas.append(jd_synth.encode(jd_synth.synth_pixels(64, 48, 1, gray=True), 90))
     out = _run(harness, datas, tmp_path)
     assert [o[13] for o in out] == [4, 4, 4, 4]
+
+
+def test_region_divisor_of_long_code_tables(harness, tmp_path):
+    """tables whose every code is long (4-bit DC, 8-bit AC codes: tools/jd_retable.py)
+    put every block and entry at >= 8 walk bits per region word, the divisor's maximum, 8; the
+    re-tabled files decode to the same pixels as the originals (the oracle honours DHT)."""
+    import jd_retable
+    import jd_synth
+
+    src = [jd_synth.encode(jd_synth.synth_pixels(64, 48, 2), 90, ss, 0) for ss in ("4:2:0", "4:4:4")]
+    datas = [jd_retable.retable(d) for d in src]
+    out = _run(harness, datas, tmp_path)
+    assert [o[13] for o in out] == [8, 8]
+    for a, b in zip(src, datas):
+        assert np.array_equal(jdoracle.decode(a)[1], jdoracle.decode(b)[1])
