@@ -580,6 +580,256 @@ int jdo_decode_ex(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* "fast" CPU mode (a CPU baseline only, never the product): the same decode with  */
+/* a 9-bit Huffman lookup table, a 64-bit bit buffer, the reference IDCT unchanged and integer     */
+/* colour terms per chroma sample (the reference's double G near integers, as the GPU does).       */
+/* Bit-exact with jdo_decode, status included (tests/test_oracle.py).                              */
+/* ------------------------------------------------------------------------------------------ */
+
+enum { kFastBits = 9 };
+typedef struct {
+    uint16_t e[1 << kFastBits]; /* len << 8 | symbol; 0: code longer than kFastBits */
+} hfast_t;
+
+static void hfast_build(const huff_t* h, hfast_t* t) {
+    memset(t, 0, sizeof(*t));
+    int code = 0, k = 0;
+    for (int l = 1; l <= kFastBits; l++) {
+        for (int i = 0; i < h->counts[l]; i++, k++, code++) {
+            const int sh = kFastBits - l;
+            for (int x = code << sh; x < ((code + 1) << sh) && x < (1 << kFastBits); x++)
+                t->e[x] = (uint16_t)((l << 8) | h->vals[k]);
+        }
+        code <<= 1;
+    }
+}
+
+typedef struct {
+    const uint8_t* d;
+    size_t n, pos;
+    uint64_t buf;  /* bits left-aligned */
+    int nbits;     /* bits in buf */
+    int nreal;     /* of which real data (the rest are 1-bit fill past a marker / the end) */
+    int at_marker;
+    int overrun;
+} fbr_t;
+
+static inline void fbr_fill(fbr_t* b) {
+    while (b->nbits <= 56) {
+        int c = 0xFF, real = 0;
+        if (!b->at_marker && b->pos < b->n) {
+            const uint8_t x = b->d[b->pos];
+            if (x != 0xFF) {
+                c = x;
+                real = 1;
+                b->pos++;
+            } else if (b->pos + 1 < b->n && b->d[b->pos + 1] == 0x00) {
+                c = 0xFF;
+                real = 1;
+                b->pos += 2;
+            } else {
+                b->at_marker = 1;
+            }
+        }
+        b->buf |= (uint64_t)c << (56 - b->nbits);
+        b->nbits += 8;
+        if (real && b->nreal == b->nbits - 8) b->nreal += 8;
+    }
+}
+
+static inline void fbr_skip(fbr_t* b, int n) {
+    if (n > b->nreal) b->overrun = 1;
+    b->buf <<= n;
+    b->nbits -= n;
+    b->nreal = b->nreal > n ? b->nreal - n : 0;
+}
+
+static inline int fbr_bits(fbr_t* b, int n) {
+    if (n == 0) return 0;
+    fbr_fill(b);
+    const int v = (int)(b->buf >> (64 - n));
+    fbr_skip(b, n);
+    return v;
+}
+
+static inline int fhuff(fbr_t* b, const huff_t* h, const hfast_t* t, int* bad) {
+    fbr_fill(b);
+    const uint16_t e = t->e[b->buf >> (64 - kFastBits)];
+    if (e) {
+        fbr_skip(b, e >> 8);
+        return e & 0xFF;
+    }
+    const uint32_t p16 = (uint32_t)(b->buf >> 48);
+    for (int l = kFastBits + 1; l <= 16; l++) {
+        const int code = (int)(p16 >> (16 - l));
+        if (code <= h->maxcode[l]) {
+            fbr_skip(b, l);
+            return h->vals[h->valptr[l] + code - h->mincode[l]];
+        }
+    }
+    fbr_skip(b, 16);
+    *bad = 1;
+    return 0;
+}
+
+static int fbr_restart(fbr_t* b, int k) {
+    /* br_restart from where the bit-serial reader would stand: after the last byte any of whose
+     * bits were consumed.  The whole unconsumed data bytes still buffered were the last ones
+     * fetched; give their file bytes back (a data 0xFF took two: FF 00). */
+    size_t pos = b->pos;
+    for (int u = b->nreal / 8; u > 0 && pos > 0; u--)
+        pos -= (pos >= 2 && b->d[pos - 1] == 0x00 && b->d[pos - 2] == 0xFF) ? 2 : 1;
+    br_t r;
+    memset(&r, 0, sizeof(r));
+    r.d = b->d;
+    r.n = b->n;
+    r.pos = pos;
+    const int ok = br_restart(&r, k);
+    b->pos = r.pos;
+    b->buf = 0;
+    b->nbits = b->nreal = 0;
+    b->at_marker = 0;
+    return ok;
+}
+
+static int decode_scan_fast(const img_t* im, const uint8_t* d, size_t n, planes_t* pl) {
+    const jdo_info* f = &im->info;
+    hfast_t* ft = (hfast_t*)malloc(sizeof(hfast_t) * 8);
+    if (!ft) return JDO_ERR_INVALID_ARG;
+    for (int c = 0; c < f->ncomp; c++) {
+        hfast_build(&im->dc[im->td[c]], &ft[2 * c]);
+        hfast_build(&im->ac[im->ta[c]], &ft[2 * c + 1]);
+    }
+    fbr_t b;
+    memset(&b, 0, sizeof(b));
+    b.d = d + f->ecs_offset;
+    b.n = n - f->ecs_offset;
+    int pred[4] = {0, 0, 0, 0};
+    int bad = 0, rst = 0;
+    const int nmcu = f->mcux * f->mcuy;
+    const int ri = f->restart_interval;
+    int32_t deq[64], out[64];
+    for (int m = 0; m < nmcu; m++) {
+        if (ri && m > 0 && m % ri == 0) {
+            if (b.overrun) bad = 1;
+            if (!fbr_restart(&b, rst)) bad = 1;
+            rst++;
+            b.overrun = 0;
+            for (int c = 0; c < 4; c++) pred[c] = 0;
+        }
+        const int my = m / f->mcux, mx = m % f->mcux;
+        for (int c = 0; c < f->ncomp; c++) {
+            const huff_t* dc = &im->dc[im->td[c]];
+            const huff_t* ac = &im->ac[im->ta[c]];
+            const int32_t* q = im->q[f->tq[c]];
+            for (int by = 0; by < f->v[c]; by++)
+                for (int bx = 0; bx < f->h[c]; bx++) {
+                    memset(deq, 0, sizeof(deq));
+                    int s = fhuff(&b, dc, &ft[2 * c], &bad);
+                    if (s > 16) {
+                        bad = 1;
+                        s = 16;
+                    }
+                    pred[c] += extend(fbr_bits(&b, s), s);
+                    deq[0] = pred[c] * q[0];
+                    for (int k = 1; k < 64;) {
+                        const int rs = fhuff(&b, ac, &ft[2 * c + 1], &bad);
+                        if (rs == 0) break;
+                        k += rs >> 4;
+                        const int sz = rs & 15;
+                        const int bits = fbr_bits(&b, sz);
+                        if (k < 64) {
+                            deq[k] = extend(bits, sz) * q[k];
+                            k++;
+                        }
+                    }
+                    jdo_idct_ref(deq, out);
+                    int32_t* dst = pl->plane[c] + (size_t)((my * f->v[c] + by) * 8) * pl->stride[c] +
+                                   (mx * f->h[c] + bx) * 8;
+                    for (int r = 0; r < 8; r++) memcpy(dst + (size_t)r * pl->stride[c], out + 8 * r, 8 * sizeof(int32_t));
+                }
+        }
+    }
+    if (b.overrun) bad = 1;
+    free(ft);
+    return bad ? JDO_ERR_CORRUPT : JDO_OK;
+}
+
+/* Integer colour of one pixel from precomputed terms (tests/test_oracle.py::test_color_fast_path_exhaustive). */
+static inline void color_fast(int y, int cb, int cr, uint8_t rgb[3]) {
+    /* n' = n + 271 * 587000 in [0, 2^29): floor(n' / 587000) by one multiply-high (the GPU's
+     * chroma_terms), the remainder exact; R and B by the GPU's 24-bit multiply-add forms */
+    const uint32_t np = (uint32_t)(202008 * cb + 419198 * cr + 271 * 587000);
+    const uint32_t qp = (uint32_t)(((uint64_t)np * 3836115526u) >> 51);
+    const int rem = (int)(np - qp * 587000u);
+    if (np != 271u * 587000u && (rem < 64 || rem > 587000 - 64)) {
+        jdo_color_ref(y, cb, cr, rgb);
+        return;
+    }
+    rgb[0] = (uint8_t)clamp255(y + ((91881 * cr + (128 << 16)) >> 16));
+    rgb[1] = (uint8_t)clamp255(np == 271u * 587000u ? y + 128 : y + 127 + 271 - (int)qp);
+    rgb[2] = (uint8_t)clamp255(y + ((58065 * cb + (128 << 15) + 32) >> 15));
+}
+
+/* Mismatches of color_fast against jdo_color_ref over every (y, cb, cr) in [-256, 255]^3. */
+long jdo_check_color_fast(void) {
+    long bad = 0;
+    for (int cb = -256; cb < 256; cb++)
+        for (int cr = -256; cr < 256; cr++)
+            for (int y = -256; y < 256; y++) {
+                uint8_t a[3], b[3];
+                jdo_color_ref(y, cb, cr, a);
+                color_fast(y, cb, cr, b);
+                bad += a[0] != b[0] || a[1] != b[1] || a[2] != b[2];
+            }
+    return bad;
+}
+
+int jdo_decode_fast(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* height) {
+    img_t* im = (img_t*)malloc(sizeof(img_t));
+    if (!im) return JDO_ERR_INVALID_ARG;
+    int st = parse(jpeg, len, im);
+    if (st != JDO_OK) {
+        free(im);
+        return st;
+    }
+    const jdo_info* f = &im->info;
+    if (width) *width = f->width;
+    if (height) *height = f->height;
+    planes_t pl;
+    memset(&pl, 0, sizeof(pl));
+    int ok = 1;
+    for (int c = 0; c < f->ncomp; c++) {
+        pl.stride[c] = f->mcux * f->h[c] * 8;
+        pl.plane[c] = (int32_t*)malloc(sizeof(int32_t) * pl.stride[c] * f->mcuy * f->v[c] * 8);
+        if (!pl.plane[c]) ok = 0;
+    }
+    if (ok) st = decode_scan_fast(im, jpeg, len, &pl);
+    int* sx = ok && rgb ? (int*)malloc(sizeof(int) * 3 * (size_t)f->width) : NULL;
+    if (ok && rgb && sx) {
+        for (int c = 0; c < f->ncomp && c < 3; c++)
+            for (int x = 0; x < f->width; x++) sx[c * f->width + x] = x * f->h[c] / f->hmax;
+        for (int y = 0; y < f->height; y++) {
+            const int32_t* row[3] = {NULL, NULL, NULL};
+            for (int c = 0; c < f->ncomp && c < 3; c++) row[c] = pl.plane[c] + (size_t)(y * f->v[c] / f->vmax) * pl.stride[c];
+            uint8_t* o = rgb + (size_t)y * f->width * 3;
+            if (f->ncomp == 1) {
+                for (int x = 0; x < f->width; x++) color_fast(row[0][x], 0, 0, o + 3 * x);
+            } else {
+                const int *s1 = sx + f->width, *s2 = sx + 2 * f->width;
+                for (int x = 0; x < f->width; x++) color_fast(row[0][sx[x]], row[1][s1[x]], row[2][s2[x]], o + 3 * x);
+            }
+        }
+    } else if (ok && rgb) {
+        ok = 0;
+    }
+    free(sx);
+    for (int c = 0; c < 4; c++) free(pl.plane[c]);
+    free(im);
+    return ok ? st : JDO_ERR_INVALID_ARG;
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* CPU baseline helper                                                                         */
 /* ------------------------------------------------------------------------------------------ */
 
@@ -590,6 +840,7 @@ typedef struct {
     int* status;
     int n;
     int next;
+    int fast;
 } work_t;
 
 static void* worker(void* arg) {
@@ -597,7 +848,8 @@ static void* worker(void* arg) {
     for (;;) {
         int i = __sync_fetch_and_add(&w->next, 1);
         if (i >= w->n) break;
-        int st = jdo_decode(w->jpegs[i], w->lens[i], w->rgbs ? w->rgbs[i] : NULL, NULL, NULL);
+        int st = w->fast ? jdo_decode_fast(w->jpegs[i], w->lens[i], w->rgbs ? w->rgbs[i] : NULL, NULL, NULL)
+                         : jdo_decode(w->jpegs[i], w->lens[i], w->rgbs ? w->rgbs[i] : NULL, NULL, NULL);
         if (w->status) w->status[i] = st;
     }
     return NULL;
@@ -605,7 +857,12 @@ static void* worker(void* arg) {
 
 double jdo_decode_many(const uint8_t* const* jpegs, const size_t* lens, int n, uint8_t* const* rgbs,
                        int threads, int* status) {
-    work_t w = {jpegs, lens, rgbs, status, n, 0};
+    return jdo_decode_many_ex(jpegs, lens, n, rgbs, threads, status, 0);
+}
+
+double jdo_decode_many_ex(const uint8_t* const* jpegs, const size_t* lens, int n, uint8_t* const* rgbs,
+                          int threads, int* status, int fast) {
+    work_t w = {jpegs, lens, rgbs, status, n, 0, fast};
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     pthread_t th[256];

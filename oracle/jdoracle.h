@@ -63,6 +63,13 @@ void jdo_color_ref(int y, int cb, int cr, uint8_t rgb[3]);
  * Returns wall seconds; statuses written to status[i] when non-NULL. */
 double jdo_decode_many(const uint8_t* const* jpegs, const size_t* lens, int n, uint8_t* const* rgbs,
                        int threads, int* status);
+/* "fast" CPU mode (LUT Huffman): the same pixels and status as jdo_decode, a CPU
+ * baseline only.  jdo_decode_many_ex(..., fast = 1) times it. */
+int jdo_decode_fast(const uint8_t* jpeg, size_t len, uint8_t* rgb, int* width, int* height);
+/* Mismatches of the fast mode's integer colour against jdo_color_ref over all of [-256, 255]^3. */
+long jdo_check_color_fast(void);
+double jdo_decode_many_ex(const uint8_t* const* jpegs, const size_t* lens, int n, uint8_t* const* rgbs,
+                          int threads, int* status, int fast);
 
 #ifdef __cplusplus
 }

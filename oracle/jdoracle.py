@@ -45,6 +45,11 @@ def lib() -> ctypes.CDLL:
         L.jdo_decode_many.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                       ctypes.c_void_p]
         L.jdo_decode_many.restype = ctypes.c_double
+        L.jdo_decode_fast.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                      ctypes.POINTER(ctypes.c_int)]
+        L.jdo_decode_many_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_int]
+        L.jdo_decode_many_ex.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -95,8 +100,20 @@ def color(y: int, cb: int, cr: int) -> Tuple[int, int, int]:
     return o[0], o[1], o[2]
 
 
-def decode_many(datas: Sequence[np.ndarray], threads: int = 1, want_rgb: bool = False):
-    """Times jdo_decode over a list of uint8 arrays.  Returns (seconds, statuses, rgbs or None)."""
+def decode_fast(data: bytes) -> Tuple[int, Optional[np.ndarray]]:
+    """The "fast" CPU mode (jdo_decode_fast: LUT Huffman, integer colour terms): a CPU baseline
+    with decode()'s status and pixels."""
+    st, i = info(data)
+    if st != 0:
+        return st, None
+    out = np.empty((i.height, i.width, 3), np.uint8)
+    st = lib().jdo_decode_fast(data, len(data), out.ctypes.data, None, None)
+    return st, out
+
+
+def decode_many(datas: Sequence[np.ndarray], threads: int = 1, want_rgb: bool = False, fast: bool = False):
+    """Times jdo_decode (fast: jdo_decode_fast) over a list of uint8 arrays.  Returns (seconds,
+    statuses, rgbs or None)."""
     n = len(datas)
     ptrs = (ctypes.c_void_p * n)(*[d.ctypes.data for d in datas])
     lens = (ctypes.c_size_t * n)(*[d.nbytes for d in datas])
@@ -109,7 +126,7 @@ def decode_many(datas: Sequence[np.ndarray], threads: int = 1, want_rgb: bool = 
             st, i = info(d.tobytes())
             rgbs.append(np.empty((i.height, i.width, 3), np.uint8))
         rgb_ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rgbs])
-    secs = lib().jdo_decode_many(ptrs, lens, n, rgb_ptrs, threads, status)
+    secs = lib().jdo_decode_many_ex(ptrs, lens, n, rgb_ptrs, threads, status, 1 if fast else 0)
     return secs, list(status), rgbs
 
 
