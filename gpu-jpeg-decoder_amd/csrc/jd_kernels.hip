@@ -2063,16 +2063,29 @@ __device__ __forceinline__ void idct_col(int* blk) {
 //
 // k_idct_color takes the fast form when every lane of the wave is in range (wave-uniform), which
 // real images always are; tests/test_gpu.py::test_idct_kat covers both over int32 inputs.
+// a * k + c as one v_mad_i32_i24 (k an inline constant or literal-free SGPR operand; |a| < 2^23)
+__device__ __forceinline__ int mad24v(int a, int k, int c) {
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
+    return r;
+}
+// blk[0] and blk[32] hold the column pass's x0 = (b0 << 8) + 8192 and x1 = b4 << 8 already: rows 0
+// and 4 leave their outputs unshifted with the low byte cleared (idct_row_dot2<true>), because
+// ((v >> 8) << 8) + 8192 = (v + 8192) & ~255 (8192 a multiple of 256; no overflow: |v| < 2^31 - 8192
+// in the fast form's range), the 8192 riding in row 0's rounding constant.
 __device__ __forceinline__ void idct_col_fast(int* blk) {
-    const int x1 = blk[8 * 4] << 8, x0 = (blk[0] << 8) + 8192;
+    const int x1 = blk[8 * 4], x0 = blk[0];
     const int b1 = blk[8 * 1], b2 = blk[8 * 2], b3 = blk[8 * 3], b5 = blk[8 * 5], b6 = blk[8 * 6], b7 = blk[8 * 7];
-    // (the rounding 4 rides in the inner multiply-add: two v_mad_i32_i24 per term)
-    int x4 = (__mul24(b1, kC1) + (__mul24(b7, kC7) + 4)) >> 3;
-    int x5 = (__mul24(b1, kC7) + (__mul24(b7, -kC1) + 4)) >> 3;
-    int x6 = (__mul24(b5, kC5) + (__mul24(b3, kC3) + 4)) >> 3;
-    int x7 = (__mul24(b5, kC3) + (__mul24(b3, -kC5) + 4)) >> 3;
-    int x2 = (__mul24(b2, kC6) + (__mul24(b6, -kC2) + 4)) >> 3;
-    int x3 = (__mul24(b2, kC2) + (__mul24(b6, kC6) + 4)) >> 3;
+    // (the rounding 4 rides in the inner multiply-add: two v_mad_i32_i24 per term, forced through
+    // asm: left to itself the compiler emitted two v_mul_i32_i24 and a v_add3 for a third of them)
+    int c4;
+    asm("v_mov_b32 %0, 4" : "=v"(c4));
+    int x4 = mad24v(b1, kC1, mad24v(b7, kC7, c4)) >> 3;
+    int x5 = mad24v(b1, kC7, mad24v(b7, -kC1, c4)) >> 3;
+    int x6 = mad24v(b5, kC5, mad24v(b3, kC3, c4)) >> 3;
+    int x7 = mad24v(b5, kC3, mad24v(b3, -kC5, c4)) >> 3;
+    int x2 = mad24v(b2, kC6, mad24v(b6, -kC2, c4)) >> 3;
+    int x3 = mad24v(b2, kC2, mad24v(b6, kC6, c4)) >> 3;
     int x8 = x0 + x1;
     int y0 = x0 - x1;
     const int y1 = x4 + x6;
@@ -2154,6 +2167,9 @@ __device__ __forceinline__ uint32_t nat_pair(const uint32_t (&dw)[32], int n_lo,
                          (uint32_t(5 + 2 * (zh & 1)) << 24);
     return __builtin_amdgcn_perm(dw[zh >> 1], dw[zl >> 1], sel);
 }
+// KEEP: the row feeds the column pass's x0 / x1 (rows 0 and 4): outputs v & ~255 instead of v >> 8
+// (one full-rate v_and instead of a shift here and another in the column pass).
+template <bool KEEP = false>
 __device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, int* out, int c128) {
     const uint32_t P0 = nat_pair(dw, 8 * r + 0, 8 * r + 4), P1 = nat_pair(dw, 8 * r + 1, 8 * r + 7);
     const uint32_t P2 = nat_pair(dw, 8 * r + 5, 8 * r + 3), P3 = nat_pair(dw, 8 * r + 2, 8 * r + 6);
@@ -2175,14 +2191,9 @@ __device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, i
     y0 -= x2;
     x2 = (181 * (x4 + x5) + 128) >> 8;
     x4 = (181 * (x4 - x5) + 128) >> 8;
-    out[0] = (x7 + y1) >> 8;
-    out[1] = (x3 + x2) >> 8;
-    out[2] = (y0 + x4) >> 8;
-    out[3] = (x8 + x6) >> 8;
-    out[4] = (x8 - x6) >> 8;
-    out[5] = (y0 - x4) >> 8;
-    out[6] = (x3 - x2) >> 8;
-    out[7] = (x7 - y1) >> 8;
+    const int v[8] = {x7 + y1, x3 + x2, y0 + x4, x8 + x6, x8 - x6, y0 - x4, x3 - x2, x7 - y1};
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[k] = KEEP ? (v[k] & ~255) : (v[k] >> 8);
 }
 // NR: rows 0 .. NR - 1 may hold nonzero coefficients, the rest are zero in every lane of the wave
 // (their row outputs are 0: (0 + 128) >> 8), so their row passes are skipped and the column pass's
@@ -2190,13 +2201,16 @@ __device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, i
 // skip7 (wave-uniform): row 7 is zero in every lane, its row pass is skipped at run time.
 template <int NR = 8>
 __device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], int (&blk)[64], bool skip7 = false) {
-    int c128;
+    int c128, c8320;
     asm("v_mov_b32 %0, 0x80" : "=v"(c128));  // one VGPR holding the row pass's rounding term
+    asm("v_mov_b32 %0, 0x2080" : "=v"(c8320));  // row 0: + the column pass's 8192 (idct_col_fast)
 #pragma unroll
     for (int r = 0; r < 8; r++) {
         if (r < NR && !(r == 7 && skip7)) {
-            idct_row_dot2(dw, r, blk + 8 * r, c128);
-        } else {
+            if (r == 0) idct_row_dot2<true>(dw, r, blk, c8320);
+            else if (r == 4) idct_row_dot2<true>(dw, r, blk + 32, c128);
+            else idct_row_dot2(dw, r, blk + 8 * r, c128);
+        } else {  // (rows 1..7 only: NR >= 1)
 #pragma unroll
             for (int k = 0; k < 8; k++) blk[8 * r + k] = 0;
         }
