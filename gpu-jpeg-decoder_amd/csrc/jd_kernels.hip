@@ -96,7 +96,7 @@ __device__ __forceinline__ int wave_scan_dpp(int x) {
 // Exclusive scan over a 256-thread block; returns the exclusive prefix, *total the block sum.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_wsum, uint32_t* total) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t incl = wave_incl_scan(x);
+    const uint32_t incl = uint32_t(wave_scan_dpp(int(x)));  // (every thread of the block calls this)
     if (lane == 63) s_wsum[wv] = incl;
     __syncthreads();
     uint32_t off = incl - x, tot = 0;
@@ -158,10 +158,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
 
     uint32_t ndrop = 0, nbrk = 0;
     const bool interior = t0 >= lo && t0 + 64 < fend;
-    if (interior) {
-        // interior thread: exact per-byte masks (high bit of each byte lane), one word at a time
-        // with the neighbours' masks carried (few live registers: this pass is latency-bound)
-        //   drop : 00 preceded by FF       brk : FF followed by neither 00 nor FF
+    // interior thread: exact per-byte masks (high bit of each byte lane), one word at a time with
+    // the neighbours' masks carried, kept per word for the break walk below
+    //   drop : 00 preceded by FF       brk : FF followed by neither 00 nor FF
+    // (computed in every thread, so that the masks need no zero-initialised copy for the edge
+    // threads, which count byte by byte below instead)
+    uint32_t dmq[16], bmq[16];
+    {
         uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;  // only its top byte is used
         uint32_t ff_cur, nz_cur;
         uint32_t zero_cur = scan_masks(w[0], ff_cur, nz_cur);
@@ -170,16 +173,18 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
         for (int q = 0; q < 16; q++) {
             uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = 0;
             if (q < 15) zero_nx = scan_masks(w[q + 1], ff_nx, nz_nx);
-            const uint32_t pf = (ff_cur << 8) | (ff_prev >> 24);
-            const uint32_t nn = (nz_cur >> 8) | (nz_nx << 24);
-            ndrop += __builtin_popcount(zero_cur & pf);
-            nbrk += __builtin_popcount(ff_cur & nn);
+            dmq[q] = zero_cur & __builtin_amdgcn_alignbit(ff_cur, ff_prev, 24);  // (ff_cur << 8) | (ff_prev >> 24)
+            bmq[q] = ff_cur & __builtin_amdgcn_alignbit(nz_nx, nz_cur, 8);     // (nz_cur >> 8) | (nz_nx << 24)
+            ndrop += __builtin_popcount(dmq[q]);
+            nbrk += __builtin_popcount(bmq[q]);
             ff_prev = ff_cur;
             ff_cur = ff_nx;
             nz_cur = nz_nx;
             zero_cur = zero_nx;
         }
-    } else {
+    }
+    if (!interior) {
+        ndrop = nbrk = 0;
 #pragma unroll 1
         for (int i = 0; i < 64; i++) {
             const uint32_t by = byte_of(w, i);
@@ -196,35 +201,26 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     uint32_t off = block_excl_scan(nbrk, s_wsum[1], &tot_brk);
     if (nbrk && interior) {
         // walk the break bits only (a wave with a break used to run a 64-byte loop): per word the
-        // same masks as the count above, then one iteration per break in it
+        // masks kept from the count above, one iteration per break in it; a word without a break
+        // in any lane of the wave costs two instructions
         Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
         uint32_t d = drop_before;
-        uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;
-        uint32_t ff_cur, nz_cur;
-        uint32_t zero_cur = scan_masks(w[0], ff_cur, nz_cur);
-        const uint32_t nznext = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = 0;
-            if (q < 15) zero_nx = scan_masks(w[q + 1], ff_nx, nz_nx);
-            const uint32_t pf = (ff_cur << 8) | (ff_prev >> 24);
-            const uint32_t nn = (nz_cur >> 8) | (nz_nx << 24);
-            const uint32_t dm = zero_cur & pf;
-            uint32_t bm = ff_cur & nn;
-            while (bm) {
-                const uint32_t bit = __builtin_ctz(bm);  // 7, 15, 23 or 31: byte k = bit >> 3
-                const uint32_t k = bit >> 3;
-                const uint32_t nbv = k < 3u ? (w[q] >> (8u * (k + 1u))) & 0xFFu : (q < 15 ? w[q < 15 ? q + 1 : q] & 0xFFu : nextb);
-                const uint32_t dd = d + __builtin_popcount(dm & ((1u << bit) - 1u));
-                const uint32_t is_term = (nbv & 0xF8u) == 0xD0u ? 0u : 1u;
-                out[off++] = Break{uint32_t(t0 + 4u * q + k - file), (dd << 1) | is_term};
-                bm &= bm - 1u;
+            const uint32_t dm = dmq[q];
+            uint32_t bm = bmq[q];
+            if (__any(bm != 0u)) {
+                while (bm) {
+                    const uint32_t bit = __builtin_ctz(bm);  // 7, 15, 23 or 31: byte k = bit >> 3
+                    const uint32_t k = bit >> 3;
+                    const uint32_t nbv = k < 3u ? (w[q] >> (8u * (k + 1u))) & 0xFFu : (q < 15 ? w[q < 15 ? q + 1 : q] & 0xFFu : nextb);
+                    const uint32_t dd = d + __builtin_popcount(dm & ((1u << bit) - 1u));
+                    const uint32_t is_term = (nbv & 0xF8u) == 0xD0u ? 0u : 1u;
+                    out[off++] = Break{uint32_t(t0 + 4u * q + k - file), (dd << 1) | is_term};
+                    bm &= bm - 1u;
+                }
             }
             d += __builtin_popcount(dm);
-            ff_prev = ff_cur;
-            ff_cur = ff_nx;
-            nz_cur = nz_nx;
-            zero_cur = zero_nx;
         }
     } else if (nbrk) {  // edge threads: byte by byte
         Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
@@ -365,6 +361,11 @@ __device__ __forceinline__ void store_run(uint32_t* s_out, uint32_t off, const u
         if (uint32_t(j) >= t && uint32_t(j) < n) so[off + j] = uint8_t(c[j >> 2] >> (8 * (j & 3)));
 }
 
+// Stuffed zeros per thread (64 bytes) removed in registers, one pass over the words each (a pass
+// runs when any lane of the wave has that many); a thread with more takes the byte-wise path.
+// Entropy-coded data has an FF (so a stuffed 00) in about 1 byte of 256: with 2, 13 % of the waves
+// had a lane beyond it and ran the byte path (~860 VALU); with 4, 0.04 %.
+constexpr int kFastDrops = 4;
 __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
     JD_PRIO_SHORT();
     __shared__ uint32_t s_out[kScanChunk / 4 + 4];
@@ -379,10 +380,10 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
     load64(t0, fend, w);
     const uint32_t prevb = (t0 > lo && t0 - 1 < fend) ? uint32_t(*reinterpret_cast<gu8*>(t0 - 1)) : 0u;
     // interior threads (all 64 bytes in the ECS): stuffed zeros from the SWAR masks of k_scan,
-    // their positions kept (the two highest); others: a per-byte keep mask
+    // their positions kept (the kFastDrops highest); others: a per-byte keep mask
     const bool interior = t0 >= lo && t0 + 64 <= fend;
     uint64_t keep = 0;
-    uint32_t nd = 0, p0 = 0, p1 = 0;
+    uint32_t nd = 0, pd[kFastDrops] = {};  // stuffed zeros, the positions of the highest kFastDrops (pd[0] highest)
     if (interior) {
         uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;
 #pragma unroll
@@ -392,15 +393,18 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
             uint32_t dm = zero & ((ff << 8) | (ff_prev >> 24));
             if (q == 0 && t0 == lo) dm &= ~0x80u;  // the ECS's first byte is never dropped
             ff_prev = ff;
-            while (dm) {
-                p1 = p0;
-                p0 = 4u * q + (uint32_t(__builtin_ctz(dm)) >> 3);
-                nd++;
-                dm &= dm - 1u;
+            if (__any(dm != 0u)) {  // (wave-uniform: a word without a stuffed zero in any lane is skipped)
+                while (dm) {
+#pragma unroll
+                    for (int r = kFastDrops - 1; r > 0; r--) pd[r] = pd[r - 1];
+                    pd[0] = 4u * q + (uint32_t(__builtin_ctz(dm)) >> 3);
+                    nd++;
+                    dm &= dm - 1u;
+                }
             }
         }
     }
-    if (!interior || nd > 2u) {
+    if (!interior || nd > uint32_t(kFastDrops)) {
 #pragma unroll
         for (int i = 0; i < 64; i++) {
             const uint32_t by = byte_of(w, i);
@@ -411,21 +415,22 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
             if (inr && !drop) keep |= 1ull << i;
         }
     }
-    const uint32_t nkeep = (interior && nd <= 2u) ? 64u - nd : uint32_t(__builtin_popcountll(keep));
+    const bool fast = interior && nd <= uint32_t(kFastDrops);
+    const uint32_t nkeep = fast ? 64u - nd : uint32_t(__builtin_popcountll(keep));
     uint32_t total;
     uint32_t off = block_excl_scan(nkeep, s_wsum, &total);
     uint8_t* so = reinterpret_cast<uint8_t*>(s_out);
-    if (interior && nd <= 2u) {
-        // common case: at most two stuffed zeros (a wave with one used to run a 64-byte loop):
-        // remove them, highest first, by shifting the later bytes down one (a funnel shift and a
+    if (fast) {
+        // common case: at most kFastDrops stuffed zeros (a wave with one used to run a 64-byte
+        // loop): remove them, highest first, by shifting the later bytes down one (a funnel shift and a
         // bit-field insert per word), then store the run
         uint32_t cw[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) cw[q] = w[q];
 #pragma unroll
-        for (int r = 0; r < 2; r++) {
+        for (int r = 0; r < kFastDrops; r++) {
             if (uint32_t(r) < nd) {
-                const uint32_t p = r == 0 ? p0 : p1;
+                const uint32_t p = pd[r];
                 const uint32_t qp = p >> 2, lowm = (1u << (8u * (p & 3u))) - 1u;
 #pragma unroll
                 for (int q = 0; q < 16; q++) {
@@ -1897,7 +1902,9 @@ __global__ __launch_bounds__(256) void k_dc_sum(BatchDev b) {
     JD_PRIO_SHORT();
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t nt = im.tiles_x * im.tiles_y, lane = threadIdx.x & 63u;
-    const uint32_t tile0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kDcTilesPerWave;
+    // (readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform, and would
+    // divide in vector registers, ~30 VALU per division, four tiles x two divisions per wave)
+    const uint32_t tile0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + (threadIdx.x >> 6)) * kDcTilesPerWave);
     if (tile0 >= nt) return;  // wave-uniform
     TileLane t[kDcTilesPerWave];
 #pragma unroll
