@@ -197,6 +197,7 @@ struct jd_ctx {
     int slot = 0;  // the slot the next launch uses
     const void* last_stream = nullptr;  // caller stream of the pending launches (nullptr: the slots' own)
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
+    int max_batch_images = 0;           // items per launched sub-batch (JD_MAX_BATCH_IMAGES)
     int64_t spare_pieces = -1;          // spare re-walk regions per image (JD_SPARE_PIECES; -1: default)
     int64_t piece_overlap = -1;         // warm-up bits (JD_PIECE_OVERLAP_BITS; -1: default)
     bool fixed_pieces = false;          // JD_FIXED_PIECES: keep the host's piece size (no k_pieceplan)
@@ -347,14 +348,18 @@ struct Plan {
 
 // Largest item prefix [lo, hi) whose sparse-coefficient words stay within the context's
 // max_batch_entries (default kMaxBatchEntries; entry indices are image-relative, this only bounds
-// the pool, 4 B per word; estimated at full-size pieces).  JD_MAX_BATCH_ENTRIES overrides it
-// (tests force multi-way splits).
+// the pool, 4 B per word; estimated at full-size pieces) and that holds at most max_batch_images
+// items (default kMaxBatchImages: the per-image kernels index images by the grid's y dimension,
+// at most 65535).  JD_MAX_BATCH_ENTRIES / JD_MAX_BATCH_IMAGES override them (tests force
+// multi-way splits).
 constexpr uint64_t kMaxBatchEntries = 8ull << 30;
+constexpr int kMaxBatchImages = 65535;
 int batch_split(jd_ctx* ctx, int lo, int n, const jd_item* items) {
     const uint64_t limit = ctx->max_batch_entries;
     uint64_t cap = 0;
     int hi = lo;
     for (; hi < n; hi++) {
+        if (hi - lo >= ctx->max_batch_images) break;
         if (ctx->pst[hi] != JD_OK) continue;
         const jd_header& h = ctx->parsed[hi].hdr;
         const uint64_t w = entry_words(items[hi].len - h.ecs_offset, image_segments(h), kPieceBits, -1,
@@ -1098,6 +1103,11 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_MAX_BATCH_ENTRIES")) {
         const unsigned long long v = std::strtoull(e, nullptr, 0);
         if (v > 0) ctx->max_batch_entries = v;
+    }
+    ctx->max_batch_images = kMaxBatchImages;
+    if (const char* e = std::getenv("JD_MAX_BATCH_IMAGES")) {
+        const long v = std::strtol(e, nullptr, 0);
+        if (v > 0 && v < kMaxBatchImages) ctx->max_batch_images = int(v);
     }
     // test knobs: fewer spare regions (re-walks fall back to their own region, no join) and a
     // shorter warm-up (many speculative starts fail)

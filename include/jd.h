@@ -123,7 +123,9 @@ jd_status jd_decode_file(jd_ctx* ctx, const char* path, uint8_t* rgb, size_t rgb
  * hip_stream: hipStream_t to order the work on, or NULL for the context's own stream.  The call
  * returns after the batch completes; per-image status in results[i].  The context's scratch pools
  * are ordered by stream only: a call on another stream than the one of still-pending
- * jd_decode_batch_async launches first collects them (jd_decode_wait). */
+ * jd_decode_batch_async launches first collects them (jd_decode_wait).  Any n: the library
+ * launches the batch in sub-batches of at most 65535 items (and of at most a device-pool budget of
+ * sparse coefficients), each collected before the next. */
 jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
                           int rgb_on_device, void* hip_stream);
 

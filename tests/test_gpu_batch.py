@@ -117,6 +117,28 @@ def test_forced_split_host_inputs_and_outputs(monkeypatch):
         dec.close()
 
 
+def test_forced_split_by_image_count(monkeypatch):
+    """Sub-batches hold at most 65535 items (the per-image kernels index images by the grid's y
+    dimension); JD_MAX_BATCH_IMAGES lowers the cap so that a small batch splits the same way, with
+    an item that fails to parse inside one of the sub-batches."""
+    datas = jd_synth.make_batch(13, 320, 240, 90, "4:2:0", 1, 0, seed0=7300)
+    datas += jd_synth.make_batch(6, 256, 256, 80, "4:4:4", 0, 0, seed0=7400)
+    datas.insert(9, b"\xff\xd8\xff\xd9")  # not a decodable JPEG
+    monkeypatch.setenv("JD_MAX_BATCH_IMAGES", "5")
+    dec = jdamd.Decoder(0)
+    try:
+        outs, status = dec.decode_batch(datas)
+        for i, (d, o, st) in enumerate(zip(datas, outs, status)):
+            if i == 9:
+                assert st != 0
+                continue
+            ref_st, ref = jdoracle.decode(d)
+            assert st == 0 and ref_st == 0 and np.array_equal(o, ref), i
+        assert dec.stats()["batches"] >= 4  # 20 items, at most 5 per sub-batch
+    finally:
+        dec.close()
+
+
 def test_async_then_blocking_call_on_another_stream():
     """a pending jd_decode_batch_async batch on the context stream, then a
     blocking call on another stream: the scratch pools must not be overwritten under it."""
