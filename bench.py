@@ -51,10 +51,20 @@ CONFIGS = {
     "c3": (3840, 2160, "4:2:0", 1, 256, "256 x 3840x2160 4:2:0 q90, DRI = 1 MCU row (BASELINE config 3)"),
     "c5": (1920, 1080, "mixed", 0, 1024, "1024 x 1080p mixed 4:4:4/4:2:2/4:2:0, q in {50,75,90,95}, no RST "
                                          "(BASELINE config 5)"),
+    # the reference's own benchmark format (4:4:4 q95: data_preprocessing/image_converter.py:6,18) at
+    # its latency-benchmark sizes 200^2 .. 2000^2 (cuda-decoder/benchmark/benchmark.cu:87), image i
+    # of size REF_SIZES[i % 10], in its throughput benchmark's batch of 3000
+    # (cuda-decoder/benchmark_thoughput/benchmark.cu:30); --sweep adds its two published curves
+    "ref444": (0, 0, "ref", 0, 3000, "3000 x 4:4:4 q95, sizes 200^2..2000^2 cycling, no RST (the reference's "
+                                     "benchmark format)"),
     # config 2 with libjpeg's fancy upsampling (JD_FLAG_FANCY_UPSAMPLING; --fancy on any config)
     "c2f": (1920, 1080, "4:2:0", 1, 1024, "1024 x 1920x1080 4:2:0 q90, DRI = 1 MCU row, fancy upsampling "
                                           "(BASELINE config 2 shape, an option beyond the reference)"),
 }
+REF_SIZES = (200, 400, 600, 800, 1000, 1200, 1400, 1600, 1800, 2000)  # cuda-decoder/benchmark/benchmark.cu:87
+REF_QUALITY = 95                                                      # data_preprocessing/image_converter.py:6
+REF_BATCHES = (1, 10, 50, 100, 250, 500, 1000, 3000)                  # figures/batchsize.pdf's range
+REF_PUBLISHED_MB_S = 552.0  # CUDA decoder, batch 3000, RTX 2080 Ti, kernel time only
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SIMDS = 1024               # 256 CUs x 4 SIMD-32
 # SQ_ACTIVE_INST_VALU counts quad-cycles (MI355X_MICROARCH.md); on gfx950 most 32-bit integer VALU
@@ -150,6 +160,12 @@ def shard_seeds(config: str, batch: int, rank: int, world: int):
     return sorted(mine)
 
 
+def ref444_jobs(seeds, quality: int = REF_QUALITY):
+    """jd_synth jobs of the ref444 workload: image `seed` is REF_SIZES[seed % 10] square, 4:4:4, no DRI."""
+    return [(REF_SIZES[s % len(REF_SIZES)], REF_SIZES[s % len(REF_SIZES)], int(s), quality, "4:4:4", 0, 0, None)
+            for s in seeds]
+
+
 def numa_cpus(device_index: int):
     """Host CPUs of the GPU's NUMA node that this process may run on (None if unknown)."""
     try:
@@ -211,15 +227,18 @@ def gather_matrix(local, world: int):
 
 RANK_FIELDS = ["elapsed_s", "pixels", "images", "ecs_bytes", "jpeg_bytes", "ecs_bytes_per_step",
                "images_per_step", "ms_per_step", "parse_ms", "plan_ms", "stage_ms", "wait_ms", "e2e_ms",
-               "h2d_GB_s", "e2e_registered_ms"]
+               "h2d_GB_s", "e2e_registered_ms", "e2e_pinned_arena_ms"]
 
 
-def rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, steps, host_ms_step, e2e_ms, h2d_gbs, reg_ms=0.0):
+def rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, steps, host_ms_step, e2e_ms, h2d_gbs, reg_ms=0.0,
+                arena_ms=0.0):
     """This rank's counter vector for the one all-gather (order: RANK_FIELDS; column 0 = elapsed
-    is max-reduced, 1-4 summed)."""
+    is max-reduced, 1-4 summed).  The three H2D-inclusive legs (staged, registered arena, pinned
+    arena) are reported separately, each from its own timed run."""
     return [elapsed, pixels * steps, n * steps, ecs * steps, jpeg_bytes * steps, ecs, n,
             elapsed / max(1, steps) * 1e3, host_ms_step.get("parse", 0.0), host_ms_step.get("plan", 0.0),
-            host_ms_step.get("stage_inputs", 0.0), host_ms_step.get("wait", 0.0), e2e_ms, h2d_gbs, reg_ms]
+            host_ms_step.get("stage_inputs", 0.0), host_ms_step.get("wait", 0.0), e2e_ms, h2d_gbs, reg_ms,
+            arena_ms]
 
 
 def per_rank_table(allc, steps):
@@ -229,6 +248,88 @@ def per_rank_table(allc, steps):
     out = {k: [round(float(x), 4) for x in allc[:, RANK_FIELDS.index(k)]] for k in keys}
     host = allc[:, 8] + allc[:, 9]
     out["host_parse_plan_over_step"] = [round(float(h / m), 4) if m > 0 else None for h, m in zip(host, allc[:, 7])]
+    return out
+
+
+def rank0_measurements(rank: int, world: int, copy_fn=None, cpu_fn=None):
+    """The line's single-host measurements, run by rank 0 only and after the counter all-gather (so
+    they never overlap any rank's timed region): the in-run HBM copy peak on rank 0's GPU and the
+    CPU baseline on rank 0's host cores (north_star: the reference's CPU decoder "in the same run",
+    at any world size).  The other ranks wait at a barrier meanwhile, so no rank's GPU or host work
+    competes with them.  Returns {"copy_peak": GB/s or None, "cpu_baseline": dict or None}."""
+    import torch.distributed as dist
+
+    out = {"copy_peak": None, "cpu_baseline": None}
+    if rank == 0:
+        if copy_fn is not None:
+            out["copy_peak"] = copy_fn()
+        if cpu_fn is not None:
+            out["cpu_baseline"] = cpu_fn()
+    if world > 1:
+        dist.barrier()
+    return out
+
+
+def roofline_block(kern: dict, config: str, copy_gbs, kernel_steps: int, rocprof_ms=None):
+    """The line's `roofline` object for the dominant kernel slot: algorithmic bytes per launch over
+    its average hipEvent launch time against the 8 TB/s HBM peak and the in-run copy peak, its PMC
+    traffic and VALU issue model.  When the two largest slots are within 1 % by hipEvents, the
+    committed rocprofv3 averages (`rocprof_ms`, profiles/*_kernel_stats.csv) pick the dominant one;
+    within 5 %, `co_dominant` gives the runner-up's figures too."""
+    by_time = sorted((k for k in kern if kern[k]["launches"]), key=lambda k: kern[k]["total_ms"] / kern[k]["launches"],
+                     reverse=True)
+    avg = {k: kern[k]["total_ms"] / max(1, kern[k]["launches"]) for k in by_time}
+    if (len(by_time) > 1 and rocprof_ms and by_time[0] in rocprof_ms and by_time[1] in rocprof_ms
+            and avg[by_time[1]] >= 0.99 * avg[by_time[0]] and rocprof_ms[by_time[1]] > rocprof_ms[by_time[0]]):
+        by_time[0], by_time[1] = by_time[1], by_time[0]
+        picked = "rocprofv3 averages (hipEvent times within 1 %)"
+    else:
+        picked = "hipEvent averages"
+
+    def figures(name):
+        k = kern[name]
+        ms = avg[name]
+        b = k["bytes"] / max(1, k["launches"])
+        a = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        vb = valu_issue(config, name, ms)
+        tr = measured_traffic(config, name)
+        bound = "valu" if vb and vb["busy_frac"] > 0.7 else "hbm" if a / HBM_PEAK_GBS > 0.5 else "latency"
+        return ms, b, a, vb, tr, bound
+
+    dom = by_time[0]
+    ms, b, a, vb, tr, bound = figures(dom)
+    co_dom = None
+    if len(by_time) > 1 and avg[by_time[1]] >= 0.95 * ms:
+        ms2, b2, a2, vb2, tr2, bound2 = figures(by_time[1])
+        co_dom = {"kernel": by_time[1], "avg_launch_ms": ms2, "algorithmic_bytes_per_launch": b2, "achieved": a2,
+                  "frac": a2 / HBM_PEAK_GBS, "traffic": tr2[0] if tr2 else None, "valu": vb2, "bound": bound2}
+    # the roof that binds: VALU issue when the committed SQ profile shows the SIMDs busy, HBM when the
+    # byte stream is near its peak, else neither (a latency- / parallelism-bound launch, e.g. C1's
+    # one image on a few CUs)
+    return {"bound": bound, "kernel": dom, "kernel_picked_by": picked, "achieved": a, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": a / HBM_PEAK_GBS, "traffic": tr[0] if tr else None,
+            "traffic_source": tr[1] if tr else None, "measured_copy_peak": copy_gbs,
+            "frac_of_measured_peak": a / copy_gbs if copy_gbs else None, "valu": vb, "avg_launch_ms": ms,
+            "algorithmic_bytes_per_launch": b,
+            "timing": f"hipEvents on the decode stream, {max(1, kernel_steps)} serialized batches",
+            "co_dominant": co_dom}
+
+
+def rocprof_averages(config: str):
+    """Per kernel slot: the average duration (ms) in the newest committed rocprofv3 --stats summary
+    of this config (profiles/<tag>_<config>_kernel_stats.csv), or None."""
+    import csv
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_kernel_stats.csv")), key=_profile_order,
+                   reverse=True)
+    if not files:
+        return None
+    out = {}
+    for r in csv.DictReader(open(files[0])):
+        name = r["Name"].split("(")[0].replace("void ", "").replace("jd::", "").split("<")[0]
+        slot = {"k_dc_sum": "k_dc_pred", "k_dc_scan": "k_dc_pred", "k_pieceplan": "k_subplan",
+                "k_chain_fix": "k_chain", "k_idct_color_exact": "k_idct_color"}.get(name, name)
+        out[slot] = out.get(slot, 0.0) + float(r["AverageNs"]) / 1e6  # instances of a slot: one each per batch
     return out
 
 
@@ -459,6 +560,96 @@ def cpu_baseline(hosts, hdrs, target_s: float = 5.0):
     return res
 
 
+def ref_sweep(dec, datas, hosts, hdrs, in_ptrs, rgb_bufs, out_offs, dev, reps: int = 5):
+    """The reference's two published curves on its own format (ref444), GPU beside its CPU decoder:
+      batch   throughput vs batch size B in REF_BATCHES (figures/batchsize.pdf; method
+              cuda-decoder/benchmark_thoughput/benchmark.cu:43-106: batches decoded one after another,
+              JPEG file bytes / time): `serial` = one blocking jd_decode_batch per batch (host parse +
+              plan + kernels + status readback, the reference's loop without its per-image
+              cudaMalloc), `kernel_ms` = the sum of the batch's kernel hipEvents (the reference's
+              cudaEvent pair around batchDecodeKernel), `pipelined` = jd_decode_batch_async steady state
+      latency single-image decode per size (figures/runtime.png; cuda-decoder/benchmark/benchmark.cu:
+              29-100: 10 iterations per image, cudaEvent around decodeKernel): median wall time of a
+              blocking one-image jd_decode_batch and its kernel hipEvent sum, next to the reference's
+              C++ decoder (oracle/_ref/ref_bench: extract + decode, cpp-decoder/benchmark/
+              benchmark.cc:29-35) on the same files, 1 thread"""
+    import numpy as np
+    import torch
+
+    import jdoracle
+
+    n = len(datas)
+    jbytes = [len(d) for d in datas]
+    out = {"published_MB_s_batch3000": REF_PUBLISHED_MB_S, "published_hw": "RTX 2080 Ti (BASELINE.md §1)",
+           "format": f"4:4:4 q{REF_QUALITY}, no RST, sizes {REF_SIZES[0]}^2..{REF_SIZES[-1]}^2 cycling by image",
+           "batch": [], "latency": []}
+
+    def kernel_ms(st):
+        return sum(v["total_ms"] for v in st["kernels"].values())
+
+    for B in REF_BATCHES:
+        B = min(B, n)
+        sets = [dec.make_batch(hosts[:B], in_ptrs[:B], [rb.data_ptr() + o for o in out_offs[:B]]) for rb in rgb_bufs]
+        mb = sum(jbytes[:B]) / 1e6
+        px = float(sum(h.width * h.height for h in hdrs[:B]))
+        r = max(2, min(reps * 4, int(20000 // B)))  # ~20 K images per point, at least 2 batches
+        dec.decode_prepared(sets[0], pipelined=False)
+        dec.reset_stats()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for k in range(r):
+            dec.decode_prepared(sets[k % len(sets)], pipelined=False)
+        torch.cuda.synchronize(dev)
+        ser = (time.perf_counter() - t) / r
+        kms = kernel_ms(dec.stats()) / r
+        for k in range(len(sets)):
+            dec.decode_prepared(sets[k], pipelined=True)
+        dec.wait()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for k in range(r):
+            dec.decode_prepared(sets[k % len(sets)], pipelined=True)
+        dec.wait()
+        torch.cuda.synchronize(dev)
+        pip = (time.perf_counter() - t) / r
+        if any(x.status for st in sets for x in st[1]):
+            raise SystemExit(f"ref444 sweep: decode failed at batch {B}")
+        out["batch"].append({"images": B, "jpeg_MB": mb, "serial_ms": ser * 1e3, "kernel_ms": kms,
+                             "pipelined_ms": pip * 1e3, "serial_MB_s": mb / ser, "kernel_MB_s": mb / (kms * 1e-3),
+                             "pipelined_MB_s": mb / pip, "pipelined_MPix_s": px / pip / 1e6,
+                             "vs_published_batch3000_kernel": mb / (kms * 1e-3) / REF_PUBLISHED_MB_S,
+                             "batches_timed": r})
+    per_size = 5  # images of each size (the reference: every file of its size folder)
+    with tempfile.TemporaryDirectory() as td:
+        for si, size in enumerate(REF_SIZES):
+            idx = [i for i in range(n) if i % len(REF_SIZES) == si][:per_size]
+            walls, kerns, paths = [], [], []
+            for i in idx:
+                one = dec.make_batch([hosts[i]], [in_ptrs[i]], [rgb_bufs[0].data_ptr() + out_offs[i]])
+                dec.decode_prepared(one, pipelined=False)
+                ws = []
+                dec.reset_stats()
+                for _ in range(10):
+                    t = time.perf_counter()
+                    dec.decode_prepared(one, pipelined=False)
+                    ws.append(time.perf_counter() - t)
+                kerns.append(kernel_ms(dec.stats()) / 10)
+                walls.append(float(np.median(ws)) * 1e3)
+                path = os.path.join(td, f"{size}_{i}.jpeg")
+                with open(path, "wb") as f:
+                    f.write(datas[i])
+                paths.append(path)
+            ref = None
+            if os.path.exists(jdoracle.REF_BENCH):
+                rr = ref_bench(paths, 1, 2 if size >= 1400 else 5)
+                ref = 1e3 / rr[0] if rr else None  # ms per image, 1 process
+            out["latency"].append({"size": size, "images": len(idx), "gpu_wall_ms_median": float(np.median(walls)),
+                                   "gpu_kernel_ms": float(np.median(kerns)), "ref_cpu_ms": ref,
+                                   "gpu_MPix_s": size * size / float(np.median(walls)) / 1e3,
+                                   "ref_cpu_MPix_s": size * size / ref / 1e3 if ref else None})
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -467,7 +658,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override images per rank")
-    ap.add_argument("--quality", type=int, default=90)
+    ap.add_argument("--quality", type=int, default=0, help="JPEG quality (default: 90; ref444: 95)")
+    ap.add_argument("--sweep", action="store_true",
+                    help="ref444: print the reference's two published curves instead of the bench line: "
+                         "throughput vs batch size (JPEG MB/s) and single-image latency per size, next to the "
+                         "reference's own CPU decoder (oracle/_ref/ref_bench) on the same files")
     ap.add_argument("--cpu-sample", type=int, default=1, help="1: time the CPU baselines, 0: skip")
     ap.add_argument("--verify", type=int, default=1, help="check images {0, n/2, n-1} bit-exact vs the oracle")
     ap.add_argument("--e2e-steps", type=int, default=24, help="steps of each H2D-inclusive leg (0: skip; the last batch's kernels after its DMA are ~6 ms of pipeline drain, so few steps understate the rate)")
@@ -505,8 +700,12 @@ def main():
         batch = args.batch
     seeds = shard_seeds(args.config, batch, rank, world)  # disjoint images per rank: shard by image
     t_gen = time.time()
-    jobs = jd_synth.make_jobs(seeds, W, H, args.quality, "4:2:0" if ss == "mixed" else ss, rrows, 0,
-                              mixed=(ss == "mixed"))
+    quality = args.quality or (REF_QUALITY if ss == "ref" else 90)
+    if ss == "ref":
+        jobs = ref444_jobs(seeds, quality)
+    else:
+        jobs = jd_synth.make_jobs(seeds, W, H, quality, "4:2:0" if ss == "mixed" else ss, rrows, 0,
+                                  mixed=(ss == "mixed"))
     datas = jd_synth.make_images(jobs)
     t_gen = time.time() - t_gen
     n = len(datas)
@@ -522,9 +721,11 @@ def main():
         otot += (h.width * h.height * 3 + 255) // 256 * 256
     # device memory through torch (plumbing); the decoder gets raw pointers over the C ABI
     jpeg_dev = torch.empty(tot, dtype=torch.uint8, device=dev)
-    # two output buffers: consecutive pipelined batches (in flight together on the decoder's two
-    # slot streams) write different memory, as distinct batches of a real stream would
-    rgb_bufs = [torch.empty(otot, dtype=torch.uint8, device=dev) for _ in range(2)]
+    # three output buffers: consecutive pipelined batches write different memory, as distinct
+    # batches of a real stream would; jd_decode_batch_async keeps two batches in flight and a
+    # batch's buffers are free again once it is collected, two calls later (include/jd.h)
+    rgb_bufs = [torch.empty(otot, dtype=torch.uint8, device=dev) for _ in range(3 if not args.no_pipeline else 1)]
+    nb = len(rgb_bufs)
     flat = np.zeros(tot, np.uint8)
     for h, o in zip(hosts, in_offs):
         flat[o:o + h.nbytes] = h
@@ -540,8 +741,8 @@ def main():
     jpeg_bytes = float(sum(len(x) for x in datas))
 
     pipelined = not args.no_pipeline
-    for w in range(max(2, args.warmup)):
-        dec.decode_prepared(batches[w & 1], pipelined=pipelined)
+    for w in range(max(nb, args.warmup)):
+        dec.decode_prepared(batches[w % nb], pipelined=pipelined)
     dec.wait()
     status = [r.status for b in batches for r in b[1]]
     if any(status) and args.verify:  # --verify 0: ablation builds decode wrong on purpose
@@ -561,6 +762,16 @@ def main():
                     raise SystemExit(f"bit-exactness check failed on image {i}")
             verified.append(i)
 
+    if args.sweep:
+        if ss != "ref" or world > 1:
+            raise SystemExit("--sweep: --config ref444 on one GPU")
+        res = ref_sweep(dec, datas, hosts, hdrs, [jpeg_dev.data_ptr() + o for o in in_offs], rgb_bufs, out_offs, dev)
+        res.update({"metric": "ref444 sweep (throughput vs batch, latency vs size)", "verified_bit_exact": verified,
+                    "cpu_model": cpu_model(), "gen_s": t_gen})
+        print(json.dumps(res))
+        dec.close()
+        return
+
     dec.reset_stats()
     torch.cuda.reset_peak_memory_stats(dev)
     if world > 1:
@@ -568,7 +779,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        dec.decode_prepared(batches[k & 1], pipelined=pipelined)
+        dec.decode_prepared(batches[k % nb], pipelined=pipelined)
     dec.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -583,18 +794,18 @@ def main():
     # includes the other batch's kernels
     dec.reset_stats()
     for k in range(max(1, args.kernel_steps)):
-        dec.decode_prepared(batches[k & 1], pipelined=False)
+        dec.decode_prepared(batches[k % nb], pipelined=False)
     st = dec.stats()
 
     # PCIe-inclusive rate (not `value`): the JPEG bytes handed over in host memory, RGB to HBM;
     # pipelined like the timed loop (the host stages batch k+1 while the GPU decodes batch k), run
     # by every rank at once so a multi-GPU run shows the shared host's feed rate
     e2e = None
-    e2e_ms = h2d_gbs = reg_ms = 0.0
+    e2e_ms = h2d_gbs = reg_ms = arena_ms = 0.0
     if args.e2e_steps:
         def e2e_leg(batches):
             """The pipelined timed loop over host-input batches: (seconds, library stats)."""
-            for k in range(2):
+            for k in range(len(batches)):
                 dec.decode_prepared(batches[k], pipelined=True)
             dec.wait()
             dec.reset_stats()
@@ -603,7 +814,7 @@ def main():
             torch.cuda.synchronize(dev)
             t = time.perf_counter()
             for k in range(args.e2e_steps):
-                dec.decode_prepared(batches[k & 1], pipelined=True)
+                dec.decode_prepared(batches[k % len(batches)], pipelined=True)
             dec.wait()
             torch.cuda.synchronize(dev)
             t = time.perf_counter() - t
@@ -646,7 +857,8 @@ def main():
         dec.host_free(parena)
         del parena, pviews
         e2e_ms = te / args.e2e_steps * 1e3
-        reg_ms = min(tr, tp) / args.e2e_steps * 1e3
+        reg_ms = tr / args.e2e_steps * 1e3
+        arena_ms = tp / args.e2e_steps * 1e3
         h2d_gbs = pinned_h2d_gbs(int(jpeg_bytes), dev)
         bound_ms = jpeg_bytes / (h2d_gbs * 1e9) * 1e3
         e2e = leg_dict(te, se, 3 * jpeg_bytes,
@@ -666,36 +878,21 @@ def main():
 
     # one all-gather of per-rank counters (RCCL over xGMI when N > 1): totals for the line, and
     # every rank's step time and host feed (so an 8-GPU run shows whether the host binds)
-    local = torch.tensor(rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, args.steps, host_ms_step, e2e_ms, h2d_gbs, reg_ms),
+    local = torch.tensor(rank_vector(elapsed, pixels, n, ecs, jpeg_bytes, args.steps, host_ms_step, e2e_ms, h2d_gbs, reg_ms,
+                                     arena_ms),
                          dtype=torch.float64, device=dev if d["backend"] == "nccl" else "cpu")
     allc = gather_matrix(local, world)
     t_max = float(allc[:, 0].max())
     tot_px, tot_img, tot_ecs, tot_bytes = (float(allc[:, k].sum()) for k in range(1, 5))
 
+    # rank 0's single-host measurements after the gather, at every world size (the others wait)
+    extra = rank0_measurements(rank, world,
+                               copy_fn=(lambda: copy_peak_gbs(dec, dev)) if args.copy_peak else None,
+                               cpu_fn=(lambda: cpu_baseline(hosts, hdrs)) if args.cpu_sample else None)
     if rank == 0:
         kern = st["kernels"]
-        by_time = sorted(kern, key=lambda k: kern[k]["total_ms"], reverse=True)
-        dom = by_time[0]
-        kd = kern[dom]
-        avg_ms = kd["total_ms"] / max(1, kd["launches"])
-        per_launch_bytes = kd["bytes"] / max(1, kd["launches"])
-        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic = measured_traffic(args.config, dom)
-        copy_gbs = copy_peak_gbs(dec, dev) if (args.copy_peak and world == 1) else None
-        vb = valu_issue(args.config, dom, avg_ms)
-        co_dom = None  # the runner-up when the two big kernels are within 5 % of each other
-        if len(by_time) > 1 and kern[by_time[1]]["total_ms"] >= 0.95 * kd["total_ms"]:
-            k2 = kern[by_time[1]]
-            ms2 = k2["total_ms"] / max(1, k2["launches"])
-            b2 = k2["bytes"] / max(1, k2["launches"])
-            a2 = b2 / (ms2 * 1e-3) / 1e9 if ms2 > 0 else 0.0
-            vb2 = valu_issue(args.config, by_time[1], ms2)
-            tr2 = measured_traffic(args.config, by_time[1])
-            co_dom = {"kernel": by_time[1], "avg_launch_ms": ms2, "algorithmic_bytes_per_launch": b2,
-                      "achieved": a2, "frac": a2 / HBM_PEAK_GBS, "traffic": tr2[0] if tr2 else None,
-                      "valu": vb2, "bound": ("valu" if vb2 and vb2["busy_frac"] > 0.7 else
-                                             "hbm" if a2 / HBM_PEAK_GBS > 0.5 else "latency")}
-        cpu = cpu_baseline(hosts, hdrs) if (args.cpu_sample and world == 1) else None
+        copy_gbs = extra["copy_peak"]
+        cpu = extra["cpu_baseline"]
         px_rank = float(sum(h.width * h.height for h in hdrs))
         res = {
             "metric": "MPixels/s decoded (and images/s) at 1/2/4/8 MI355X; % HBM roofline",
@@ -710,10 +907,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": f"synthetic (seeded sinusoid + noise, baseline encode "
-                    f"{'q in {50,75,90,95}' if ss == 'mixed' else f'q{args.quality}'} by "
+                    f"{'q in {50,75,90,95}' if ss == 'mixed' else f'q{quality}'} by "
                     f"{'tools/jdenc.c' if jd_synth.default_encoder() == 'jdenc' else 'Pillow'}, std Huffman tables)",
             "config": {"workload": desc, "config": args.config, "images_per_rank": n,
-                       "global_batch": int(allc[:, 6].sum()), "width": W, "height": H, "subsampling": ss,
+                       "global_batch": int(allc[:, 6].sum()), "width": W or list(REF_SIZES), "height": H or list(REF_SIZES),
+                       "subsampling": "4:4:4" if ss == "ref" else ss,
                        "restart_rows": rrows, "parallelism": f"dp{world} (image sharding)",
                        "entropy_path": args.path, "host_pipelined": pipelined,
                        "upsampling": "fancy (libjpeg triangular)" if args.fancy else "replicate",
@@ -727,20 +925,7 @@ def main():
             "images_per_s": tot_img / t_max,
             "jpeg_MB_per_s": tot_bytes / t_max / 1e6,
             "ecs_MB_per_s": tot_ecs / t_max / 1e6,
-            # the roof that binds: VALU issue when the committed SQ profile shows the SIMDs busy, HBM
-            # when the byte stream is near its peak, else neither (a latency- / parallelism-bound launch,
-            # e.g. C1's one image on a few CUs)
-            "roofline": {"bound": ("valu" if vb and vb["busy_frac"] > 0.7 else
-                                   "hbm" if achieved / HBM_PEAK_GBS > 0.5 else "latency"), "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic[0] if traffic else None,
-                         "traffic_source": traffic[1] if traffic else None,
-                         "measured_copy_peak": copy_gbs,
-                         "frac_of_measured_peak": achieved / copy_gbs if copy_gbs else None,
-                         "valu": vb,
-                         "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes,
-                         "timing": f"hipEvents on the decode stream, {max(1, args.kernel_steps)} serialized batches",
-                         "co_dominant": co_dom},
+            "roofline": roofline_block(kern, args.config, copy_gbs, args.kernel_steps, rocprof_averages(args.config)),
             "kernel_rooflines": kernel_rooflines(kern, args.config),
             "kernels_ms_per_step": {k: v["total_ms"] / max(1, v["launches"]) for k, v in kern.items()},
             "kernels_ms_per_step_overlapped": {k: v["total_ms"] / max(1, v["launches"])

@@ -2738,6 +2738,10 @@ __device__ __forceinline__ void load_entry_quads(const EntryRange& r, uint4 (&E)
 // Per slot one compare against the quad's limit (slot q is the block's when q < lead + cnt - 8 qi,
 // and, in quad 0, q >= lead); both values of a word by one packed arithmetic shift, the high one
 // stored from the word's upper half (ds_write_b16_d16_hi).
+#ifndef JD_ABL_SCATTER
+#define JD_ABL_SCATTER 0  // diagnostic builds (wrong pixels): 1 = every slot to a fixed, bank-conflict-free
+                          // position of its row; 2 = no scatter stores
+#endif
 __device__ __forceinline__ void scatter_quad(uint8_t* s_bytes, uint32_t base, const uint4& v, int qi,
                                              const EntryRange& r) {
     typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -2746,6 +2750,16 @@ __device__ __forceinline__ void scatter_quad(uint8_t* s_bytes, uint32_t base, co
 #pragma unroll
     for (int d = 0; d < 4; d++) {
         const s16x2 val = __builtin_bit_cast(s16x2, w[d]) >> short(6);
+        if (JD_ABL_SCATTER == 2) {
+            if (2 * d < lim) __builtin_amdgcn_sched_barrier(0);
+            continue;
+        }
+        if (JD_ABL_SCATTER == 1) {  // dword (l + d) mod 32 of the lane's row: bank (l + d) mod 32
+            const uint32_t a = (base & ~127u) | (((threadIdx.x + uint32_t(d)) & 31u) << 2);
+            if (2 * d < lim && (qi > 0 || 2 * d >= int(r.lead))) *reinterpret_cast<int16_t*>(s_bytes + a) = val.x;
+            if (2 * d + 1 < lim && (qi > 0 || 2 * d + 1 >= int(r.lead))) *reinterpret_cast<int16_t*>(s_bytes + (a | 2u)) = val.y;
+            continue;
+        }
         if (2 * d < lim && (qi > 0 || 2 * d >= int(r.lead)))
             *reinterpret_cast<int16_t*>(s_bytes + (base ^ ((w[d] << 1) & 0x7Eu))) = val.x;
         if (2 * d + 1 < lim && (qi > 0 || 2 * d + 1 >= int(r.lead)))

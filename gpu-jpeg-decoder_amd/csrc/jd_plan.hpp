@@ -52,13 +52,19 @@ inline uint32_t adaptive_piece_bits(uint64_t ecs_bits) {
 
 // An image's AC-entry offsets are image-relative 32-bit values in 16-bit slot units
 // (BlockInfo::entry_start, k_gather's running offset): its reservation must stay below 2^31
-// words, else the plan rejects it with JD_ERR_CAPACITY.  piece_bits: the shortest pieces any
-// batch holding the image can get (adaptive_piece_bits of its own bits, or a forced size); div:
-// its region divisor.
+// words, else the plan rejects it with JD_ERR_CAPACITY.  The reservation is made at the batch's
+// piece size, which lies between the shortest pieces any batch holding the image can get
+// (pmin: adaptive_piece_bits of its own bits) and pmax (kPieceBits; a forced size gives pmin =
+// pmax), always a power-of-two multiple of pmin.  entry_words is not monotonic in the piece size
+// (the spare regions grow with it, the per-piece slack shrinks), so every candidate is checked.
+// div: the image's region divisor.
 constexpr uint64_t kMaxImageEntryWords = 0x7FFFFF00ull;
-inline bool image_fits(uint64_t ecs_bytes, const jd_header& h, uint32_t piece_bits, int64_t spare_pieces = -1,
+inline bool image_fits(uint64_t ecs_bytes, const jd_header& h, uint32_t pmin, uint32_t pmax, int64_t spare_pieces = -1,
                        uint32_t div = 2u) {
-    return entry_words(ecs_bytes, image_segments(h), piece_bits, spare_pieces, div) <= kMaxImageEntryWords;
+    for (uint64_t p = pmin;; p *= 2) {
+        if (entry_words(ecs_bytes, image_segments(h), uint32_t(p), spare_pieces, div) > kMaxImageEntryWords) return false;
+        if (p >= pmax) return true;
+    }
 }
 
 // Per image of the plan: what the sequential pass decides (table set, quant slots, bases).

@@ -143,14 +143,31 @@ class Pool {
 
 }  // namespace
 
-// One launched batch whose results are not collected yet (jd_decode_batch_async keeps two in
-// flight: the host plans batch k+1 while the GPU decodes batch k).  Each slot owns its device
-// scratch and, unless the caller names a stream, its own stream, so batch k+1's first kernels
-// run beside batch k's latency-bound tail (re-walks, chain, DC scan).
+// One of the context's two device-scratch slots.  Each owns the device scratch of the batch it
+// runs and, unless the caller names a stream, its own stream, so one batch's first kernels run
+// beside the other slot's latency-bound tail (re-walks, chain, DC scan) and big kernels.  A slot is
+// reused by every second launch; the work of consecutive launches on one slot is ordered by its
+// stream, so batch k+2 can be planned and enqueued while batch k still runs.
+struct Slot {
+    hipStream_t stream = nullptr;                // this slot's internal stream
+    DevBuf d_plan, d_brk, d_blocks, d_entries, d_comp, d_planes, d_stamps;  // device scratch of the batch
+    void* plan_host = nullptr;                   // pinned staging of the slot's plan blob
+    size_t plan_cap = 0;
+    void* in_host = nullptr;                     // pinned staging of the slot's host-memory JPEG inputs
+    size_t in_cap = 0;
+    DevBuf d_input;                              // device copy of those inputs
+    hipEvent_t h2d_done = nullptr;               // after the slot's latest host-input copies
+    hipEvent_t plan_done = nullptr;              // after the slot's latest plan upload
+    bool h2d_recorded = false, plan_recorded = false;
+};
+
+// One launched batch whose results are not collected yet.  jd_decode_batch_async keeps up to
+// kAsyncDepth of them in flight: the host parses, plans and enqueues batch k+2 on its slot's stream
+// (behind batch k) before it waits for batch k, so batch k+2's front-end starts the moment batch k
+// ends instead of a host plan later.
 struct Pending {
     bool active = false;
-    hipStream_t stream = nullptr;               // this slot's internal stream
-    DevBuf d_plan, d_brk, d_blocks, d_entries, d_comp, d_planes, d_stamps;  // device scratch of the batch
+    uint64_t seq = 0;                           // launch order
     jd_result* results = nullptr;
     int lo = 0, hi = 0;
     std::vector<jd_status> pst;                 // per item lo..hi: host-side status
@@ -158,20 +175,15 @@ struct Pending {
     std::vector<int> item_of_img;
     std::vector<std::array<uint64_t, 3>> host_copies;  // {host dst, device src, bytes} (host output)
     uint32_t nimg = 0;
-    void* host = nullptr;                       // pinned: u64 counters[2], then u32 status[nimg]
+    void* host = nullptr;                       // pinned: u64 counters[4], then u32 status[nimg]
     size_t host_cap = 0;
-    void* plan_host = nullptr;                  // pinned staging of this slot's plan blob
-    size_t plan_cap = 0;
-    void* in_host = nullptr;                    // pinned staging of this slot's host-memory JPEG inputs
-    size_t in_cap = 0;
-    DevBuf d_input;                             // device copy of those inputs
     hipEvent_t done = nullptr;
-    hipEvent_t h2d_done = nullptr;              // after this slot's host-input copies (h2d_after)
     hipEvent_t ev[JD_NUM_KERNELS][2] = {};
     bool timing = false, fancy = false;
     double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0, piece_overlap = 0;
     double t_plan = 0, t_upload = 0;
 };
+constexpr int kNumPending = 4;  // records (>= the async depth + 2: a record is reused 4 launches later)
 
 struct jd_ctx {
     int device = 0;
@@ -193,8 +205,11 @@ struct jd_ctx {
     // staged per slot (Pending::in_host / d_input), so host-input batches pipeline too
     DevBuf output;
 
-    Pending pend[2];
-    int slot = 0;  // the slot the next launch uses
+    Slot slots[2];
+    Pending pend[kNumPending];
+    int slot = 0;                        // the slot the next launch uses
+    uint64_t seq = 0;                    // launches so far (the next launch's record: pend[seq % kNumPending])
+    int async_depth = 2;                 // batches jd_decode_batch_async leaves in flight (JD_ASYNC_DEPTH: 1 or 2)
     const void* last_stream = nullptr;  // caller stream of the pending launches (nullptr: the slots' own)
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     int max_batch_images = 0;           // items per launched sub-batch (JD_MAX_BATCH_IMAGES)
@@ -395,7 +410,8 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
                               : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u
                               : (ctx->flags & JD_FLAG_FULL_PIECES) ? kPieceBits
                                                                    : adaptive_piece_bits(ecs_img * 8);
-        if (!image_fits(ecs_img, h, pmin, ctx->spare_pieces, region_divisor(pj))) {
+        const bool forced = (ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES | JD_FLAG_FULL_PIECES)) != 0;
+        if (!image_fits(ecs_img, h, pmin, forced ? pmin : kPieceBits, ctx->spare_pieces, region_divisor(pj))) {
             ctx->pst[it] = JD_ERR_CAPACITY;
             continue;
         }
@@ -552,7 +568,9 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             d.sub_base = uint32_t(sub);
             d.sub_cap = uint32_t(piece_slots(d.len - d.ecs_off, d.nseg, P.piece_bits));
             d.entry_base = entry_cursor;
-            d.entry_cap = uint32_t(entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces, d.rw_div));
+            const uint64_t words = entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces, d.rw_div);
+            if (words > kMaxImageEntryWords) return JD_ERR_CAPACITY;  // image_fits checked every piece size
+            d.entry_cap = uint32_t(words);
             entry_cursor += align_up(size_t(d.entry_cap), kRegionAlign);
             sub += d.sub_cap;
             for (uint32_t k = 0; k < d.nseg; k++) P.chain_seg.push_back(d.seg_base + k);
@@ -619,11 +637,14 @@ bool host_registered(const jd_ctx* ctx, const uint8_t* p, size_t n) {
 
 jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_result* results, int rgb_on_device,
                        hipStream_t s) {
-    Pending& pd = ctx->pend[ctx->slot];
-    if (pd.active) {
+    Slot& sl = ctx->slots[ctx->slot];
+    Pending& pd = ctx->pend[ctx->seq % kNumPending];
+    if (pd.active) {  // (the async depth keeps fewer batches in flight: normally collected already)
         const jd_status fst = finish_batch(ctx, pd);
         if (fst != JD_OK) return fst;
     }
+    // The slot's previous batch (launched two calls ago) may still run: its device scratch is
+    // reused in stream order; its pinned staging only once its copies are done (below).
     // An error return after the host inputs' H2D copies were queued (plan capacity, a HIP failure)
     // leaves the slot inactive, so nothing else would wait for them: wait here, before the staging
     // buffers can be refilled or freed by a later call.
@@ -650,10 +671,15 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     size_t in_bytes = 0, reg_bytes = 0, out_bytes = 0;
     if (!reg_items.empty()) {
         std::sort(reg_items.begin(), reg_items.end(), [&](int a, int b) { return items[a].jpeg < items[b].jpeg; });
-        constexpr uintptr_t kSpanGap = uintptr_t(1) << 20;  // a gap up to this is copied along
+        // A gap between neighbouring files is copied along only while it is small against the span
+        // (at most 4 KiB, or an eighth of the span so far): sparse files in a large arena move their
+        // own bytes, not the arena's.
+        constexpr uintptr_t kSpanGap = uintptr_t(4) << 10;
         for (int i : reg_items) {
             const uintptr_t a = reinterpret_cast<uintptr_t>(items[i].jpeg), e = a + items[i].len;
-            if (spans.empty() || a > spans.back().hi + kSpanGap || reg_range(ctx, a) != reg_range(ctx, spans.back().lo))
+            const bool merge = !spans.empty() && reg_range(ctx, a) == reg_range(ctx, spans.back().lo) &&
+                               (a <= spans.back().hi + std::max(kSpanGap, (spans.back().hi - spans.back().lo) / 8));
+            if (!merge)
                 spans.push_back({a, e, 0});
             else
                 spans.back().hi = std::max(spans.back().hi, e);
@@ -668,11 +694,11 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         sp.off = in_bytes + reg_bytes;
         reg_bytes += align_up(size_t(sp.hi - sp.lo) + 64, 256);
     }
-    if (in_bytes + reg_bytes) HIPCHK(ctx, ensure_dev(ctx, pd.d_input, in_bytes + reg_bytes));
-    if (in_bytes + reg_bytes && ctx->h2d_serial && ctx->last_h2d && ctx->last_h2d != pd.h2d_done)
+    if (in_bytes + reg_bytes) HIPCHK(ctx, ensure_dev(ctx, sl.d_input, in_bytes + reg_bytes));
+    if (in_bytes + reg_bytes && ctx->h2d_serial && ctx->last_h2d && ctx->last_h2d != sl.h2d_done)
         HIPCHK(ctx, hipStreamWaitEvent(s, ctx->last_h2d, 0));
     if (reg_bytes) {
-        uint8_t* const dbase = static_cast<uint8_t*>(pd.d_input.p);
+        uint8_t* const dbase = static_cast<uint8_t*>(sl.d_input.p);
         for (const Span& sp : spans)  // (in JD_STAGE_CHUNK_MB pieces, as the staged copies)
             for (uintptr_t c = sp.lo; c < sp.hi; c += std::min<uintptr_t>(ctx->stage_chunk, sp.hi - c)) {
                 staging.s = s;
@@ -685,8 +711,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             while (a >= spans[k].hi) k++;
             dev_addr[i] = reinterpret_cast<uint64_t>(dbase) + spans[k].off + (a - spans[k].lo);
         }
-        ctx->stats.h2d_bytes += double(reg_bytes);
-        ctx->stats.h2d_registered_bytes += double(reg_bytes);
+        ctx->stats.h2d_bytes += double(reg_bytes);  // what moves (spans, gaps included)
+        for (int i : reg_items) ctx->stats.h2d_registered_bytes += double(items[i].len);  // the files' own bytes
     }
     if (in_bytes) {
         // Host-memory inputs: copied into this slot's pinned staging by the host workers in
@@ -696,7 +722,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         // here (collected above).
         Range r("jd_stage_inputs");
         const auto ts0 = std::chrono::steady_clock::now();
-        HIPCHK(ctx, ensure_pinned(pd.in_host, pd.in_cap, in_bytes));
+        if (sl.h2d_recorded) HIPCHK(ctx, hipEventSynchronize(sl.h2d_done));  // the slot's last DMA read it
+        HIPCHK(ctx, ensure_pinned(sl.in_host, sl.in_cap, in_bytes));
         struct Piece { const uint8_t* src; size_t off, n; };
         std::vector<Piece> pieces;
         constexpr size_t kStagePiece = size_t(1) << 20;
@@ -705,11 +732,11 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             if (ctx->pst[i] != JD_OK || items[i].jpeg_dev || registered[size_t(i)]) continue;
             for (size_t k = 0; k < items[i].len; k += kStagePiece)
                 pieces.push_back({items[i].jpeg + k, off + k, std::min(kStagePiece, items[i].len - k)});
-            dev_addr[i] = reinterpret_cast<uint64_t>(pd.d_input.p) + off;
+            dev_addr[i] = reinterpret_cast<uint64_t>(sl.d_input.p) + off;
             off += align_up(items[i].len + 64, 256);
         }
-        uint8_t* const stage = static_cast<uint8_t*>(pd.in_host);
-        uint8_t* const dstage = static_cast<uint8_t*>(pd.d_input.p);
+        uint8_t* const stage = static_cast<uint8_t*>(sl.in_host);
+        uint8_t* const dstage = static_cast<uint8_t*>(sl.d_input.p);
         const size_t kStageChunk = ctx->stage_chunk;  // H2D granularity (JD_STAGE_CHUNK_MB)
         for (size_t p0 = 0; p0 < pieces.size();) {
             size_t p1 = p0 + 1;
@@ -727,9 +754,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         ctx->stats.host_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
         ctx->stats.h2d_bytes += double(in_bytes);
     }
-    if (in_bytes + reg_bytes && ctx->h2d_serial) {
-        HIPCHK(ctx, hipEventRecord(pd.h2d_done, s));
-        ctx->last_h2d = pd.h2d_done;
+    if (in_bytes + reg_bytes) {
+        HIPCHK(ctx, hipEventRecord(sl.h2d_done, s));
+        sl.h2d_recorded = true;
+        if (ctx->h2d_serial) ctx->last_h2d = sl.h2d_done;
     }
     for (int i = lo; i < hi; i++)
         if (ctx->pst[i] == JD_OK && items[i].jpeg_dev) dev_addr[i] = reinterpret_cast<uint64_t>(items[i].jpeg_dev);
@@ -759,8 +787,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     if (st != JD_OK) return st;
     const uint32_t nimg = uint32_t(P.imgs.size());
     if (nimg) {
-        HIPCHK(ctx, ensure_dev(ctx, pd.d_comp, std::max<size_t>(16, P.comp_bytes)));
-        for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(pd.d_comp.p);
+        HIPCHK(ctx, ensure_dev(ctx, sl.d_comp, std::max<size_t>(16, P.comp_bytes)));
+        for (ImgDesc& d : P.imgs) d.comp += reinterpret_cast<uint64_t>(sl.d_comp.p);
         const bool fancy = (ctx->flags & JD_FLAG_FANCY_UPSAMPLING) != 0;
         uint32_t max_fancy_wgs = 0;
         if (fancy) {  // int16 component planes over the padded MCU grid, 256-B aligned per image
@@ -777,9 +805,9 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
                 max_fancy_wgs = std::max<uint32_t>(max_fancy_wgs & 0xFFFFu, (d.width + kFancyW - 1) / kFancyW) |
                                 (std::max<uint32_t>(max_fancy_wgs >> 16, (d.height + kFancyRowsPerWg - 1) / kFancyRowsPerWg) << 16);
             }
-            HIPCHK(ctx, ensure_dev(ctx, pd.d_planes, std::max<size_t>(16, tot)));
+            HIPCHK(ctx, ensure_dev(ctx, sl.d_planes, std::max<size_t>(16, tot)));
             for (size_t i = 0; i < P.imgs.size(); i++)
-                P.imgs[i].planes = reinterpret_cast<uint64_t>(pd.d_planes.p) + poff[i];
+                P.imgs[i].planes = reinterpret_cast<uint64_t>(sl.d_planes.p) + poff[i];
         }
         std::vector<uint8_t> blob;
         const size_t nseg = P.seg_img.size();
@@ -822,15 +850,18 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_fix = reserve(end, nseg * 4);
         const size_t o_tdc = reserve(end, size_t(P.total_tiles) * sizeof(DcPred));
         const size_t o_slow = reserve(end, size_t(P.total_tiles) * 8);
-        HIPCHK(ctx, ensure_dev(ctx, pd.d_plan, end));
-        HIPCHK(ctx, ensure_pinned(pd.plan_host, pd.plan_cap, upload));
-        memcpy(pd.plan_host, blob.data(), upload);
-        HIPCHK(ctx, hipMemcpyAsync(pd.d_plan.p, pd.plan_host, upload, hipMemcpyHostToDevice, s));
-        HIPCHK(ctx, ensure_dev(ctx, pd.d_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
-        HIPCHK(ctx, ensure_dev(ctx, pd.d_blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
-        HIPCHK(ctx, ensure_dev(ctx, pd.d_entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
+        HIPCHK(ctx, ensure_dev(ctx, sl.d_plan, end));
+        if (sl.plan_recorded) HIPCHK(ctx, hipEventSynchronize(sl.plan_done));  // the slot's last plan upload
+        HIPCHK(ctx, ensure_pinned(sl.plan_host, sl.plan_cap, upload));
+        memcpy(sl.plan_host, blob.data(), upload);
+        HIPCHK(ctx, hipMemcpyAsync(sl.d_plan.p, sl.plan_host, upload, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipEventRecord(sl.plan_done, s));
+        sl.plan_recorded = true;
+        HIPCHK(ctx, ensure_dev(ctx, sl.d_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
+        HIPCHK(ctx, ensure_dev(ctx, sl.d_blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
+        HIPCHK(ctx, ensure_dev(ctx, sl.d_entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
 
-        uint8_t* base = static_cast<uint8_t*>(pd.d_plan.p);
+        uint8_t* base = static_cast<uint8_t*>(sl.d_plan.p);
         BatchDev b;
         memset(&b, 0, sizeof(b));
         b.imgs = reinterpret_cast<const ImgDesc*>(base + o_imgs);
@@ -882,10 +913,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.chunk_nbrk = reinterpret_cast<uint32_t*>(base + o_nbrk);
         b.chunk_drops = reinterpret_cast<uint32_t*>(base + o_drops);
         b.chunk_coff = reinterpret_cast<uint32_t*>(base + o_coff);
-        b.chunk_brk = static_cast<Break*>(pd.d_brk.p);
-        b.blocks = static_cast<BlockInfo*>(pd.d_blocks.p);
-        b.entries = static_cast<uint32_t*>(pd.d_entries.p);
-        b.entries_cap = (pd.d_entries.cap - 64) / 4;  // last 64 B: padding for 16-byte over-reads
+        b.chunk_brk = static_cast<Break*>(sl.d_brk.p);
+        b.blocks = static_cast<BlockInfo*>(sl.d_blocks.p);
+        b.entries = static_cast<uint32_t*>(sl.d_entries.p);
+        b.entries_cap = (sl.d_entries.cap - 64) / 4;  // last 64 B: padding for 16-byte over-reads
         b.status = reinterpret_cast<uint32_t*>(base + o_status);
         b.counters = reinterpret_cast<unsigned long long*>(base + o_ctr);
         b.max_tiles = P.max_tiles;
@@ -896,9 +927,9 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             b.mode_max_tiles[m] = P.mode_max_tiles[m];
         }
         if (std::getenv("JD_STAMPS")) {  // diagnostic builds (JD_STAMP): per-tile phase stamps
-            HIPCHK(ctx, ensure_dev(ctx, pd.d_stamps, size_t(P.total_tiles) * 64));
-            HIPCHK(ctx, hipMemsetAsync(pd.d_stamps.p, 0, size_t(P.total_tiles) * 64, s));
-            b.stamps = static_cast<unsigned long long*>(pd.d_stamps.p);
+            HIPCHK(ctx, ensure_dev(ctx, sl.d_stamps, size_t(P.total_tiles) * 64));
+            HIPCHK(ctx, hipMemsetAsync(sl.d_stamps.p, 0, size_t(P.total_tiles) * 64, s));
+            b.stamps = static_cast<unsigned long long*>(sl.d_stamps.p);
         }
         b.fancy = fancy ? 1u : 0u;
         b.max_fancy_wgs = max_fancy_wgs;
@@ -963,6 +994,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     }
     HIPCHK(ctx, hipEventRecord(pd.done, s));
     pd.active = true;
+    pd.seq = ctx->seq++;
     staging.s = nullptr;  // the slot's done event now covers the copies
     ctx->slot ^= 1;
     return JD_OK;
@@ -1045,14 +1077,24 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
     return JD_OK;
 }
 
-// Collects every launched batch, oldest first.
-jd_status finish_all(jd_ctx* ctx) {
-    for (int k = 0; k < 2; k++) {
-        const jd_status st = finish_batch(ctx, ctx->pend[(ctx->slot + k) & 1]);
+// Collects launched batches, oldest first, until at most `keep` are left in flight.
+jd_status collect_until(jd_ctx* ctx, int keep) {
+    while (true) {
+        Pending* oldest = nullptr;
+        int active = 0;
+        for (Pending& pd : ctx->pend)
+            if (pd.active) {
+                active++;
+                if (!oldest || pd.seq < oldest->seq) oldest = &pd;
+            }
+        if (active <= keep) return JD_OK;
+        const jd_status st = finish_batch(ctx, *oldest);
         if (st != JD_OK) return st;
     }
-    return JD_OK;
 }
+
+// Collects every launched batch, oldest first.
+jd_status finish_all(jd_ctx* ctx) { return collect_until(ctx, 0); }
 
 }  // namespace
 
@@ -1116,6 +1158,7 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
     if (const char* e = std::getenv("JD_STAGE_NT")) ctx->stage_nt = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_H2D_SERIAL")) ctx->h2d_serial = std::strtoll(e, nullptr, 0) != 0;
+    if (const char* e = std::getenv("JD_ASYNC_DEPTH")) ctx->async_depth = std::strtoll(e, nullptr, 0) == 1 ? 1 : 2;
     if (const char* e = std::getenv("JD_STAGE_CHUNK_MB")) {
         const long long mb = std::strtoll(e, nullptr, 0);
         ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);
@@ -1124,10 +1167,17 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
         delete ctx;
         return JD_ERR_HIP;
     }
+    for (Slot& sl : ctx->slots) {
+        bool ok = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&sl.h2d_done, hipEventDisableTiming) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&sl.plan_done, hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            jd_ctx_destroy(ctx);
+            return JD_ERR_HIP;
+        }
+    }
     for (Pending& pd : ctx->pend) {
-        bool ok = hipStreamCreateWithFlags(&pd.stream, hipStreamNonBlocking) == hipSuccess;
-        ok = ok && hipEventCreateWithFlags(&pd.done, hipEventDisableTiming) == hipSuccess;
-        ok = ok && hipEventCreateWithFlags(&pd.h2d_done, hipEventDisableTiming) == hipSuccess;
+        bool ok = hipEventCreateWithFlags(&pd.done, hipEventDisableTiming) == hipSuccess;
         for (int k = 0; k < JD_NUM_KERNELS; k++)
             for (int j = 0; j < 2; j++) ok = ok && hipEventCreate(&pd.ev[k][j]) == hipSuccess;
         if (!ok) {
@@ -1145,16 +1195,19 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
     (void)quiesce(ctx);
     for (DevBuf* b : {&ctx->lut_dev, &ctx->output})
         if (b->p) (void)hipFree(b->p);
-    for (Pending& pd : ctx->pend) {
-        for (DevBuf* b : {&pd.d_plan, &pd.d_brk, &pd.d_blocks, &pd.d_entries, &pd.d_comp, &pd.d_planes, &pd.d_stamps,
-                          &pd.d_input})
+    for (Slot& sl : ctx->slots) {
+        for (DevBuf* b : {&sl.d_plan, &sl.d_brk, &sl.d_blocks, &sl.d_entries, &sl.d_comp, &sl.d_planes, &sl.d_stamps,
+                          &sl.d_input})
             if (b->p) (void)hipFree(b->p);
-        if (pd.in_host) (void)hipHostFree(pd.in_host);
-        if (pd.stream) (void)hipStreamDestroy(pd.stream);
+        if (sl.in_host) (void)hipHostFree(sl.in_host);
+        if (sl.plan_host) (void)hipHostFree(sl.plan_host);
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        if (sl.h2d_done) (void)hipEventDestroy(sl.h2d_done);
+        if (sl.plan_done) (void)hipEventDestroy(sl.plan_done);
+    }
+    for (Pending& pd : ctx->pend) {
         if (pd.host) (void)hipHostFree(pd.host);
-        if (pd.plan_host) (void)hipHostFree(pd.plan_host);
         if (pd.done) (void)hipEventDestroy(pd.done);
-        if (pd.h2d_done) (void)hipEventDestroy(pd.h2d_done);
         for (int k = 0; k < JD_NUM_KERNELS; k++)
             for (int j = 0; j < 2; j++)
                 if (pd.ev[k][j]) (void)hipEventDestroy(pd.ev[k][j]);
@@ -1259,14 +1312,14 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
     if (ctx->host_timing) std::fprintf(stderr, "host parse %.3f ms\n", t_parse);
     for (int lo = 0; lo < n;) {
         const int hi = batch_split(ctx, lo, n, items);
-        hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->pend[ctx->slot].stream;
+        hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->slots[ctx->slot].stream;
         jd_status st = launch_batch(ctx, items, lo, hi, results, rgb_on_device, s);
         if (st != JD_OK) return st;
-        if (async) {  // collect the previous launch (its slot is the current one now)
-            st = finish_batch(ctx, ctx->pend[ctx->slot]);
-        } else {  // collect this sub-batch before the next one reuses the staging and output pools
-            st = finish_batch(ctx, ctx->pend[ctx->slot ^ 1]);
-        }
+        // async: the newest async_depth launches stay in flight (with 2, this launch was enqueued
+        // behind the batch two launches back on its slot's stream before that batch is waited
+        // for); otherwise collect this sub-batch before the next one reuses the staging and
+        // output pools
+        st = collect_until(ctx, async ? ctx->async_depth : 0);
         if (st != JD_OK) return st;
         lo = hi;
     }

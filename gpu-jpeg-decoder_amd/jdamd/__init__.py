@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -90,6 +91,12 @@ EXPORTED_SYMBOLS = [
 _lib = None
 
 
+def _abi_mismatch_allowed() -> bool:
+    """JDAMD_ALLOW_ABI_MISMATCH=1 (set by tools/ab.sh and tools/trace.sh for experiment builds
+    from older trees): skip the ABI-version check and tolerate missing entry points."""
+    return os.environ.get("JDAMD_ALLOW_ABI_MISMATCH") == "1"
+
+
 def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     """Load libjdamd.so (in-tree build).  Raises if it is absent: there is no fallback."""
     global _lib
@@ -136,7 +143,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         "jd_host_alloc": (c_int, [c_void_p, c_size_t, ctypes.POINTER(c_void_p)]),
         "jd_host_free": (c_int, [c_void_p, c_void_p]),
     }
-    experiment = p != LIB_PATH  # an A/B build from an older tree may lack newer entry points
+    # an A/B build from an older tree may lack newer entry points: tolerated only on explicit opt-in
+    experiment = p != LIB_PATH and _abi_mismatch_allowed()
     for name, (res, args) in sig.items():
         if experiment and not hasattr(lib, name):
             continue
@@ -249,8 +257,12 @@ class Decoder:
         """fancy=True: libjpeg's triangular chroma upsampling instead of replication
         (JD_FLAG_FANCY_UPSAMPLING; an option beyond the reference, see include/jd.h)."""
         self.lib = load_library()
-        if self.lib.jd_abi_version() != JD_ABI_VERSION and not os.environ.get("JDAMD_LIB"):  # (A/B builds may be older)
-            raise JDError(JD_ERR_INVALID_ARG, f"libjdamd ABI {self.lib.jd_abi_version()} != {JD_ABI_VERSION}: rebuild")
+        abi = self.lib.jd_abi_version()
+        if abi != JD_ABI_VERSION:
+            if not _abi_mismatch_allowed():
+                raise JDError(JD_ERR_INVALID_ARG, f"libjdamd ABI {abi} != {JD_ABI_VERSION}: rebuild")
+            warnings.warn(f"libjdamd ABI {abi} != {JD_ABI_VERSION}: loaded anyway (JDAMD_ALLOW_ABI_MISMATCH=1)")
+        self._arenas = {}  # pointer -> registered numpy arena (kept alive while registered)
         self.ctx = ctypes.c_void_p()
         opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path] | (JD_FLAG_FANCY_UPSAMPLING if fancy else 0),
                      parse_threads)
@@ -260,8 +272,9 @@ class Decoder:
 
     def close(self) -> None:
         if self.ctx:
-            self.lib.jd_ctx_destroy(self.ctx)
+            self.lib.jd_ctx_destroy(self.ctx)  # unregisters the arenas still registered
             self.ctx = ctypes.c_void_p()
+        self._arenas = {}
 
     def __enter__(self):
         return self
@@ -364,16 +377,21 @@ class Decoder:
     def register_host(self, arena: np.ndarray) -> None:
         """jd_host_register: page-lock a caller-owned input arena (a contiguous numpy array) so that
         batch items whose bytes lie in it are uploaded straight from it (no staging copy).  The
-        arena must stay alive and unchanged while batches reading it are in flight."""
+        arena must stay unchanged while batches reading it are in flight; the Decoder keeps a
+        reference to it until unregister_host() or close(), so it cannot be freed while registered."""
+        if not isinstance(arena, np.ndarray) or not arena.flags["C_CONTIGUOUS"]:
+            raise JDError(JD_ERR_INVALID_ARG, "jd_host_register: the arena must be a C-contiguous numpy array")
         st = self.lib.jd_host_register(self.ctx, arena.ctypes.data, arena.nbytes)
         if st != JD_OK:
             raise JDError(st, "jd_host_register " + (self.last_error() if st == JD_ERR_HIP else ""))
+        self._arenas[arena.ctypes.data] = arena
 
     def unregister_host(self, arena: np.ndarray) -> None:
         """jd_host_unregister (waits for the context's in-flight batches first)."""
         st = self.lib.jd_host_unregister(self.ctx, arena.ctypes.data)
         if st != JD_OK:
             raise JDError(st, "jd_host_unregister " + (self.last_error() if st == JD_ERR_HIP else ""))
+        self._arenas.pop(arena.ctypes.data, None)
 
     def host_alloc(self, nbytes: int) -> np.ndarray:
         """jd_host_alloc: a pinned input arena (hipHostMalloc) owned by the context, as a numpy

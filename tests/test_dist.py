@@ -48,10 +48,23 @@ def _worker(rank, world, port, batch, q):
     # the bench's real per-rank vector: rank 1 is host-bound (slow parse + plan, slow e2e leg)
     host = {"parse": 0.5 + 2.0 * rank, "plan": 0.25 + rank, "stage_inputs": 1.0, "wait": 0.1}
     vec = bench.rank_vector(2.0 + rank, 64 * 48, batch, 1000.0, 1500.0, 10, host, 20.0 + 5 * rank, 50.0 - rank,
-                            12.0 + rank)
+                            12.0 + rank, 11.5 + rank)
     full = bench.gather_matrix(torch.tensor(vec, dtype=torch.float64), world)
     table = bench.per_rank_table(full, 10)
-    q.put((rank, d, threads, info, seeds_c2, seeds_c5, digests, t_max, sums, mat.tolist(), table, full.tolist()))
+    # rank 0's single-host measurements after the gather, the other rank waiting at the barrier
+    # (an N > 1 line carries the CPU baseline and the copy peak)
+    calls = []
+    extra = bench.rank0_measurements(d["rank"], d["world"], copy_fn=lambda: calls.append("copy") or 5650.0,
+                                     cpu_fn=lambda: calls.append("cpu") or {"value": 1750.0, "cores": 16})
+    kern = {"k_piece": {"launches": 3, "total_ms": 8.4, "bytes": 3 * 2.3e9},
+            "k_idct_color": {"launches": 3, "total_ms": 8.45, "bytes": 3 * 8.1e9},
+            "k_scan": {"launches": 3, "total_ms": 0.6, "bytes": 3 * 0.65e9}}
+    roof = bench.roofline_block(kern, "c2", extra["copy_peak"], 3) if d["rank"] == 0 else None
+    # within 1 % by hipEvents: the committed rocprof averages decide
+    roof_rp = bench.roofline_block(kern, "c2", extra["copy_peak"], 3, {"k_piece": 2.95, "k_idct_color": 2.90})
+    line = {"cpu_baseline": extra["cpu_baseline"], "roofline": roof} if d["rank"] == 0 else None
+    q.put((rank, d, threads, info, seeds_c2, seeds_c5, digests, t_max, sums, mat.tolist(), table, full.tolist(),
+           calls, line, roof_rp["kernel"]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,7 +82,7 @@ def test_bench_rank_setup_sharding_and_counter_gather_gloo():
         p.join(60)
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
-    for rank, d, threads, info, _, _, _, t_max, sums, mat, table, full in out:
+    for rank, d, threads, info, _, _, _, t_max, sums, mat, table, full, calls, line, picked in out:
         assert d["world_seen"] == world and d["rank"] == rank and d["backend"] == "gloo"
         assert d["device_index"] == rank  # one device per local rank (no GPU here: index only)
         assert 1 <= threads <= bench_share() and info["rank_cpus"] >= 1
@@ -84,7 +97,17 @@ def test_bench_rank_setup_sharding_and_counter_gather_gloo():
         assert table["parse_ms"] == [0.5, 2.5] and table["plan_ms"] == [0.25, 1.25]
         assert table["stage_ms"] == [1.0, 1.0] and table["wait_ms"] == [0.1, 0.1]
         assert table["e2e_ms"] == [20.0, 25.0] and table["h2d_GB_s"] == [50.0, 49.0]
-        assert table["e2e_registered_ms"] == [12.0, 13.0]
+        assert table["e2e_registered_ms"] == [12.0, 13.0]  # each H2D leg on its own, no best-of
+        assert table["e2e_pinned_arena_ms"] == [11.5, 12.5]
+        if rank == 0:  # the 2-rank line carries the CPU baseline and the in-run copy peak
+            assert calls == ["copy", "cpu"]
+            assert line["cpu_baseline"]["value"] == 1750.0
+            assert line["roofline"]["measured_copy_peak"] == 5650.0
+            assert line["roofline"]["kernel"] == "k_idct_color" and line["roofline"]["co_dominant"]["kernel"] == "k_piece"
+            assert line["roofline"]["frac_of_measured_peak"] > 0
+        else:
+            assert calls == [] and line is None
+        assert picked == "k_piece"
         assert table["host_parse_plan_over_step"] == [round(0.75 / 200.0, 4), round(3.75 / 300.0, 4)]
         assert max(r[0] for r in full) == 3.0 and sum(r[1] for r in full) == 2 * 64 * 48 * 10
     d0, d1 = set(out[0][6]), set(out[1][6])

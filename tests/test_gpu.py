@@ -125,6 +125,34 @@ def test_full_size_vs_oracle(decoder, w, h, ss, rows, blocks, q):
     assert np.array_equal(out, ref)
 
 
+def test_c1_exact_image_vs_oracle(decoder):
+    """BASELINE config 1 exactly as bench.py --config c1 builds it: 512 x 512 4:4:4 q90, no DRI,
+    seed 0."""
+    import bench
+
+    W, H, ss, rows, _, _ = bench.CONFIGS["c1"]
+    (job,) = jd_synth.make_jobs([0], W, H, 90, ss, rows, 0)
+    (data,) = jd_synth.make_images([job], workers=1)
+    assert data == jd_synth.encode(jd_synth.synth_pixels(512, 512, 0), 90, "4:4:4")
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    assert np.array_equal(decoder.decode(data), ref)
+
+
+@pytest.mark.parametrize("size", [200, 1000, 2000])
+def test_ref444_sizes_vs_oracle(decoder, size):
+    """The reference's own benchmark format (4:4:4 q95, data_preprocessing/image_converter.py:6,18)
+    at its latency-benchmark sizes (cuda-decoder/benchmark/benchmark.cu:87), as bench.py
+    --config ref444 builds them."""
+    import bench
+
+    (data,) = jd_synth.make_images(bench.ref444_jobs([bench.REF_SIZES.index(size)], 95), workers=1)
+    assert jdamd.parse(data).width == size
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    assert np.array_equal(decoder.decode(data), ref)
+
+
 def test_rst_invariance_full_size(decoder):
     px = jd_synth.synth_pixels(1920, 1080, 7)
     a = decoder.decode(jd_synth.encode(px, 90, "4:2:0"))

@@ -35,7 +35,7 @@ static int plan_one(const uint8_t* buf, size_t len, const ParsedJpeg& pj, ImgDes
     delete lut;
     if (!ok) return JD_ERR_CORRUPT;
     const uint64_t ecs = len - h.ecs_offset;
-    if (!image_fits(ecs, h, adaptive_piece_bits(ecs * 8), -1, region_divisor(pj))) return JD_ERR_CAPACITY;
+    if (!image_fits(ecs, h, adaptive_piece_bits(ecs * 8), kPieceBits, -1, region_divisor(pj))) return JD_ERR_CAPACITY;
     PlanImg pi{};
     pi.nseg = image_segments(h);
     pi.nchunks = uint32_t((len - (h.ecs_offset & ~uint64_t(15)) + kScanChunk - 1) / kScanChunk);
