@@ -560,7 +560,7 @@ def cpu_baseline(hosts, hdrs, target_s: float = 5.0):
     return res
 
 
-def ref_sweep(dec, datas, hosts, hdrs, in_ptrs, rgb_bufs, out_offs, dev, reps: int = 5):
+def ref_sweep(dec, datas, hosts, hdrs, in_ptrs, rgb_bufs, out_offs, dev, reps: int = 5, part: str = "all"):
     """The reference's two published curves on its own format (ref444), GPU beside its CPU decoder:
       batch   throughput vs batch size B in REF_BATCHES (figures/batchsize.pdf; method
               cuda-decoder/benchmark_thoughput/benchmark.cu:43-106: batches decoded one after another,
@@ -587,7 +587,7 @@ def ref_sweep(dec, datas, hosts, hdrs, in_ptrs, rgb_bufs, out_offs, dev, reps: i
     def kernel_ms(st):
         return sum(v["total_ms"] for v in st["kernels"].values())
 
-    for B in REF_BATCHES:
+    for B in (REF_BATCHES if part in ("all", "batch") else ()):
         B = min(B, n)
         sets = [dec.make_batch(hosts[:B], in_ptrs[:B], [rb.data_ptr() + o for o in out_offs[:B]]) for rb in rgb_bufs]
         mb = sum(jbytes[:B]) / 1e6
@@ -621,9 +621,9 @@ def ref_sweep(dec, datas, hosts, hdrs, in_ptrs, rgb_bufs, out_offs, dev, reps: i
                              "batches_timed": r})
     per_size = 5  # images of each size (the reference: every file of its size folder)
     with tempfile.TemporaryDirectory() as td:
-        for si, size in enumerate(REF_SIZES):
+        for si, size in enumerate(REF_SIZES if part in ("all", "latency") else ()):
             idx = [i for i in range(n) if i % len(REF_SIZES) == si][:per_size]
-            walls, kerns, paths = [], [], []
+            walls, kerns, paths, per_k = [], [], [], {}
             for i in idx:
                 one = dec.make_batch([hosts[i]], [in_ptrs[i]], [rgb_bufs[0].data_ptr() + out_offs[i]])
                 dec.decode_prepared(one, pipelined=False)
@@ -633,7 +633,11 @@ def ref_sweep(dec, datas, hosts, hdrs, in_ptrs, rgb_bufs, out_offs, dev, reps: i
                     t = time.perf_counter()
                     dec.decode_prepared(one, pipelined=False)
                     ws.append(time.perf_counter() - t)
-                kerns.append(kernel_ms(dec.stats()) / 10)
+                stt = dec.stats()
+                kerns.append(kernel_ms(stt) / 10)
+                for kn, kv in stt["kernels"].items():
+                    if kv["launches"]:
+                        per_k[kn] = per_k.get(kn, 0.0) + kv["total_ms"] / kv["launches"] / len(idx)
                 walls.append(float(np.median(ws)) * 1e3)
                 path = os.path.join(td, f"{size}_{i}.jpeg")
                 with open(path, "wb") as f:
@@ -645,6 +649,7 @@ def ref_sweep(dec, datas, hosts, hdrs, in_ptrs, rgb_bufs, out_offs, dev, reps: i
                 ref = 1e3 / rr[0] if rr else None  # ms per image, 1 process
             out["latency"].append({"size": size, "images": len(idx), "gpu_wall_ms_median": float(np.median(walls)),
                                    "gpu_kernel_ms": float(np.median(kerns)), "ref_cpu_ms": ref,
+                                   "kernels_ms": {k: round(v, 4) for k, v in per_k.items()},
                                    "gpu_MPix_s": size * size / float(np.median(walls)) / 1e3,
                                    "ref_cpu_MPix_s": size * size / ref / 1e3 if ref else None})
     return out
@@ -659,7 +664,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override images per rank")
     ap.add_argument("--quality", type=int, default=0, help="JPEG quality (default: 90; ref444: 95)")
-    ap.add_argument("--sweep", action="store_true",
+    ap.add_argument("--sweep", nargs="?", const="all", default=None, choices=["all", "batch", "latency"],
                     help="ref444: print the reference's two published curves instead of the bench line: "
                          "throughput vs batch size (JPEG MB/s) and single-image latency per size, next to the "
                          "reference's own CPU decoder (oracle/_ref/ref_bench) on the same files")
@@ -765,7 +770,8 @@ def main():
     if args.sweep:
         if ss != "ref" or world > 1:
             raise SystemExit("--sweep: --config ref444 on one GPU")
-        res = ref_sweep(dec, datas, hosts, hdrs, [jpeg_dev.data_ptr() + o for o in in_offs], rgb_bufs, out_offs, dev)
+        res = ref_sweep(dec, datas, hosts, hdrs, [jpeg_dev.data_ptr() + o for o in in_offs], rgb_bufs, out_offs, dev,
+                        part=args.sweep)
         res.update({"metric": "ref444 sweep (throughput vs batch, latency vs size)", "verified_bit_exact": verified,
                     "cpu_model": cpu_model(), "gen_s": t_gen})
         print(json.dumps(res))

@@ -194,6 +194,9 @@ constexpr int kPieceThreads = JD_PIECE_THREADS;
 #define JD_SMALL_PIECE_LANES 16384
 #endif
 constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
+// k_chain leaves intervals of more pieces to k_chain_big (wave-parallel re-walk rounds and counts),
+// which the host launches instead of k_chain_fix when an image's ECS may hold that many pieces
+constexpr uint32_t kBigInterval = 4096;
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;
@@ -311,7 +314,8 @@ struct BatchDev {
     uint32_t* piece_join;         // checkpoints recorded << 16 | (segment B = own region from
                                   // checkpoint join - 1; 0 = none)
     uint32_t* piece_mcu0;         // chain: first MCU of the piece within its segment
-    uint32_t* seg_fix;            // k_chain: 1 = the interval needs k_chain_fix's serial walk
+    uint32_t* seg_fix;            // k_chain: 1 = the interval needs k_chain_fix / k_chain_big
+    uint32_t big_chain;           // an interval may have more than kBigInterval pieces: k_chain_big
     CpRec* piece_cp;              // kCpRecords per piece slot (CpRec)
     const uint32_t* chain_seg;    // k_chain_fix: segment of each lane, grouped by table set
     uint32_t nchain;              // multiple of kPieceThreads

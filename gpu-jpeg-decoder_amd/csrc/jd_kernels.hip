@@ -1615,6 +1615,8 @@ __device__ __forceinline__ void chain_interval(const BatchDev& b, uint32_t s, ui
     if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
 }
 
+// Intervals of more than kBigInterval pieces are left to k_chain_big (launched instead of
+// k_chain_fix when the host sees that an interval may have that many: BatchDev::big_chain).
 __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     JD_PRIO_CRIT();
     const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1625,44 +1627,44 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const bool final_seg = seg_is_final(b, s);
+    if (n > kBigInterval) {  // (one interval without DRI: a big image in short pieces) -> k_chain_big
+        if (lane == 0) b.seg_fix[s] = 1u;
+        return;
+    }
     if (n > 64)
         chain_interval<4>(b, s, lane, S, base, n, nmcu_seg, final_seg);
     else
         chain_interval<1>(b, s, lane, S, base, n, nmcu_seg, final_seg);
 }
 
-// One lane per interval flagged by k_chain (workgroups grouped by table set): walk its pieces in
-// order, re-walk every piece whose start disagrees with its predecessor's end (the workgroup
-// stages its tables only when some lane needs them), and take the counts serially.
-// 64-lane workgroups with the tables in global memory, as k_redo: almost every workgroup exits at
-// once, and with the 73 KB of LDS a piece workgroup takes, each of them had to wait for a CU's
-// LDS under the other batch's k_idct_color (1.1 ms instead of 0.02 in a kernel trace).
-__global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
-    JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
-    const uint32_t li = blockIdx.x * kRedoThreads + threadIdx.x;
-    uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
-    if (s != kInvalidImage && !b.seg_fix[s]) s = kInvalidImage;
-    const bool need = s != kInvalidImage;
-    if (!__syncthreads_or(need)) return;  // workgroup-uniform: the common case
-    const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
-    SegInfo S;
-    uint32_t base = 0, n = 0;
-    if (need) {
-        seg_info(b, s, S);
-        base = b.seg_sub_base[s];
-        n = b.seg_nsub[s];
-    } else {
-        seg_invalid(b, S);
-    }
-    if (!need) return;
-    const uint32_t* const luts = reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0);
-    uint32_t dcp, acp;
-    table_slots(ts, S, dcp, acp);
-    uint32_t* const row = s_rows + threadIdx.x * row_words(kWin);
-    uint32_t* const ring = s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords;
-    uint32_t* const rring = s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords;
+// The intervals k_chain flagged: a start still disagreeing after k_redo (a double failure, rare),
+// or (k_chain_big) an interval of more than kBigInterval pieces.
+//  * k_chain_fix: one lane per interval (64-lane workgroups grouped by table set) walks its pieces
+//    in order, re-walking every disagreeing one (chain_fix_serial).  64-lane workgroups with the
+//    tables in global memory, as k_redo: almost every workgroup exits at once, and with the 73 KB
+//    of LDS a piece workgroup takes, each of them had to wait for a CU's LDS under the other
+//    batch's k_idct_color (1.1 ms instead of 0.02 in a kernel trace).
+//  * k_chain_big: one wave per flagged interval, for batches whose intervals may have thousands of
+//    pieces (an image without DRI in a small batch, in short pieces: one 2000 x 2000 4:4:4 q95
+//    image has 45 K pieces of 512 bits, and the serial walk took 0.3 us per piece, 13 ms).  A
+//    64-lane workgroup covers 64 entries of the chain list and takes its flagged intervals one after
+//    the other:
+//      - rounds: every piece whose start disagrees with its predecessor's end is re-walked from that
+//        end, all of them at once (a round re-walks from the previous round's ends).  A piece whose
+//        predecessors all agree starts at the truth, so each round settles at least the first
+//        disagreement and a run of r consecutive failures takes r rounds;
+//      - then the counts by prefix sums, wave-parallel (chain_interval);
+//      - after kFixRounds rounds without agreement (never seen), the serial walk.
+constexpr uint32_t kFixRounds = 32;
+constexpr uint32_t kFixPer = 16;
+// A piece's start and its predecessor's end, as this round sees them: loads that another lane of
+// the wave may have stored in the previous round (a workgroup-scope fence orders the rounds).
+__device__ __forceinline__ uint32_t ld_wg(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S, const uint32_t* luts, uint32_t dcp,
+                                 uint32_t acp, uint32_t* row, uint32_t* ring, uint32_t* rring) {
+    const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const bool final_seg = seg_is_final(b, s);  // trailing bytes after its last MCU are ignored
     bool bad = false, done = false;
@@ -1674,8 +1676,8 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
             b.piece_nmcu[u] = 0u;
             continue;
         }
-        uint32_t pend = b.piece_end[u];
-        if (b.piece_bit[u] != expect) {  // the start had not synchronised: re-walk from the truth
+        uint32_t pend = ld_wg(b.piece_end + u);
+        if (ld_wg(b.piece_bit + u) != expect) {  // the start had not synchronised: re-walk from the truth
             const PieceGeo P = piece_geo(b, S, s, u);
             pend = redo_piece<true>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, rring, true);
         }
@@ -1689,6 +1691,98 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
         expect = pend;
     }
     if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+    b.seg_fix[s] = 0u;
+}
+
+__global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
+    JD_PRIO_CRIT();
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
+    const uint32_t li = blockIdx.x * kRedoThreads + threadIdx.x;
+    uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
+    if (s != kInvalidImage && !b.seg_fix[s]) s = kInvalidImage;
+    const bool need = s != kInvalidImage;
+    if (!__syncthreads_or(need)) return;  // workgroup-uniform: the common case
+    const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
+    if (!need) return;
+    SegInfo S;
+    seg_info(b, s, S);
+    uint32_t dcp, acp;
+    table_slots(ts, S, dcp, acp);
+    chain_fix_serial(b, s, S, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
+                     s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
+                     s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords);
+}
+
+__global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
+    JD_PRIO_CRIT();
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t li = blockIdx.x * kRedoThreads + lane;
+    const uint32_t sl = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
+    uint64_t todo = __ballot(sl != kInvalidImage && b.seg_fix[sl] != 0u);
+    if (!todo) return;  // wave-uniform: the common case
+    const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
+    const uint32_t* const luts = reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0);
+    uint32_t* const row = s_rows + lane * row_words(kWin);
+    uint32_t* const ring = s_rows + kRedoThreads * row_words(kWin) + lane * kRingWords;
+    uint32_t* const rring = s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + lane * kRecRingWords;
+    while (todo) {  // wave-uniform
+        const int L = __builtin_ctzll(todo);
+        todo &= todo - 1u;
+        const uint32_t s = uint32_t(__shfl(int(sl), L, 64));
+        SegInfo S;
+        seg_info(b, s, S);
+        uint32_t dcp, acp;
+        table_slots(ts, S, dcp, acp);
+        const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
+        bool agreed = false;
+        for (uint32_t round = 0; round < kFixRounds && !agreed; round++) {
+            agreed = true;
+            // kFixPer consecutive pieces per lane: their loads in flight together (45 K pieces: 44
+            // wave-iterations per round)
+            for (uint32_t j0 = 0; j0 < n; j0 += kRedoThreads * kFixPer) {
+                const uint32_t jb = j0 + lane * kFixPer;
+                uint32_t ends[kFixPer + 1], starts[kFixPer];
+                ends[0] = (jb > 0 && jb < n) ? ld_wg(b.piece_end + base + jb - 1u) : 0u;
+#pragma unroll
+                for (uint32_t t = 0; t < kFixPer; t++) {
+                    const bool in = jb + t < n;
+                    starts[t] = in ? ld_wg(b.piece_bit + base + jb + t) : 0u;
+                    ends[t + 1] = in ? ld_wg(b.piece_end + base + jb + t) : 0u;
+                }
+                uint32_t mis = 0;  // bit t: piece jb + t disagrees (piece 0 starts at bit 0: always right)
+#pragma unroll
+                for (uint32_t t = 0; t < kFixPer; t++)
+                    mis |= (jb + t > 0 && jb + t < n && starts[t] != ends[t]) ? (1u << t) : 0u;
+                if (!__any(mis != 0u)) continue;  // wave-uniform
+                agreed = false;
+#pragma unroll
+                for (uint32_t t = 0; t < kFixPer; t++) {
+                    const bool need = (mis >> t) & 1u;
+                    if (!__any(need)) continue;  // wave-uniform
+                    const uint32_t u = base + jb + t;
+                    PieceGeo P{0u, 1u, 0u, 0u, 0u};
+                    if (need) P = piece_geo(b, S, s, u);
+                    redo_piece<true>(b, S, P, s, u, ends[t], luts, dcp, acp, row, ring, rring, need);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this round's ends before the next reads
+        }
+        if (agreed) {  // the counts, wave-parallel (it clears seg_fix)
+            const uint32_t nmcu_seg = S.nblk / S.bpm;
+            const bool final_seg = seg_is_final(b, s);
+            if (n > 4096)
+                chain_interval<16>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+            else if (n > 64)
+                chain_interval<4>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+            else
+                chain_interval<1>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+        } else if (lane == 0) {
+            chain_fix_serial(b, s, S, luts, dcp, acp, row, ring, rring);
+        }
+    }
 }
 
 // k_gather: a piece's block records -> BlockInfo at the blocks' global positions, AC-entry offsets
@@ -3593,7 +3687,10 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
         case 6:
             if (!b.nseg) break;
             hipLaunchKernelGGL(k_chain, dim3((b.nseg + 3) / 4), dim3(256), 0, s, b);
-            if (b.nchain) hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
+            if (b.nchain && b.big_chain)
+                hipLaunchKernelGGL(k_chain_big, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
+            else if (b.nchain)
+                hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
             break;
         case 7:
             if (b.nsub) hipLaunchKernelGGL(k_gather, dim3((b.nsub + 255) / 256), dim3(256), 0, s, b);  // 64 pieces per wave

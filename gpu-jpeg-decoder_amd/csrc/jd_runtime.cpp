@@ -159,12 +159,18 @@ struct Slot {
     hipEvent_t h2d_done = nullptr;               // after the slot's latest host-input copies
     hipEvent_t plan_done = nullptr;              // after the slot's latest plan upload
     bool h2d_recorded = false, plan_recorded = false;
+    // JD_IDCT_STREAM=1 (experiment): the colour stage on a stream of its own (JD_IDCT_PRIO), entered
+    // and left through events, so that its waves can be given another dispatch priority
+    hipStream_t istream = nullptr;
+    hipEvent_t ev_tail = nullptr, ev_idct = nullptr;
 };
 
-// One launched batch whose results are not collected yet.  jd_decode_batch_async keeps up to
-// kAsyncDepth of them in flight: the host parses, plans and enqueues batch k+2 on its slot's stream
-// (behind batch k) before it waits for batch k, so batch k+2's front-end starts the moment batch k
-// ends instead of a host plan later.
+// One launched batch whose results are not collected yet.  jd_decode_batch_async returns with the
+// newest async_depth launches in flight: 1 by default (the previous launch is collected before the
+// call returns); with JD_ASYNC_DEPTH=2 the host parses, plans and enqueues batch k+2 on its slot's
+// stream (behind batch k) before it waits for batch k.  That starts batch k+2's front-end the
+// moment batch k ends, but the two slots' walks then often run together, and the step measured
+// 3-4 % slower.
 struct Pending {
     bool active = false;
     uint64_t seq = 0;                           // launch order
@@ -183,7 +189,8 @@ struct Pending {
     double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0, piece_overlap = 0;
     double t_plan = 0, t_upload = 0;
 };
-constexpr int kNumPending = 4;  // records (>= the async depth + 2: a record is reused 4 launches later)
+constexpr int kNumPending = 4;
+constexpr int kIdctSlot = 9;    // timing slot of k_idct_color (jd_kernel_name): the colour stage starts here  // records (>= the async depth + 2: a record is reused 4 launches later)
 
 struct jd_ctx {
     int device = 0;
@@ -209,7 +216,7 @@ struct jd_ctx {
     Pending pend[kNumPending];
     int slot = 0;                        // the slot the next launch uses
     uint64_t seq = 0;                    // launches so far (the next launch's record: pend[seq % kNumPending])
-    int async_depth = 2;                 // batches jd_decode_batch_async leaves in flight (JD_ASYNC_DEPTH: 1 or 2)
+    int async_depth = 1;                 // batches jd_decode_batch_async leaves in flight (JD_ASYNC_DEPTH: 1 or 2)
     const void* last_stream = nullptr;  // caller stream of the pending launches (nullptr: the slots' own)
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     int max_batch_images = 0;           // items per launched sub-batch (JD_MAX_BATCH_IMAGES)
@@ -891,6 +898,11 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.piece_plan = (P.piece_bits == kPieceBits && !(ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES)) &&
                         !ctx->fixed_pieces) ? piece_lanes_resident(huffman_lds_bytes(P.max_slots)) : 0u;
         b.no_pool = ctx->spare_pieces == 0 ? 1u : 0u;
+        {  // an interval holds at most its image's ECS bits, in pieces of at least P.piece_bits
+            uint64_t most = 0;
+            for (const ImgDesc& d : P.imgs) most = std::max<uint64_t>(most, (uint64_t(d.len - d.ecs_off) * 8 + P.piece_bits - 1) / P.piece_bits);
+            b.big_chain = most > kBigInterval ? 1u : 0u;
+        }
         b.piece_overlap = P.piece_overlap;
         uint32_t* pc[9];
         for (int q = 0; q < 9; q++) pc[q] = reinterpret_cast<uint32_t*>(base + o_piece[q]);
@@ -947,11 +959,24 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const double t_upload = tms();
         rng.reset(new Range("jd_launch"));
         double t_k[JD_NUM_KERNELS];
+        const bool split = sl.istream != nullptr && s == sl.stream;  // (a caller stream orders everything)
         for (int k = 0; k < JD_NUM_KERNELS; k++) {
-            if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][0], s));
-            HIPCHK(ctx, launch_kernel(k, b, s));
-            if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][1], s));
+            hipStream_t ks = s;
+            if (split && k >= kIdctSlot) {
+                if (k == kIdctSlot) {
+                    HIPCHK(ctx, hipEventRecord(sl.ev_tail, s));
+                    HIPCHK(ctx, hipStreamWaitEvent(sl.istream, sl.ev_tail, 0));
+                }
+                ks = sl.istream;
+            }
+            if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][0], ks));
+            HIPCHK(ctx, launch_kernel(k, b, ks));
+            if (timing) HIPCHK(ctx, hipEventRecord(pd.ev[k][1], ks));
             t_k[k] = tms();
+        }
+        if (split) {  // the slot's later work (status readback, the next batch) after the colour stage
+            HIPCHK(ctx, hipEventRecord(sl.ev_idct, sl.istream));
+            HIPCHK(ctx, hipStreamWaitEvent(s, sl.ev_idct, 0));
         }
         if (ctx->host_timing) {
             std::fprintf(stderr, "host launch returns:");
@@ -1158,7 +1183,7 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
     if (const char* e = std::getenv("JD_STAGE_NT")) ctx->stage_nt = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_H2D_SERIAL")) ctx->h2d_serial = std::strtoll(e, nullptr, 0) != 0;
-    if (const char* e = std::getenv("JD_ASYNC_DEPTH")) ctx->async_depth = std::strtoll(e, nullptr, 0) == 1 ? 1 : 2;
+    if (const char* e = std::getenv("JD_ASYNC_DEPTH")) ctx->async_depth = std::strtoll(e, nullptr, 0) == 2 ? 2 : 1;
     if (const char* e = std::getenv("JD_STAGE_CHUNK_MB")) {
         const long long mb = std::strtoll(e, nullptr, 0);
         ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);
@@ -1167,10 +1192,24 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
         delete ctx;
         return JD_ERR_HIP;
     }
+    // experiment knobs: JD_SLOT_PRIO / JD_IDCT_PRIO = 1 (greatest priority) or -1 (least); JD_IDCT_STREAM=1
+    int prio_least = 0, prio_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    auto prio_of = [&](const char* env) {
+        const char* e = std::getenv(env);
+        const long v = e ? std::strtol(e, nullptr, 0) : 0;
+        return v > 0 ? prio_greatest : v < 0 ? prio_least : 0;
+    };
+    const bool idct_stream = std::getenv("JD_IDCT_STREAM") && std::strtol(std::getenv("JD_IDCT_STREAM"), nullptr, 0) != 0;
     for (Slot& sl : ctx->slots) {
-        bool ok = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess;
+        bool ok = hipStreamCreateWithPriority(&sl.stream, hipStreamNonBlocking, prio_of("JD_SLOT_PRIO")) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&sl.h2d_done, hipEventDisableTiming) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&sl.plan_done, hipEventDisableTiming) == hipSuccess;
+        if (ok && idct_stream) {
+            ok = hipStreamCreateWithPriority(&sl.istream, hipStreamNonBlocking, prio_of("JD_IDCT_PRIO")) == hipSuccess;
+            ok = ok && hipEventCreateWithFlags(&sl.ev_tail, hipEventDisableTiming) == hipSuccess;
+            ok = ok && hipEventCreateWithFlags(&sl.ev_idct, hipEventDisableTiming) == hipSuccess;
+        }
         if (!ok) {
             jd_ctx_destroy(ctx);
             return JD_ERR_HIP;
@@ -1204,6 +1243,9 @@ jd_status jd_ctx_destroy(jd_ctx* ctx) {
         if (sl.stream) (void)hipStreamDestroy(sl.stream);
         if (sl.h2d_done) (void)hipEventDestroy(sl.h2d_done);
         if (sl.plan_done) (void)hipEventDestroy(sl.plan_done);
+        if (sl.istream) (void)hipStreamDestroy(sl.istream);
+        if (sl.ev_tail) (void)hipEventDestroy(sl.ev_tail);
+        if (sl.ev_idct) (void)hipEventDestroy(sl.ev_idct);
     }
     for (Pending& pd : ctx->pend) {
         if (pd.host) (void)hipHostFree(pd.host);

@@ -130,18 +130,16 @@ jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* r
                           int rgb_on_device, void* hip_stream);
 
 /* Pipelined form of jd_decode_batch with device outputs (rgb are device pointers): returns once
- * the batch is launched, leaving it and the batch launched before it in flight; the batch two
- * calls back is collected by then.  The host parses and plans batch k+2 (and stages its host
- * inputs) and enqueues it on its slot's stream behind batch k before it waits for batch k, so
- * the GPU never waits for the host between batches (JD_ASYNC_DEPTH=1: one batch in flight, the
- * previous one collected before the call returns).  Inputs may be device-resident (jpeg_dev) or
- * host memory (jpeg_dev NULL): host inputs are copied into the launching slot's pinned staging by
- * the context's host workers before the call returns, and uploaded by an H2D on that slot's
- * stream, which overlaps the other slot's kernels.  results[], the rgb buffers and the jpeg_dev
- * buffers must stay valid and unused by other calls until the batch is collected: by the second
- * jd_decode_batch_async call after it, by a jd_decode_batch call, or by jd_decode_wait; host jpeg
- * buffers only until the call returns, unless they lie in a range registered with
- * jd_host_register (then until the batch is collected). */
+ * the batch is launched, after collecting the batch launched before it, so the host parses and
+ * plans batch k+1 (and stages its host inputs) while the GPU decodes batch k.  Inputs may be
+ * device-resident (jpeg_dev) or host memory (jpeg_dev NULL): host inputs are copied into the
+ * launching slot's pinned staging by the context's host workers before the call returns, and
+ * uploaded by an H2D on that slot's stream, which overlaps the other slot's kernels.  results[],
+ * the rgb buffers and the jpeg_dev buffers must stay valid and unused by other calls until the
+ * batch is collected: by the next jd_decode_batch_async call (the second next with
+ * JD_ASYNC_DEPTH=2, which leaves two batches in flight), by a jd_decode_batch call, or by
+ * jd_decode_wait; host jpeg buffers only until the call returns, unless they lie in a range
+ * registered with jd_host_register (then until the batch is collected). */
 jd_status jd_decode_batch_async(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
                                 void* hip_stream);
 /* Collects every launched batch (fills their results). */

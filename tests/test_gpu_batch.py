@@ -201,6 +201,38 @@ def test_mutated_files_batch_matches_oracle_status_and_pixels():
         dec.close()
 
 
+@pytest.mark.parametrize("depth", [1, 2])
+def test_async_depth_results_and_pixels(monkeypatch, depth):
+    """jd_decode_batch_async with one or two batches left in flight (JD_ASYNC_DEPTH): after call k
+    returns, batch k - depth is collected (its results filled); host-staged and device inputs
+    alternate, every image bit-exact after jd_decode_wait."""
+    monkeypatch.setenv("JD_ASYNC_DEPTH", str(depth))
+    sets = [jd_synth.make_batch(6, 640 + 64 * k, 360, 90, ("4:2:0", "4:4:4", "4:2:2")[k % 3], k % 2, 0,
+                                seed0=9700 + 20 * k) for k in range(5)]
+    dec = jdamd.Decoder(0)
+    try:
+        runs = []
+        for k, datas in enumerate(sets):
+            hosts, hdrs, din, dout, offs, ooffs = _device_batch(dec, datas)
+            dev_in = [din.ptr + o for o in offs] if k % 2 == 0 else [None] * len(datas)  # odd: host-staged
+            bt = dec.make_batch(hosts, dev_in, [dout.ptr + o for o in ooffs])
+            for r in bt[1]:
+                r.status = -1
+            dec.decode_prepared(bt, pipelined=True)
+            runs.append((bt, hdrs, din, dout, ooffs, datas))
+            if k >= depth:  # the batch `depth` calls back is collected by now
+                assert [r.status for r in runs[k - depth][0][1]] == [0] * len(sets[k - depth])
+            assert [r.status for r in bt[1]] == [-1] * len(datas)  # this one is in flight
+        dec.wait()
+        for bt, hdrs, din, dout, ooffs, datas in runs:
+            assert [r.status for r in bt[1]] == [0] * len(datas)
+            for i, h in enumerate(hdrs):
+                got = dout.download(np.empty((h.height, h.width, 3), np.uint8), ooffs[i])
+                assert np.array_equal(got, jdoracle.decode(datas[i])[1]), i
+    finally:
+        dec.close()
+
+
 def test_download_after_async_without_wait():
     """jd_memcpy_d2h right after jd_decode_batch_async, with no
     jd_decode_wait: the copy is ordered after the pending batch on the context."""

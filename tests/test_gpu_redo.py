@@ -128,3 +128,27 @@ def test_dense_streams_without_spare_regions(monkeypatch, dense_batch, path):
         assert list(dec.debug_fetch("rw_div")[:5]) == [4, 4, 4, 4, 4]
     finally:
         dec.close()
+
+
+@pytest.mark.parametrize("overlap,spare", [("1024", "default"), ("256", "default"), ("64", "0")])
+def test_big_interval_rounds_vs_oracle(monkeypatch, overlap, spare):
+    """One image without DRI in a batch of its own: a single interval of ~45 K 512-bit pieces, which
+    k_chain leaves to k_chain_big (wave-parallel re-walk rounds, then the counts by prefix sums).
+    A short warm-up makes runs of consecutive failed starts (several rounds); with a 64-bit warm-up
+    and no spare regions the runs outlast kFixRounds and the serial walk finishes the interval."""
+    import bench
+
+    (data,) = jd_synth.make_images(bench.ref444_jobs([bench.REF_SIZES.index(2000)], 95), workers=1)
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    monkeypatch.setenv("JD_PIECE_OVERLAP_BITS", overlap)
+    if spare != "default":
+        monkeypatch.setenv("JD_SPARE_PIECES", spare)
+    dec = jdamd.Decoder(0, timing=True)
+    try:
+        out = dec.decode(data)
+        nsub = int((dec.debug_fetch("sub_seg") != 0xFFFFFFFF).sum())
+        assert nsub > 4096  # one interval beyond kBigInterval pieces
+        assert np.array_equal(out, ref)
+    finally:
+        dec.close()

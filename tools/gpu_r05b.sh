@@ -6,3 +6,5 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu.py 
 tail -2 gpurun_out/r05b/tests.log
 AB_REPS=2 bash tools/ab.sh gpurun_out/r05b/ab cur@JD_ASYNC_DEPTH=1 cur@JD_ASYNC_DEPTH=2
 bash tools/trace.sh r05b cur@JD_ASYNC_DEPTH=1 cur@JD_ASYNC_DEPTH=2
+# k_idct_color scatter ablations (wrong pixels; serialized kernel times from the bench line)
+bash tools/ab.sh gpurun_out/r05b/abl cur ablsc1 ablsc2
