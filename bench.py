@@ -34,6 +34,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -379,11 +380,28 @@ def valu_issue(config: str, kernel: str, avg_ms: float):
     clk = k.get("clock_ghz") or 2.4
     n = k.get("dispatches_per_batch", 1.0)  # instances per timing slot (one per sampling layout)
     busy = (k.get("counters", {}).get("SQ_ACTIVE_INST_VALU") or k["valu_insts"]) * n
-    frac = busy * VALU_CYCLES_PER_QUAD / (SIMDS * clk * 1e9 * avg_ms * 1e-3)
+    cyc, wsrc = valu_weight(kernel)
+    frac = busy * cyc / (SIMDS * clk * 1e9 * avg_ms * 1e-3)
     return {"valu_insts_per_launch": k["valu_insts"] * n, "dispatches_per_batch": n, "clock_ghz": clk, "busy_frac": frac,
+            "busy_frac_x4": busy * VALU_CYCLES_PER_QUAD / (SIMDS * clk * 1e9 * avg_ms * 1e-3),
+            "cycles_per_valu": cyc,
             "note": "issue model, not a measured utilisation: VALU instructions (SQ_ACTIVE_INST_VALU, equal to "
-                    "SQ_INSTS_VALU on gfx950) x 4 cycles over the launch's SIMD cycles",
+                    "SQ_INSTS_VALU on gfx950) x the kernel's static-mix issue cycles per instruction (" + wsrc +
+                    ") over the launch's SIMD cycles; busy_frac_x4 prices every instruction at 4 cycles",
             "source": src}
+
+
+def valu_weight(kernel: str):
+    """Wave64 issue cycles per VALU instruction of `kernel` (the mean over its instances, e.g. one
+    k_idct_color per sampling layout) from the committed static-mix table (tools/valu_weights.py:
+    the ISA's opcode mix priced by tools/micro/valurate.hip's measured rates), else 4."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_weights.json")), key=_profile_order, reverse=True)
+    if files:
+        ks = json.load(open(files[0]))["kernels"]
+        w = [v["cycles_per_valu"] for v in ks.values() if re.match(rf"{kernel}(E|I)", v["name"])]
+        if w:
+            return sum(w) / len(w), os.path.relpath(files[0], ROOT)
+    return float(VALU_CYCLES_PER_QUAD), "flat 4 cycles"
 
 
 def kernel_rooflines(kern: dict, config: str) -> dict:

@@ -316,6 +316,7 @@ struct BatchDev {
     uint32_t* piece_mcu0;         // chain: first MCU of the piece within its segment
     uint32_t* seg_fix;            // k_chain: 1 = the interval needs k_chain_fix / k_chain_big
     uint32_t big_chain;           // an interval may have more than kBigInterval pieces: k_chain_big
+    uint32_t small_fold;          // small batch (no piece plan): k_compact's first workgroups run the subplan
     CpRec* piece_cp;              // kCpRecords per piece slot (CpRec)
     const uint32_t* chain_seg;    // k_chain_fix: segment of each lane, grouped by table set
     uint32_t nchain;              // multiple of kPieceThreads

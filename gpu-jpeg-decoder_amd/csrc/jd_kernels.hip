@@ -142,6 +142,8 @@ __device__ __forceinline__ uint32_t scan_masks(uint32_t x, uint32_t& ff, uint32_
     return zero;
 }
 
+__device__ void subplan_image(const BatchDev& b, uint32_t img, int lane);  // (below, with k_subplan)
+
 __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     JD_PRIO_SHORT();
     __shared__ uint32_t s_wsum[2][kScanThreads / 64];
@@ -372,6 +374,7 @@ __global__ __launch_bounds__(kScanThreads) void k_compact(BatchDev b) {
     __shared__ uint32_t s_wsum[kScanThreads / 64];
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t c = blockIdx.x;
+    if (b.small_fold && c == 0 && threadIdx.x < 64) subplan_image(b, blockIdx.y, int(threadIdx.x));  // (k_index's output only)
     if (c >= im.nchunks) return;
     const uintptr_t file = uintptr_t(im.jpeg);
     const uintptr_t lo = file + im.ecs_off, fend = file + im.len;
@@ -655,10 +658,12 @@ __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
 // first region word: piece j of an interval of n pieces owns region_words(plen) words from
 // seg_ent + j * region_words(plen).  The image's spare words after them (img_pool) are handed
 // out to re-walks (k_redo, k_chain_fix).
-__global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
-    JD_PRIO_SHORT();
-    const ImgDesc& im = b.imgs[blockIdx.x];
-    const int lane = threadIdx.x;
+// (small batches: run by the first k_compact workgroup of each image, beside its compaction, which
+// saves a launch on a small batch's critical path; in a large batch the per-image waves lengthen
+// k_compact's tail by more than the launch costs: 0.24 -> 0.48 ms on C2, so k_subplan runs as a
+// kernel of its own there)
+__device__ void subplan_image(const BatchDev& b, uint32_t img, int lane) {
+    const ImgDesc& im = b.imgs[img];
     const uint32_t piece_bits = b.piece_plan ? uint32_t(b.counters[3] & 0xFFFFFFFFull) : b.piece_bits;
     uint32_t run = 0, wrun = 0;
     for (uint32_t k0 = 0; k0 < im.nseg; k0 += 64) {
@@ -683,7 +688,7 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     }
     // run <= sub_cap and wrun <= entry_cap by construction (host bounds: ceil(ECS bits /
     // piece_bits) + nseg pieces, ECS bits / rw_div + kRegionSlack + 4 words per piece)
-    if (lane == 0) b.img_pool[blockIdx.x] = wrun;
+    if (lane == 0) b.img_pool[img] = wrun;
     const uint32_t used = min(run, im.sub_cap);
     // the image's slots: the next `used` of its table set's range (every image's share fits: the
     // range holds the sum of their caps), so the batch's pieces are dense from the range's start
@@ -698,6 +703,10 @@ __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
         for (uint32_t u = lane; u < n; u += 64)
             if (off + u < used) b.sub_seg[base + off + u] = s;
     }
+}
+__global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
+    JD_PRIO_SHORT();
+    subplan_image(b, blockIdx.x, int(threadIdx.x));
 }
 
 // Bytes a window round advances (the piece walks' LDS rows hold one window plus an 8-byte
@@ -1538,7 +1547,8 @@ __device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_
 // One wave per interval s of n pieces (k_chain), kPer consecutive pieces per lane: an interval
 // without DRI can have a thousand pieces, and each wave-iteration is a round of dependent global
 // loads (kPer = 4 there; 1 for the short intervals of DRI streams).
-template <uint32_t kPer>
+// kAgreed: the caller has just verified every start (k_chain_big's last round): no second check.
+template <uint32_t kPer, bool kAgreed = false>
 __device__ __forceinline__ void chain_interval(const BatchDev& b, uint32_t s, uint32_t lane, const SegInfo& S,
                                                uint32_t base, uint32_t n, uint32_t nmcu_seg, bool final_seg) {
     // The scan's last interval ends at EOI, and what follows its last MCU is ignored: the piece
@@ -1570,7 +1580,7 @@ __device__ __forceinline__ void chain_interval(const BatchDev& b, uint32_t s, ui
         }
     }
     bool need = false;
-    for (uint32_t j0 = 0; j0 <= jl; j0 += kStep) {
+    for (uint32_t j0 = 0; !kAgreed && j0 <= jl; j0 += kStep) {
 #pragma unroll
         for (uint32_t t = 0; t < kPer; t++) {
             const uint32_t j = j0 + kPer * lane + t;
@@ -1774,11 +1784,11 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
             const uint32_t nmcu_seg = S.nblk / S.bpm;
             const bool final_seg = seg_is_final(b, s);
             if (n > 4096)
-                chain_interval<16>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+                chain_interval<16, true>(b, s, lane, S, base, n, nmcu_seg, final_seg);
             else if (n > 64)
-                chain_interval<4>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+                chain_interval<4, true>(b, s, lane, S, base, n, nmcu_seg, final_seg);
             else
-                chain_interval<1>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+                chain_interval<1, true>(b, s, lane, S, base, n, nmcu_seg, final_seg);
         } else if (lane == 0) {
             chain_fix_serial(b, s, S, luts, dcp, acp, row, ring, rring);
         }
@@ -3664,10 +3674,15 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             break;
         case 1: hipLaunchKernelGGL(k_index, dim3(b.nimg), dim3(64), 0, s, b); break;
         case 2:
+            if (b.small_fold && b.nsub) {  // (before k_compact, which runs the subplan) every slot not
+                                           // claimed by an interval (per-image slack, padding) reads invalid
+                const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
+                if (e != hipSuccess) return e;
+            }
             if (b.max_chunks) hipLaunchKernelGGL(k_compact, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
             break;
         case 3: {
-            if (!b.nsub) break;
+            if (!b.nsub || b.small_fold) break;
             // every slot not claimed by an interval (per-image slack, padding) must read invalid
             const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
             if (e != hipSuccess) return e;

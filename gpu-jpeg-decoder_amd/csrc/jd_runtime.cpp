@@ -190,7 +190,10 @@ struct Pending {
     double t_plan = 0, t_upload = 0;
 };
 constexpr int kNumPending = 4;
-constexpr int kIdctSlot = 9;    // timing slot of k_idct_color (jd_kernel_name): the colour stage starts here  // records (>= the async depth + 2: a record is reused 4 launches later)
+constexpr int kIdctSlot = 9;
+// batches of at most this many images without a piece plan fold the subplan into k_compact
+// (jd_kernels.hip subplan_image: a launch saved on a small batch's critical path)
+constexpr uint32_t kSmallFoldImages = 64;    // timing slot of k_idct_color (jd_kernel_name): the colour stage starts here  // records (>= the async depth + 2: a record is reused 4 launches later)
 
 struct jd_ctx {
     int device = 0;
@@ -898,6 +901,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.piece_plan = (P.piece_bits == kPieceBits && !(ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES)) &&
                         !ctx->fixed_pieces) ? piece_lanes_resident(huffman_lds_bytes(P.max_slots)) : 0u;
         b.no_pool = ctx->spare_pieces == 0 ? 1u : 0u;
+        b.small_fold = (b.piece_plan == 0 && P.total_chunks > 0 && nimg <= kSmallFoldImages) ? 1u : 0u;
         {  // an interval holds at most its image's ECS bits, in pieces of at least P.piece_bits
             uint64_t most = 0;
             for (const ImgDesc& d : P.imgs) most = std::max<uint64_t>(most, (uint64_t(d.len - d.ecs_off) * 8 + P.piece_bits - 1) / P.piece_bits);
