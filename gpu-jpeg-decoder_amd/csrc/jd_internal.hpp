@@ -196,7 +196,7 @@ constexpr int kPieceThreads = JD_PIECE_THREADS;
 constexpr uint32_t kSmallPieceLanes = JD_SMALL_PIECE_LANES;
 // k_chain leaves intervals of more pieces to k_chain_big (wave-parallel re-walk rounds and counts),
 // which the host launches instead of k_chain_fix when an image's ECS may hold that many pieces
-constexpr uint32_t kBigInterval = 4096;
+constexpr uint32_t kBigInterval = 256;
 
 // Scan / compaction geometry: each chunk is 16 KiB of one image's ECS, 256 threads x 64 bytes.
 constexpr int kScanThreads = 256;
@@ -315,7 +315,8 @@ struct BatchDev {
                                   // checkpoint join - 1; 0 = none)
     uint32_t* piece_mcu0;         // chain: first MCU of the piece within its segment
     uint32_t* seg_fix;            // k_chain: 1 = the interval needs k_chain_fix / k_chain_big
-    uint32_t big_chain;           // an interval may have more than kBigInterval pieces: k_chain_big
+    uint32_t big_chain;           // a small batch (no piece plan) whose intervals may have more than
+                                  // kBigInterval pieces: k_chain_big, and re-walks with LDS tables
     uint32_t small_fold;          // small batch (no piece plan): k_compact's first workgroups run the subplan
     CpRec* piece_cp;              // kCpRecords per piece slot (CpRec)
     const uint32_t* chain_seg;    // k_chain_fix: segment of each lane, grouped by table set

@@ -1483,10 +1483,15 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
 // predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images).
 // Starting from that end is exact when the predecessor is right; a predecessor re-walked in this
 // round keeps its end when it joins its speculative walk, and otherwise k_chain notices.
+// LT: the table set staged in LDS (small batches, BatchDev::big_chain or small_fold: the re-walks'
+// lookups are a serial chain, ~1 us each from global memory); else read from global memory, so the
+// workgroups need little LDS and fit beside the other batch's big kernels.
+template <bool LT>
 __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
     JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // [tables,] the lanes' rows and rings
+    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + (LT ? size_t(b.max_slots) * sizeof(HuffLut) : 0));
     const uint32_t u = blockIdx.x * kRedoThreads + threadIdx.x;
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
     uint32_t expect = 0;
@@ -1498,6 +1503,10 @@ __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
     if (!__syncthreads_or(need)) return;  // workgroup-uniform
     // the piece workgroup (kPieceThreads lanes, one table set) this one is part of
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
+    if (LT) {
+        stage_luts(b, ts, s_lut, kRedoThreads);
+        __syncthreads();
+    }
     SegInfo S;
     PieceGeo P{0u, 1u, 0u, 0u, 0u};
     if (need) {
@@ -1508,10 +1517,11 @@ __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
     }
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    redo_piece<true>(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
-                     s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
-                     s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords,
-                     need);
+    redo_piece<!LT>(b, S, P, s, u, expect,
+                    LT ? reinterpret_cast<const uint32_t*>(s_lut) : reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0),
+                    dcp, acp, s_rows + threadIdx.x * row_words(kWin),
+                    s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
+                    s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords, need);
 }
 
 // The MCUs piece j contributes, given its first MCU m0 (the interval has nmcu_seg): a piece before
@@ -1637,7 +1647,7 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
     const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const bool final_seg = seg_is_final(b, s);
-    if (n > kBigInterval) {  // (one interval without DRI: a big image in short pieces) -> k_chain_big
+    if (b.big_chain && n > kBigInterval) {  // (one interval without DRI: a big image in short pieces) -> k_chain_big
         if (lane == 0) b.seg_fix[s] = 1u;
         return;
     }
@@ -1672,6 +1682,7 @@ constexpr uint32_t kFixPer = 16;
 __device__ __forceinline__ uint32_t ld_wg(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+template <bool GL>
 __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S, const uint32_t* luts, uint32_t dcp,
                                  uint32_t acp, uint32_t* row, uint32_t* ring, uint32_t* rring) {
     const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
@@ -1689,7 +1700,7 @@ __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S
         uint32_t pend = ld_wg(b.piece_end + u);
         if (ld_wg(b.piece_bit + u) != expect) {  // the start had not synchronised: re-walk from the truth
             const PieceGeo P = piece_geo(b, S, s, u);
-            pend = redo_piece<true>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, rring, true);
+            pend = redo_piece<GL>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, rring, true);
         }
         const uint32_t pm = b.piece_nmcu[u], em = b.piece_emcu[u];
         const bool last = j + 1 == n || (final_seg && mcu_run + pm >= nmcu_seg);
@@ -1719,22 +1730,87 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
     seg_info(b, s, S);
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    chain_fix_serial(b, s, S, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
+    chain_fix_serial<true>(b, s, S, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
                      s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
                      s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords);
 }
 
+// chain_interval's counts for an interval whose starts all agree, in one pass of kFixPer pieces per
+// lane (k_chain_big): the piece whose MCUs reach the final interval's count (jl, the last that
+// matters) is found in the same pass that hands out the first MCUs.  Pieces before jl take what
+// they walked, jl the rest, the ones after it nothing; if no piece reaches the count, the interval
+// is short of MCUs (corrupt), as chain_interval decides with jl = n - 1.
+__device__ void chain_counts_onepass(const BatchDev& b, uint32_t s, uint32_t lane, uint32_t base, uint32_t n,
+                                     uint32_t nmcu_seg, bool final_seg) {
+    constexpr uint32_t kPer = kFixPer, kStep = 64 * kPer;
+    uint32_t jl = final_seg ? 0xFFFFFFFFu : n - 1u;  // wave-uniform
+    uint32_t mcu_run = 0;
+    bool bad = false;
+    for (uint32_t j0 = 0; j0 < n; j0 += kStep) {
+        const uint32_t jb = j0 + kPer * lane;
+        uint32_t pm[kPer], em[kPer], c[kPer];
+#pragma unroll
+        for (uint32_t t = 0; t < kPer; t++) {
+            const bool in = jb + t < n;
+            pm[t] = in ? b.piece_nmcu[base + jb + t] : 0u;
+            em[t] = in ? b.piece_emcu[base + jb + t] : kNoError;
+        }
+        if (jl == 0xFFFFFFFFu) {  // wave-uniform: is the last piece that matters in this chunk?
+#pragma unroll
+            for (uint32_t t = 0; t < kPer; t++) c[t] = pm[t] + (t ? c[t - 1] : 0u);
+            const uint32_t before = mcu_run + uint32_t(wave_scan_dpp(int(c[kPer - 1]))) - c[kPer - 1];
+            uint32_t tf = kPer;
+#pragma unroll
+            for (int t = kPer - 1; t >= 0; t--)
+                if (jb + t < n && before + c[t] >= nmcu_seg) tf = uint32_t(t);
+            const uint64_t hit = __ballot(tf < kPer);
+            if (hit) {
+                const int L = __builtin_ctzll(hit);
+                jl = j0 + kPer * uint32_t(L) + uint32_t(__shfl(int(tf), L, 64));
+            }
+        }
+        uint32_t pin[kPer], ex[kPer], tot = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < kPer; t++) {
+            const uint32_t j = jb + t;
+            pin[t] = (j < jl && j < n) ? pm[t] : 0u;  // (jl unknown: every piece of the chunk is before it)
+            ex[t] = tot;
+            tot += pin[t];
+        }
+        const uint32_t before = mcu_run + uint32_t(wave_scan_dpp(int(tot))) - tot;
+#pragma unroll
+        for (uint32_t t = 0; t < kPer; t++) {
+            const uint32_t j = jb + t;
+            if (j >= n) continue;
+            const uint32_t m0 = before + ex[t];
+            uint32_t take = 0;
+            if (j <= jl) take = piece_take(pm[t], em[t], m0, nmcu_seg, j == jl, final_seg, bad);
+            b.piece_mcu0[base + j] = min(m0, nmcu_seg);
+            b.piece_nmcu[base + j] = (m0 <= nmcu_seg) ? min(take, nmcu_seg - m0) : 0u;
+        }
+        mcu_run = uint32_t(__shfl(int(before + tot), 63, 64));
+    }
+    bad |= jl == 0xFFFFFFFFu;  // no piece reached the final interval's count
+    if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+    if (lane == 0) b.seg_fix[s] = 0u;
+}
+
 __global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
     JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
+    // (small batches only: the table set is staged in LDS, as in k_piece -- the re-walks of each
+    // round are serial chains of lookups, ~1 us each from global memory)
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];
+    HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const uint32_t lane = threadIdx.x;
     const uint32_t li = blockIdx.x * kRedoThreads + lane;
     const uint32_t sl = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
     uint64_t todo = __ballot(sl != kInvalidImage && b.seg_fix[sl] != 0u);
     if (!todo) return;  // wave-uniform: the common case
     const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
-    const uint32_t* const luts = reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0);
+    stage_luts(b, ts, s_lut, kRedoThreads);
+    __syncthreads();
+    const uint32_t* const luts = reinterpret_cast<const uint32_t*>(s_lut);
     uint32_t* const row = s_rows + lane * row_words(kWin);
     uint32_t* const ring = s_rows + kRedoThreads * row_words(kWin) + lane * kRingWords;
     uint32_t* const rring = s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + lane * kRecRingWords;
@@ -1748,11 +1824,21 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
         table_slots(ts, S, dcp, acp);
         const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
         bool agreed = false;
+        // chunks of kRedoThreads * kFixPer pieces to (re)check: every chunk in the first round, then
+        // only those where the round before re-walked a piece, and the chunk after each (its first
+        // piece follows the re-walked chunk's last): bit ci for chunk ci < 64, hi for the rest
+        uint64_t dirty = ~0ull;
+        bool dirty_hi = true;
         for (uint32_t round = 0; round < kFixRounds && !agreed; round++) {
             agreed = true;
+            uint64_t next = 0;
+            bool next_hi = false;
             // kFixPer consecutive pieces per lane: their loads in flight together (45 K pieces: 44
             // wave-iterations per round)
-            for (uint32_t j0 = 0; j0 < n; j0 += kRedoThreads * kFixPer) {
+            for (uint32_t j0 = 0, ci = 0; j0 < n; j0 += kRedoThreads * kFixPer, ci++) {
+                const bool look = ci < 64 ? (((dirty >> ci) & 1u) || (ci > 0 && ((dirty >> (ci - 1)) & 1u)))
+                                          : (dirty_hi || (ci == 64 && (dirty >> 63)));
+                if (!look) continue;  // wave-uniform
                 const uint32_t jb = j0 + lane * kFixPer;
                 uint32_t ends[kFixPer + 1], starts[kFixPer];
                 ends[0] = (jb > 0 && jb < n) ? ld_wg(b.piece_end + base + jb - 1u) : 0u;
@@ -1768,6 +1854,8 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
                     mis |= (jb + t > 0 && jb + t < n && starts[t] != ends[t]) ? (1u << t) : 0u;
                 if (!__any(mis != 0u)) continue;  // wave-uniform
                 agreed = false;
+                if (ci < 64) next |= 1ull << ci;
+                else next_hi = true;
 #pragma unroll
                 for (uint32_t t = 0; t < kFixPer; t++) {
                     const bool need = (mis >> t) & 1u;
@@ -1775,22 +1863,17 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
                     const uint32_t u = base + jb + t;
                     PieceGeo P{0u, 1u, 0u, 0u, 0u};
                     if (need) P = piece_geo(b, S, s, u);
-                    redo_piece<true>(b, S, P, s, u, ends[t], luts, dcp, acp, row, ring, rring, need);
+                    redo_piece<false>(b, S, P, s, u, ends[t], luts, dcp, acp, row, ring, rring, need);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this round's ends before the next reads
+            dirty = next;
+            dirty_hi = next_hi;
         }
-        if (agreed) {  // the counts, wave-parallel (it clears seg_fix)
-            const uint32_t nmcu_seg = S.nblk / S.bpm;
-            const bool final_seg = seg_is_final(b, s);
-            if (n > 4096)
-                chain_interval<16, true>(b, s, lane, S, base, n, nmcu_seg, final_seg);
-            else if (n > 64)
-                chain_interval<4, true>(b, s, lane, S, base, n, nmcu_seg, final_seg);
-            else
-                chain_interval<1, true>(b, s, lane, S, base, n, nmcu_seg, final_seg);
+        if (agreed) {  // the counts, wave-parallel, in one pass
+            chain_counts_onepass(b, s, lane, base, n, S.nblk / S.bpm, seg_is_final(b, s));
         } else if (lane == 0) {
-            chain_fix_serial(b, s, S, luts, dcp, acp, row, ring, rring);
+            chain_fix_serial<false>(b, s, S, luts, dcp, acp, row, ring, rring);
         }
     }
 }
@@ -3697,13 +3780,18 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
                 hipLaunchKernelGGL(k_piece<64>, dim3(b.nsub / 64), dim3(64), piece_lds_bytes(b.max_slots, 64), s, b);
             break;
         case 5:
-            if (b.nsub) hipLaunchKernelGGL(k_redo, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
+            if (b.nsub && (b.big_chain || b.small_fold))
+                hipLaunchKernelGGL(k_redo<true>, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads),
+                                   size_t(b.max_slots) * sizeof(HuffLut) + kRedoLds, s, b);
+            else if (b.nsub)
+                hipLaunchKernelGGL(k_redo<false>, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
             break;
         case 6:
             if (!b.nseg) break;
             hipLaunchKernelGGL(k_chain, dim3((b.nseg + 3) / 4), dim3(256), 0, s, b);
             if (b.nchain && b.big_chain)
-                hipLaunchKernelGGL(k_chain_big, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
+                hipLaunchKernelGGL(k_chain_big, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads),
+                                   size_t(b.max_slots) * sizeof(HuffLut) + kRedoLds, s, b);
             else if (b.nchain)
                 hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
             break;

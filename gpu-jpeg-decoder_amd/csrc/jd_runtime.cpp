@@ -902,7 +902,9 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
                         !ctx->fixed_pieces) ? piece_lanes_resident(huffman_lds_bytes(P.max_slots)) : 0u;
         b.no_pool = ctx->spare_pieces == 0 ? 1u : 0u;
         b.small_fold = (b.piece_plan == 0 && P.total_chunks > 0 && nimg <= kSmallFoldImages) ? 1u : 0u;
-        {  // an interval holds at most its image's ECS bits, in pieces of at least P.piece_bits
+        if (!b.piece_plan) {  // small batches only (a large batch keeps k_chain_fix and its small footprint
+                              // beside the other batch's kernels): an interval holds at most its image's
+                              // ECS bits, in pieces of at least P.piece_bits
             uint64_t most = 0;
             for (const ImgDesc& d : P.imgs) most = std::max<uint64_t>(most, (uint64_t(d.len - d.ecs_off) * 8 + P.piece_bits - 1) / P.piece_bits);
             b.big_chain = most > kBigInterval ? 1u : 0u;

@@ -148,7 +148,7 @@ def test_big_interval_rounds_vs_oracle(monkeypatch, overlap, spare):
     try:
         out = dec.decode(data)
         nsub = int((dec.debug_fetch("sub_seg") != 0xFFFFFFFF).sum())
-        assert nsub > 4096  # one interval beyond kBigInterval pieces
+        assert nsub > 4096  # one interval of thousands of pieces (kBigInterval = 256)
         assert np.array_equal(out, ref)
     finally:
         dec.close()
