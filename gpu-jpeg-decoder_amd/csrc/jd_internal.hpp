@@ -298,6 +298,10 @@ struct BatchDev {
     uint32_t* ts_cursor;          // next free piece slot of each table set's range: k_subplan packs the
                                   // pieces of the batch's images densely from its start (whole waves
                                   // of the range's tail stay unused and exit at once)
+    const uint32_t* img_order;    // images in table-set order (the host's piece-slot ranges)
+    uint32_t* img_cand;           // k_index (large batches): pieces of each image at k_pieceplan's 16
+                                  // candidate piece sizes
+    uint32_t* img_base;           // k_pieceplan: first piece slot of each image
     uint32_t max_slots;           // LUT slots staged per workgroup
     uint32_t piece_bits, piece_overlap;
     uint32_t piece_plan;          // k_pieceplan: resident piece lanes (0: use piece_bits as is)

@@ -254,6 +254,34 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
 //   seg_cend[k]          = interval k's data ends at the first fill byte / marker after it
 // The first terminating marker ends the ECS; breaks after it are ignored.
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, uint32_t(__shfl_xor(int(x), o, 64)));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += uint32_t(__shfl_xor(int(x), o, 64));
+    return x;
+}
+
+// Piece-size candidates of a large batch (k_pieceplan): P = piece_bits * (8 + c) / 8, c < kPlanCands.
+constexpr int kPlanCands = 16;
+__device__ __forceinline__ uint32_t plan_cand(uint32_t piece_bits, int c) { return piece_bits * uint32_t(8 + c) / 8u; }
+// Pieces of an interval of `bits` bits at piece size p: ceil(bits / p), at least 1 (k_subplan's count).
+__device__ __forceinline__ uint32_t pieces_of(uint32_t bits, uint32_t p) {
+    const uint32_t q = bits / p;
+    return max(1u, q + (q * p != bits ? 1u : 0u));
+}
+// The same from a float reciprocal of p: the estimate is within one of bits / p (q < 2^23), then
+// corrected exactly.
+__device__ __forceinline__ uint32_t pieces_of_rcp(uint32_t bits, uint32_t p, float inv) {
+    int64_t q = int64_t(float(bits) * inv);
+    const int64_t r = int64_t(bits) - q * int64_t(p);
+    q += r < 0 ? -1 : (r >= int64_t(p) ? 1 : 0);
+    return max(1u, uint32_t(q) + (uint64_t(q) * p != bits ? 1u : 0u));
+}
+
 __device__ __forceinline__ uint32_t fill_before(uintptr_t file, uint32_t lo, uint32_t pos) {
     uint32_t n = 0;
     while (pos > lo + n && *reinterpret_cast<gu8*>(file + pos - 1 - n) == 0xFFu) n++;
@@ -338,6 +366,27 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
         b.seg_cend[sb + k] = end_all;
     }
     if (__any(order_bad) && lane == 0) atomicOr(&b.status[ii], kStRstOrder);
+    if (!b.piece_plan) return;
+    // large batches: the image's pieces at each of k_pieceplan's candidate piece sizes (exact, as
+    // k_subplan will count them), so that k_pieceplan only sums per image and k_subplan needs no
+    // allocation atomic (1 024 images on one table set's cursor took ~60 us, serialised)
+    // this wave's seg_cstart / seg_cend stores are read back by other lanes of the wave: wait until
+    // the L2 has them (vmcnt(0); __threadfence's L2 write-back cost ~20 us here) and read past the L1
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    // lane = candidate c (lane & 15) over every 4th interval (lane >> 4): few registers, so that
+    // k_index still fits beside a walk (64 VGPRs per SIMD left)
+    const uint32_t p = plan_cand(b.piece_bits, lane & 15);
+    const float inv = 1.0f / float(p);
+    uint32_t cnt = 0;
+#pragma unroll 4
+    for (uint32_t k = uint32_t(lane) >> 4; k < nseg; k += 4) {
+        const uint32_t cs = __hip_atomic_load(b.seg_cstart + sb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t ce = max(cs, __hip_atomic_load(b.seg_cend + sb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        cnt += pieces_of_rcp((ce - cs) * 8, p, inv);
+    }
+    cnt += uint32_t(__shfl_xor(int(cnt), 16, 64));
+    cnt += uint32_t(__shfl_xor(int(cnt), 32, 64));
+    if (lane < kPlanCands) b.img_cand[size_t(ii) * kPlanCands + lane] = cnt;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -596,68 +645,120 @@ __device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts
     }
 }
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = max(x, uint32_t(__shfl_xor(int(x), o, 64)));
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += uint32_t(__shfl_xor(int(x), o, 64));
-    return x;
-}
-
-// Piece size of a large batch (one workgroup, before k_subplan): every interval of b bits is cut
-// into ceil(b / P) pieces, a lane each, and a lane walks about P + overlap bits; k_piece keeps
-// piece_plan lanes resident.  The candidates P = piece_bits * (8 + c) / 8 are scored by
+// Piece size of a large batch (one workgroup, after k_index, before k_subplan): every interval of b
+// bits is cut into ceil(b / P) pieces, a lane each, and a lane walks about P + overlap bits; k_piece
+// keeps piece_plan lanes resident.  The candidates P = plan_cand(piece_bits, c) are scored by
 // ceil(pieces / resident) x (P + overlap) -- a partial last round of lanes takes as long as a full
-// one -- and the cheapest (the smallest P on ties) is written to counters[3] (pieces << 32 | P) for
-// k_subplan.  Counts use a float reciprocal: an estimate (k_subplan divides exactly).
-constexpr int kPlanCands = 16;
+// one -- and the cheapest (the smallest P on ties) is written to counters[3] (pieces << 32 | P).
+// The pieces per image and candidate come from k_index (img_cand, exact).  Then each image's first
+// piece slot (img_base): its table set's range start plus the pieces of the images before it in
+// the host's table-set order (img_order), so the batch's pieces are dense from each range's start
+// without an allocation atomic in k_subplan.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x = max(x, y);
+    }
+    return x;
+}
 __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
     JD_PRIO_SHORT();
     __shared__ unsigned long long s_cnt[kPlanCands];
+    __shared__ uint32_t s_ws[16], s_wm[16], s_choice;
     const uint32_t t = threadIdx.x;
+    const int lane = int(t & 63u), wv = int(t >> 6);
     if (t < kPlanCands) s_cnt[t] = 0;
     __syncthreads();
-    float inv[kPlanCands];
-#pragma unroll
-    for (int c = 0; c < kPlanCands; c++) inv[c] = 8.0f / float(b.piece_bits * uint32_t(8 + c));
     uint32_t cnt[kPlanCands] = {};
-    for (uint32_t s = t; s < b.nseg; s += blockDim.x) {
-        const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
-        const float bits = float((ce - cs) * 8u);
+    for (uint32_t img = t; img < b.nimg; img += 1024) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(b.img_cand + size_t(img) * kPlanCands);
 #pragma unroll
-        for (int c = 0; c < kPlanCands; c++) cnt[c] += max(1u, uint32_t(ceilf(bits * inv[c])));
+        for (int q = 0; q < kPlanCands / 4; q++) {
+            const u32x4 v = src[q];
+            cnt[4 * q] += v.x;
+            cnt[4 * q + 1] += v.y;
+            cnt[4 * q + 2] += v.z;
+            cnt[4 * q + 3] += v.w;
+        }
     }
 #pragma unroll
     for (int c = 0; c < kPlanCands; c++) {
         const uint32_t w = wave_sum_u32(cnt[c]);
-        if ((t & 63u) == 0) atomicAdd(&s_cnt[c], (unsigned long long)w);
+        if (lane == 0) atomicAdd(&s_cnt[c], (unsigned long long)w);
     }
     __syncthreads();
     if (t == 0) {
         double best = 1e300;
-        uint32_t pb = b.piece_bits;
+        uint32_t pb = b.piece_bits, bc = 0;
         unsigned long long np = s_cnt[0];
         for (int c = 0; c < kPlanCands; c++) {
-            const uint32_t p = b.piece_bits * uint32_t(8 + c) / 8u;
+            const uint32_t p = plan_cand(b.piece_bits, c);
             const double rounds = double((s_cnt[c] + b.piece_plan - 1) / b.piece_plan);
             const double cost = rounds * double(p + b.piece_overlap);
             if (cost < best) {
                 best = cost;
                 pb = p;
+                bc = uint32_t(c);
                 np = s_cnt[c];
             }
         }
         b.counters[3] = (np << 32) | pb;
+        s_choice = bc;
+    }
+    __syncthreads();
+    const uint32_t c = s_choice;
+    uint32_t run = 0, mrun = 0;
+    for (uint32_t i0 = 0; i0 < b.nimg; i0 += 1024) {
+        const uint32_t i = i0 + t;
+        const bool v = i < b.nimg;
+        uint32_t img = 0, ts = 0, used = 0;
+        bool first = false;
+        if (v) {
+            img = b.img_order[i];
+            const ImgDesc& im = b.imgs[img];
+            ts = im.tableset;
+            used = min(b.img_cand[size_t(img) * kPlanCands + c], im.sub_cap);
+            first = i == 0 || b.imgs[b.img_order[i - 1]].tableset != ts;
+        }
+        // exclusive sum of the pieces over the order
+        const uint32_t incl = uint32_t(wave_scan_dpp(int(used)));
+        if (lane == 63) s_ws[wv] = incl;
+        __syncthreads();
+        uint32_t excl = run + incl - used, tot = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            if (j < wv) excl += s_ws[j];
+            tot += s_ws[j];
+        }
+        // the sum at the first image of this image's table set: an inclusive max over the order of
+        // (first ? sum : 0), the sums never decreasing
+        const uint32_t mk = wave_incl_max(first ? excl : 0u);
+        if (lane == 63) s_wm[wv] = mk;
+        __syncthreads();
+        uint32_t m = max(mrun, mk), mt = mrun;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            if (j < wv) m = max(m, s_wm[j]);
+            mt = max(mt, s_wm[j]);
+        }
+        if (v) b.img_base[img] = b.ts_cursor[ts] + (excl - m);
+        run += tot;
+        mrun = mt;
+        __syncthreads();  // (s_ws / s_wm are rewritten by the next round)
     }
 }
 
 // Per image (one wave): pieces of every interval, interval -> piece map, and each interval's
 // first region word: piece j of an interval of n pieces owns region_words(plen) words from
 // seg_ent + j * region_words(plen).  The image's spare words after them (img_pool) are handed
-// out to re-walks (k_redo, k_chain_fix).
+// out to re-walks (k_redo, k_chain_fix).  The image's slots are the next ones of its table set's
+// range (every image's share fits: the range holds the sum of their caps), so the batch's pieces
+// are dense from the range's start: k_pieceplan's img_base in a large batch, else an atomic on the
+// table set's cursor.  One pass over the intervals, 64 at a time; the interval -> piece map of
+// each 64 is written from registers (an earlier form re-read every interval's base and count
+// after a fence: two dependent loads per interval, ~60 us per C2 batch with the atomic).
 // (small batches: run by the first k_compact workgroup of each image, beside its compaction, which
 // saves a launch on a small batch's critical path; in a large batch the per-image waves lengthen
 // k_compact's tail by more than the launch costs: 0.24 -> 0.48 ms on C2, so k_subplan runs as a
@@ -665,44 +766,53 @@ __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
 __device__ void subplan_image(const BatchDev& b, uint32_t img, int lane) {
     const ImgDesc& im = b.imgs[img];
     const uint32_t piece_bits = b.piece_plan ? uint32_t(b.counters[3] & 0xFFFFFFFFull) : b.piece_bits;
+    uint32_t base;
+    if (b.piece_plan) {
+        base = b.img_base[img];
+    } else {
+        uint32_t n = 0;
+        for (uint32_t k = uint32_t(lane); k < im.nseg; k += 64) {
+            const uint32_t s = im.seg_base + k;
+            const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
+            n += pieces_of((ce - cs) * 8, piece_bits);
+        }
+        // run <= sub_cap by construction (host bound: ceil(ECS bits / piece_bits) + nseg pieces)
+        const uint32_t used = min(wave_sum_u32(n), im.sub_cap);
+        uint32_t bs = 0;
+        if (lane == 0) bs = atomicAdd(&b.ts_cursor[im.tableset], used);
+        base = uint32_t(__shfl(int(bs), 0, 64));
+    }
     uint32_t run = 0, wrun = 0;
     for (uint32_t k0 = 0; k0 < im.nseg; k0 += 64) {
-        const uint32_t k = k0 + lane;
+        const uint32_t k = k0 + uint32_t(lane);
         uint32_t n = 0, w = 0;
         if (k < im.nseg) {
             const uint32_t s = im.seg_base + k;
             const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
             const uint32_t bits = (ce - cs) * 8;
-            n = max(1u, uint32_t((uint64_t(bits) + piece_bits - 1) / piece_bits));
+            n = pieces_of(bits, piece_bits);
             w = n * region_words((bits + n - 1u) / n, im.rw_div);
         }
         const uint32_t incl = wave_incl_scan(n), wincl = wave_incl_scan(w);
+        const uint32_t off = run + incl - n;
         if (k < im.nseg) {
             const uint32_t s = im.seg_base + k;
-            b.seg_sub_base[s] = run + incl - n;  // image-relative until the image's slots are allocated
+            b.seg_sub_base[s] = base + off;
             b.seg_nsub[s] = n;
             b.seg_ent[s] = wrun + wincl - w;
         }
-        run += __shfl(int(incl), 63, 64);
-        wrun += __shfl(int(wincl), 63, 64);
+        // (wrun <= entry_cap by construction: ECS bits / rw_div + kRegionSlack + 4 words per piece)
+        const uint32_t m = min(64u, im.nseg - k0);
+        for (uint32_t j = 0; j < m; j++) {
+            const uint32_t oj = uint32_t(__builtin_amdgcn_readlane(int(off), int(j)));
+            const uint32_t nj = uint32_t(__builtin_amdgcn_readlane(int(n), int(j)));
+            for (uint32_t u = uint32_t(lane); u < nj; u += 64)
+                if (oj + u < im.sub_cap) b.sub_seg[base + oj + u] = im.seg_base + k0 + j;
+        }
+        run += uint32_t(__shfl(int(incl), 63, 64));
+        wrun += uint32_t(__shfl(int(wincl), 63, 64));
     }
-    // run <= sub_cap and wrun <= entry_cap by construction (host bounds: ceil(ECS bits /
-    // piece_bits) + nseg pieces, ECS bits / rw_div + kRegionSlack + 4 words per piece)
     if (lane == 0) b.img_pool[img] = wrun;
-    const uint32_t used = min(run, im.sub_cap);
-    // the image's slots: the next `used` of its table set's range (every image's share fits: the
-    // range holds the sum of their caps), so the batch's pieces are dense from the range's start
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&b.ts_cursor[im.tableset], used);
-    base = uint32_t(__shfl(int(base), 0, 64));
-    __threadfence();  // this wave's seg_sub_base / seg_nsub stores before the loads below
-    for (uint32_t k = 0; k < im.nseg; k++) {
-        const uint32_t s = im.seg_base + k;
-        const uint32_t off = b.seg_sub_base[s], n = b.seg_nsub[s];
-        if (lane == 0) b.seg_sub_base[s] = base + off;
-        for (uint32_t u = lane; u < n; u += 64)
-            if (off + u < used) b.sub_seg[base + off + u] = s;
-    }
 }
 __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     JD_PRIO_SHORT();
@@ -3753,22 +3863,20 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     }
     switch (k) {
         case 0:
+            if (b.nsub) {  // (k_subplan / k_compact's subplan fill it) every slot not claimed by an
+                           // interval (per-image slack, padding) must read invalid; here, at the
+                           // front-end's start, the fill runs beside the other batch's kernels
+                const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
+                if (e != hipSuccess) return e;
+            }
             if (b.max_chunks) hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
             break;
         case 1: hipLaunchKernelGGL(k_index, dim3(b.nimg), dim3(64), 0, s, b); break;
         case 2:
-            if (b.small_fold && b.nsub) {  // (before k_compact, which runs the subplan) every slot not
-                                           // claimed by an interval (per-image slack, padding) reads invalid
-                const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
-                if (e != hipSuccess) return e;
-            }
             if (b.max_chunks) hipLaunchKernelGGL(k_compact, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
             break;
         case 3: {
             if (!b.nsub || b.small_fold) break;
-            // every slot not claimed by an interval (per-image slack, padding) must read invalid
-            const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
-            if (e != hipSuccess) return e;
             if (b.piece_plan) hipLaunchKernelGGL(k_pieceplan, dim3(1), dim3(1024), 0, s, b);
             hipLaunchKernelGGL(k_subplan, dim3(b.nimg), dim3(64), 0, s, b);
             break;

@@ -362,6 +362,7 @@ struct Plan {
     std::vector<uint16_t> qtabs;
     std::vector<uint32_t> seg_img, wg_tableset;
     std::vector<uint32_t> ts_slot0;  // first piece slot of each table set's range (k_subplan allocates from it)
+    std::vector<uint32_t> img_order;  // images in table-set order (k_pieceplan's dense allocation)
     uint32_t piece_bits = kPieceBits, piece_overlap = kPieceOverlap;
     std::vector<uint32_t> chain_seg, chain_wg_tableset;  // k_chain lanes, grouped by table set
     uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0;
@@ -570,6 +571,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     uint64_t sub = 0, entry_cursor = 0;
     P.chain_seg.reserve(seg_cursor + kPieceThreads * P.tablesets.size());
     P.ts_slot0.assign(P.tablesets.size(), 0u);
+    P.img_order = order;
     for (size_t oi = 0; oi < order.size();) {
         const int ts = pim[order[oi]].ts;
         P.ts_slot0[ts] = uint32_t(sub);
@@ -841,6 +843,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
         const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // entries, slow tiles, IDCT queue
         const size_t o_tscur = put(blob, P.ts_slot0);
+        const size_t o_order = put(blob, P.img_order);
         const size_t upload = blob.size();
         // device-written scratch after the uploaded part (no initialisation needed)
         size_t end = upload;
@@ -854,6 +857,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_subseg = reserve(end, nsub * 4);
         const size_t o_segent = reserve(end, nseg * 4);
         const size_t o_pool = reserve(end, size_t(nimg) * 4);
+        const size_t o_cand = reserve(end, size_t(nimg) * 16 * 4);
+        const size_t o_ibase = reserve(end, size_t(nimg) * 4);
         size_t o_piece[9];
         for (int q = 0; q < 9; q++) o_piece[q] = reserve(end, nsub * 4);
         const size_t o_cp = reserve(end, nsub * kCpRecords * sizeof(CpRec));
@@ -892,6 +897,9 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.nsub = uint32_t(nsub);
         b.wg_tableset = reinterpret_cast<const uint32_t*>(base + o_wgts);
         b.ts_cursor = reinterpret_cast<uint32_t*>(base + o_tscur);
+        b.img_order = reinterpret_cast<const uint32_t*>(base + o_order);
+        b.img_cand = reinterpret_cast<uint32_t*>(base + o_cand);
+        b.img_base = reinterpret_cast<uint32_t*>(base + o_ibase);
         b.chain_seg = reinterpret_cast<const uint32_t*>(base + o_chain);
         b.nchain = uint32_t(P.chain_seg.size());
         b.chain_wg_tableset = reinterpret_cast<const uint32_t*>(base + o_chts);
