@@ -125,6 +125,12 @@ __device__ __forceinline__ void load64(uintptr_t t0, uintptr_t fend, uint32_t (&
     }
 }
 
+// load64 again, as a fresh load (k_scan's edge threads: the count pass's words are not kept alive)
+__device__ __forceinline__ void reload64(uintptr_t t0, uintptr_t fend, uint32_t (&w)[16]) {
+    asm("" : "+v"(t0));
+    load64(t0, fend, w);
+}
+
 // ------------------------------------------------------------------------------------------
 // Stage 0: scan.  In an ECS a data FF is always followed by a stuffed 00, so:
 //   FF 00      -> the 00 is dropped by un-stuffing (the reference's loop, parser.cpp:84-96)
@@ -161,11 +167,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     uint32_t ndrop = 0, nbrk = 0;
     const bool interior = t0 >= lo && t0 + 64 < fend;
     // interior thread: exact per-byte masks (high bit of each byte lane), one word at a time with
-    // the neighbours' masks carried, kept per word for the break walk below
+    // the neighbours' masks carried
     //   drop : 00 preceded by FF       brk : FF followed by neither 00 nor FF
-    // (computed in every thread, so that the masks need no zero-initialised copy for the edge
-    // threads, which count byte by byte below instead)
-    uint32_t dmq[16], bmq[16];
+    // Only which words hold a break (brkw) and the stuffed zeros before each word (cum, a byte per
+    // word) are kept for the break walk below, which recomputes the masks of those words alone:
+    // keeping both masks of all 16 words took 84 VGPRs, so only one workgroup per CU fitted beside
+    // k_idct_color (112 VGPRs per SIMD left), and the next batch's scan ran one chunk per CU at a time
+    // (computed in every thread, so that nothing needs a zero-initialised copy for the edge threads,
+    // which count byte by byte below instead)
+    uint32_t brkw = 0, cum[4];
     {
         uint32_t ff_prev = (prevb == 0xFFu) ? 0x80000000u : 0u;  // only its top byte is used
         uint32_t ff_cur, nz_cur;
@@ -175,10 +185,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
         for (int q = 0; q < 16; q++) {
             uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = 0;
             if (q < 15) zero_nx = scan_masks(w[q + 1], ff_nx, nz_nx);
-            dmq[q] = zero_cur & __builtin_amdgcn_alignbit(ff_cur, ff_prev, 24);  // (ff_cur << 8) | (ff_prev >> 24)
-            bmq[q] = ff_cur & __builtin_amdgcn_alignbit(nz_nx, nz_cur, 8);     // (nz_cur >> 8) | (nz_nx << 24)
-            ndrop += __builtin_popcount(dmq[q]);
-            nbrk += __builtin_popcount(bmq[q]);
+            const uint32_t dm = zero_cur & __builtin_amdgcn_alignbit(ff_cur, ff_prev, 24);  // (ff_cur << 8) | (ff_prev >> 24)
+            const uint32_t bm = ff_cur & __builtin_amdgcn_alignbit(nz_nx, nz_cur, 8);     // (nz_cur >> 8) | (nz_nx << 24)
+            cum[q >> 2] = (q & 3) ? (cum[q >> 2] | (ndrop << (8 * (q & 3)))) : ndrop;
+            ndrop += __builtin_popcount(dm);
+            nbrk += __builtin_popcount(bm);
+            brkw |= min(bm, 1u) << q;
+            // (brkw and cum built here: left to itself the compiler sinks them past the block scan and
+            // keeps every word's break mask and drop prefix alive until then: 71 VGPRs)
+            asm volatile("" : "+v"(brkw), "+v"(cum[q >> 2]));
             ff_prev = ff_cur;
             ff_cur = ff_nx;
             nz_cur = nz_nx;
@@ -187,6 +202,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     }
     if (!interior) {
         ndrop = nbrk = 0;
+        reload64(t0, fend, w);
 #pragma unroll 1
         for (int i = 0; i < 64; i++) {
             const uint32_t by = byte_of(w, i);
@@ -202,31 +218,41 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     const uint32_t drop_before = block_excl_scan(ndrop, s_wsum[0], &tot_drop);
     uint32_t off = block_excl_scan(nbrk, s_wsum[1], &tot_brk);
     if (nbrk && interior) {
-        // walk the break bits only (a wave with a break used to run a 64-byte loop): per word the
-        // masks kept from the count above, one iteration per break in it; a word without a break
-        // in any lane of the wave costs two instructions
+        // walk the break bits only, in the words that hold one (a word without a break in any lane
+        // of the wave costs two instructions); their masks recomputed as in the count pass
         Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
-        uint32_t d = drop_before;
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            const uint32_t dm = dmq[q];
-            uint32_t bm = bmq[q];
-            if (__any(bm != 0u)) {
+            if (__any((brkw >> q) & 1u)) {
+                // (the words loaded again: the L1 / L2 still hold them, and keeping the count pass's
+                // words or masks alive for this is what the recomputation is to avoid)
+                uintptr_t aq = t0 + 4u * q;
+                asm("" : "+v"(aq));  // (a fresh load, not the count pass's value kept alive)
+                const uint32_t wc = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(aq);
+                const uint32_t wp = q > 0 ? *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(aq - 4) : 0u;
+                const uint32_t wn = q < 15 ? *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(aq + 4) : 0u;
+                uint32_t ff, nz, ffp = (prevb == 0xFFu) ? 0x80000000u : 0u, nzp, ffn, nzn = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;
+                const uint32_t zero = scan_masks(wc, ff, nz);
+                if (q > 0) (void)scan_masks(wp, ffp, nzp);
+                if (q < 15) (void)scan_masks(wn, ffn, nzn);
+                const uint32_t dm = zero & __builtin_amdgcn_alignbit(ff, ffp, 24);
+                uint32_t bm = ff & __builtin_amdgcn_alignbit(nzn, nz, 8);
+                const uint32_t d = drop_before + ((cum[q >> 2] >> (8 * (q & 3))) & 0xFFu);
                 while (bm) {
                     const uint32_t bit = __builtin_ctz(bm);  // 7, 15, 23 or 31: byte k = bit >> 3
                     const uint32_t k = bit >> 3;
-                    const uint32_t nbv = k < 3u ? (w[q] >> (8u * (k + 1u))) & 0xFFu : (q < 15 ? w[q < 15 ? q + 1 : q] & 0xFFu : nextb);
+                    const uint32_t nbv = k < 3u ? (wc >> (8u * (k + 1u))) & 0xFFu : (q < 15 ? wn & 0xFFu : nextb);
                     const uint32_t dd = d + __builtin_popcount(dm & ((1u << bit) - 1u));
                     const uint32_t is_term = (nbv & 0xF8u) == 0xD0u ? 0u : 1u;
                     out[off++] = Break{uint32_t(t0 + 4u * q + k - file), (dd << 1) | is_term};
                     bm &= bm - 1u;
                 }
             }
-            d += __builtin_popcount(dm);
         }
     } else if (nbrk) {  // edge threads: byte by byte
         Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
         uint32_t d = drop_before;
+        reload64(t0, fend, w);
 #pragma unroll 1
         for (int i = 0; i < 64; i++) {
             const uint32_t by = byte_of(w, i);
