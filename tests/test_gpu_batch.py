@@ -385,3 +385,39 @@ def test_full_baseline_batch_every_image_bit_exact(config):
         dout.free()
     finally:
         dec.close()
+
+
+def test_piece_plan_over_1024_images_and_many_table_sets():
+    """Round 5: in a large batch k_pieceplan hands out each image's first piece slot by a scan over
+    the images in the host's table-set order (no allocation atomics), and k_subplan writes each
+    image's interval -> piece map in one pass, 64 intervals at a time.  This batch takes that path
+    (path "full": the full-batch piece geometry) with more than 1 024 images (the scan's second
+    round), several hundred table sets interleaved in image order (every fourth image carries
+    Pillow's optimised per-image Huffman tables), images of more than 64 restart intervals (an
+    interval per MCU), and every image checked against the oracle.  Reference path replaced:
+    parallelHuffManDecode's per-image setup (cuda-decoder/src/parser.cu:132-208)."""
+    rng = np.random.default_rng(7)
+    datas = []
+    for i in range(1300):
+        w, h = int(rng.integers(40, 260)), int(rng.integers(24, 200))
+        px = jd_synth.synth_pixels(w, h, 900000 + i)
+        sub = ["4:2:0", "4:4:4", "4:2:2"][i % 3]
+        q = int(rng.integers(50, 96))
+        if i % 4 == 1:
+            datas.append(jd_synth.encode(px, q, sub, restart_rows=int(rng.integers(0, 3)), optimize=True))
+        elif i % 7 == 3:
+            datas.append(jd_synth.encode(px, q, sub, restart_blocks=1))
+        else:
+            datas.append(jd_synth.encode(px, q, sub, restart_rows=int(rng.integers(0, 3))))
+    hdrs0 = [jdamd.parse(d) for d in datas]
+    assert max(-(-h.mcux * h.mcuy // h.restart_interval) if h.restart_interval else 1 for h in hdrs0) > 64
+    dec = jdamd.Decoder(0, path="full")
+    try:
+        hosts, hdrs, din, dout, offs, ooffs = _device_batch(dec, datas)
+        status = dec.decode_batch_device(hosts, [din.ptr + o for o in offs], [dout.ptr + o for o in ooffs])
+        assert status == [0] * len(datas)
+        _every_image_vs_oracle(dec, datas, hosts, hdrs, dout, ooffs, chunk=256)
+        din.free()
+        dout.free()
+    finally:
+        dec.close()
