@@ -377,8 +377,10 @@ struct Plan {
 // the pool, 4 B per word; estimated at full-size pieces) and that holds at most max_batch_images
 // items (default kMaxBatchImages: the per-image kernels index images by the grid's y dimension,
 // at most 65535).  JD_MAX_BATCH_ENTRIES / JD_MAX_BATCH_IMAGES override them (tests force
-// multi-way splits).
-constexpr uint64_t kMaxBatchEntries = 8ull << 30;
+// multi-way splits).  12 G words (48 GB of entry pool per slot, two slots: a third of the 288 GB):
+// the reference's own 3000-image batch (ref444, ~9 G words reserved) runs as one launch (at 8 G it
+// was split in two, and the pipelined rate fell below the kernel-only one).
+constexpr uint64_t kMaxBatchEntries = 12ull << 30;
 constexpr int kMaxBatchImages = 65535;
 int batch_split(jd_ctx* ctx, int lo, int n, const jd_item* items) {
     const uint64_t limit = ctx->max_batch_entries;
