@@ -156,13 +156,18 @@ struct BlockInfo {
     uint32_t cnt_dc;
 };
 
-// A break in the raw ECS found by the scan: FF followed by RSTn, or a terminating marker.
-//   pos  : byte position in the file
-//   info : (stuffed zero bytes in [chunk start, pos) << 1) | is_terminator
+// A break in the raw ECS found by the scan: FF followed by RSTn, or a terminating marker.  One word
+// (a 16 KiB chunk can hold 8 192 of them: the pool is kScanCap words per chunk, twice the ECS):
+//   bits 0..13   byte offset of the FF in its scan chunk
+//   bits 14..27  stuffed zero bytes in [chunk start, FF) (<= 8 192)
+//   bit  31      terminating marker
 struct Break {
-    uint32_t pos;
-    uint32_t info;
+    uint32_t w;
 };
+JD_HD inline Break brk_make(uint32_t rel, uint32_t drops, uint32_t term) { return Break{rel | (drops << 14) | (term << 31)}; }
+JD_HD inline uint32_t brk_rel(Break k) { return k.w & 0x3FFFu; }
+JD_HD inline uint32_t brk_drops(Break k) { return (k.w >> 14) & 0x3FFFu; }
+JD_HD inline bool brk_term(Break k) { return (k.w >> 31) != 0u; }
 
 constexpr uint32_t kInvalidImage = 0xFFFFFFFFu;
 
@@ -203,6 +208,7 @@ constexpr int kScanThreads = 256;
 constexpr int kScanBytesPerThread = 64;
 constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
 constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cannot hold more
+static_assert(kScanChunk <= 16384, "Break: 14-bit chunk offsets and drop counts");
 
 #ifndef JD_CP_MAX
 #define JD_CP_MAX 8

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
                     const uint32_t nbv = k < 3u ? (wc >> (8u * (k + 1u))) & 0xFFu : (q < 15 ? wn & 0xFFu : nextb);
                     const uint32_t dd = d + __builtin_popcount(dm & ((1u << bit) - 1u));
                     const uint32_t is_term = (nbv & 0xF8u) == 0xD0u ? 0u : 1u;
-                    out[off++] = Break{uint32_t(t0 + 4u * q + k - file), (dd << 1) | is_term};
+                    out[off++] = brk_make(threadIdx.x * uint32_t(kScanBytesPerThread) + 4u * q + k, dd, is_term);
                     bm &= bm - 1u;
                 }
             }
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
             d += (inr && a > lo && by == 0x00u && pb == 0xFFu) ? 1u : 0u;
             if (inr && a + 1 < fend && by == 0xFFu && nb != 0x00u && nb != 0xFFu) {
                 const uint32_t is_term = (nb & 0xF8u) == 0xD0u ? 0u : 1u;
-                out[off++] = Break{uint32_t(a - file), (d << 1) | is_term};
+                out[off++] = brk_make(threadIdx.x * uint32_t(kScanBytesPerThread) + uint32_t(i), d, is_term);
             }
         }
     }
@@ -332,8 +332,8 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
             const uint32_t n = b.chunk_nbrk[cb + c];
             const Break* br = b.chunk_brk + size_t(cb + c) * kScanCap;
             for (uint32_t j = 0; j < n; j++)
-                if (br[j].info & 1u) {
-                    term = min(term, br[j].pos);
+                if (brk_term(br[j])) {
+                    term = min(term, a0 + c * uint32_t(kScanChunk) + brk_rel(br[j]));
                     break;
                 }
         }
@@ -352,7 +352,8 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
         const uint32_t nbrk = vc ? b.chunk_nbrk[cb + c] : 0u;
         const Break* br = b.chunk_brk + size_t(cb + c) * kScanCap;
         uint32_t nmark = 0;
-        for (uint32_t j = 0; j < nbrk; j++) nmark += (!(br[j].info & 1u) && br[j].pos < term) ? 1u : 0u;
+        const uint32_t cpos0 = a0 + c * uint32_t(kScanChunk);  // file offset of the chunk's first byte
+        for (uint32_t j = 0; j < nbrk; j++) nmark += (!brk_term(br[j]) && cpos0 + brk_rel(br[j]) < term) ? 1u : 0u;
         const uint32_t di = wave_incl_scan(drops), mi = wave_incl_scan(nmark);
         const uint32_t dprefix = drops_run + di - drops, mprefix = marks_run + mi - nmark;
         if (vc) {
@@ -361,16 +362,17 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
             uint32_t m = mprefix;
             for (uint32_t j = 0; j < nbrk; j++) {
                 const Break k = br[j];
-                const uint32_t cpos = (k.pos - lo) - (dprefix + (k.info >> 1));
-                if (k.info & 1u) {
-                    if (k.pos == term) term_comp = cpos - fill_before(file, lo, k.pos);
+                const uint32_t kpos = cpos0 + brk_rel(k);  // file offset of the FF
+                const uint32_t cpos = (kpos - lo) - (dprefix + brk_drops(k));
+                if (brk_term(k)) {
+                    if (kpos == term) term_comp = cpos - fill_before(file, lo, kpos);
                     continue;
                 }
-                if (k.pos >= term) continue;
-                if (m < nseg) b.seg_cend[sb + m] = cpos - fill_before(file, lo, k.pos);
+                if (kpos >= term) continue;
+                if (m < nseg) b.seg_cend[sb + m] = cpos - fill_before(file, lo, kpos);
                 if (m + 1 < nseg) {
                     b.seg_cstart[sb + m + 1] = cpos + 2;
-                    if ((*reinterpret_cast<gu8*>(file + k.pos + 1) & 7u) != (m & 7u)) order_bad = true;
+                    if ((*reinterpret_cast<gu8*>(file + kpos + 1) & 7u) != (m & 7u)) order_bad = true;
                 }
                 m++;
             }
