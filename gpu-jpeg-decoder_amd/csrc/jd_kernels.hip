@@ -1873,45 +1873,90 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
                      s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords);
 }
 
-// chain_interval's counts for an interval whose starts all agree, in one pass of kFixPer pieces per
-// lane (k_chain_big): the piece whose MCUs reach the final interval's count (jl, the last that
-// matters) is found in the same pass that hands out the first MCUs.  Pieces before jl take what
-// they walked, jl the rest, the ones after it nothing; if no piece reaches the count, the interval
-// is short of MCUs (corrupt), as chain_interval decides with jl = n - 1.
-__device__ void chain_counts_onepass(const BatchDev& b, uint32_t s, uint32_t lane, uint32_t base, uint32_t n,
-                                     uint32_t nmcu_seg, bool final_seg) {
+// k_chain_big's workgroup: 8 waves on one interval at a time (16 would leave 128 VGPRs a lane and
+// spill).  One wave took 0.69 ms for the 68 K pieces of a single 2 000 x 2 000 4:4:4 q95 image:
+// every round and the counts pass walked its 67 chunks of 1 024 pieces one after the other.
+constexpr uint32_t kBigWaves = 8;
+constexpr uint32_t kBigThreads = 64 * kBigWaves;
+constexpr size_t kBigLds = size_t(kBigThreads) * (row_words(kWin) + kRingWords + kRecRingWords) * 4;
+
+// chain_interval's counts for an interval whose starts all agree (k_chain_big), its pieces cut into
+// one contiguous slice per wave: the slices' MCU sums, their prefix, the piece whose MCUs reach the
+// final interval's count (jl, the last that matters: found by the wave whose slice holds it), then
+// every wave hands out its slice's first MCUs from its prefix.  Pieces before jl take what they
+// walked, jl the rest, the ones after it nothing; if no piece reaches the count, the interval is
+// short of MCUs (corrupt), as chain_interval decides with jl = n - 1.
+__device__ void chain_counts_wg(const BatchDev& b, uint32_t s, uint32_t base, uint32_t n, uint32_t nmcu_seg,
+                                bool final_seg, uint32_t* s_sum, uint32_t* s_jl) {
     constexpr uint32_t kPer = kFixPer, kStep = 64 * kPer;
-    uint32_t jl = final_seg ? 0xFFFFFFFFu : n - 1u;  // wave-uniform
-    uint32_t mcu_run = 0;
-    bool bad = false;
-    for (uint32_t j0 = 0; j0 < n; j0 += kStep) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t sl = ((n + kBigWaves - 1) / kBigWaves + 63u) & ~63u;  // pieces per slice
+    const uint32_t lo = min(n, wv * sl), hi = min(n, lo + sl);
+    // the slice's MCUs
+    uint32_t sum = 0;
+    for (uint32_t j0 = lo; j0 < hi; j0 += kStep) {
         const uint32_t jb = j0 + kPer * lane;
-        uint32_t pm[kPer], em[kPer], c[kPer];
 #pragma unroll
-        for (uint32_t t = 0; t < kPer; t++) {
-            const bool in = jb + t < n;
-            pm[t] = in ? b.piece_nmcu[base + jb + t] : 0u;
-            em[t] = in ? b.piece_emcu[base + jb + t] : kNoError;
-        }
-        if (jl == 0xFFFFFFFFu) {  // wave-uniform: is the last piece that matters in this chunk?
+        for (uint32_t t = 0; t < kPer; t++) sum += jb + t < hi ? b.piece_nmcu[base + jb + t] : 0u;
+    }
+    sum = uint32_t(__builtin_amdgcn_readlane(wave_scan_dpp(int(sum)), 63));
+    if (lane == 0) s_sum[wv] = sum;
+    __syncthreads();
+    uint32_t pre = 0, wj = kBigWaves;  // MCUs before the slice; the slice holding jl
+    for (uint32_t v = 0, run = 0; v < kBigWaves; v++) {
+        if (v == wv) pre = run;
+        if (wj == kBigWaves && final_seg && run + s_sum[v] >= nmcu_seg) wj = v;
+        run += s_sum[v];
+    }
+    if (!final_seg) wj = (n - 1u) / sl;  // jl = n - 1
+    if (wv == wj && final_seg) {  // find jl in this slice (it is there: the slice reaches the count)
+        uint32_t run = pre, jl = 0xFFFFFFFFu;
+        for (uint32_t j0 = lo; j0 < hi && jl == 0xFFFFFFFFu; j0 += kStep) {
+            const uint32_t jb = j0 + kPer * lane;
+            uint32_t c[kPer];
 #pragma unroll
-            for (uint32_t t = 0; t < kPer; t++) c[t] = pm[t] + (t ? c[t - 1] : 0u);
-            const uint32_t before = mcu_run + uint32_t(wave_scan_dpp(int(c[kPer - 1]))) - c[kPer - 1];
+            for (uint32_t t = 0; t < kPer; t++) c[t] = (jb + t < hi ? b.piece_nmcu[base + jb + t] : 0u) + (t ? c[t - 1] : 0u);
+            const uint32_t before = run + uint32_t(wave_scan_dpp(int(c[kPer - 1]))) - c[kPer - 1];
             uint32_t tf = kPer;
 #pragma unroll
             for (int t = kPer - 1; t >= 0; t--)
-                if (jb + t < n && before + c[t] >= nmcu_seg) tf = uint32_t(t);
+                if (jb + t < hi && before + c[t] >= nmcu_seg) tf = uint32_t(t);
             const uint64_t hit = __ballot(tf < kPer);
-            if (hit) {
+            if (hit) {  // wave-uniform
                 const int L = __builtin_ctzll(hit);
-                jl = j0 + kPer * uint32_t(L) + uint32_t(__shfl(int(tf), L, 64));
+                const uint32_t t = uint32_t(__shfl(int(tf), L, 64));
+                jl = j0 + kPer * uint32_t(L) + t;
+                // MCUs of the pieces before jl: lane L's prefix through its piece t - 1
+                uint32_t cl = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < kPer; q++) cl = (q + 1 == t) ? c[q] : cl;  // inclusive through t - 1
+                const uint32_t run_jl = uint32_t(__shfl(int(before + (t ? cl : 0u)), L, 64));
+                if (lane == 0) {
+                    s_jl[0] = jl;
+                    s_jl[1] = run_jl;
+                }
             }
+            run = uint32_t(__shfl(int(before + c[kPer - 1]), 63, 64));
         }
-        uint32_t pin[kPer], ex[kPer], tot = 0;
+    }
+    if (threadIdx.x == 0 && (!final_seg || wj == kBigWaves)) {
+        s_jl[0] = final_seg ? 0xFFFFFFFFu : n - 1u;  // (final and never reached: every piece before jl)
+        s_jl[1] = 0u;
+    }
+    __syncthreads();
+    const uint32_t jl = s_jl[0];
+    // the MCUs before this slice that count: every piece before min(lo, jl)
+    uint32_t mcu_run = (jl == 0xFFFFFFFFu || lo <= jl) ? pre : s_jl[1];
+    bool bad = false;
+    for (uint32_t j0 = lo; j0 < hi; j0 += kStep) {
+        const uint32_t jb = j0 + kPer * lane;
+        uint32_t pm[kPer], em[kPer], pin[kPer], ex[kPer], tot = 0;
 #pragma unroll
         for (uint32_t t = 0; t < kPer; t++) {
-            const uint32_t j = jb + t;
-            pin[t] = (j < jl && j < n) ? pm[t] : 0u;  // (jl unknown: every piece of the chunk is before it)
+            const bool in = jb + t < hi;
+            pm[t] = in ? b.piece_nmcu[base + jb + t] : 0u;
+            em[t] = in ? b.piece_emcu[base + jb + t] : kNoError;
+            pin[t] = (in && jb + t < jl) ? pm[t] : 0u;
             ex[t] = tot;
             tot += pin[t];
         }
@@ -1919,7 +1964,7 @@ __device__ void chain_counts_onepass(const BatchDev& b, uint32_t s, uint32_t lan
 #pragma unroll
         for (uint32_t t = 0; t < kPer; t++) {
             const uint32_t j = jb + t;
-            if (j >= n) continue;
+            if (j >= hi) continue;
             const uint32_t m0 = before + ex[t];
             uint32_t take = 0;
             if (j <= jl) take = piece_take(pm[t], em[t], m0, nmcu_seg, j == jl, final_seg, bad);
@@ -1928,52 +1973,65 @@ __device__ void chain_counts_onepass(const BatchDev& b, uint32_t s, uint32_t lan
         }
         mcu_run = uint32_t(__shfl(int(before + tot), 63, 64));
     }
-    bad |= jl == 0xFFFFFFFFu;  // no piece reached the final interval's count
+    bad |= jl == 0xFFFFFFFFu && wv == 0;  // no piece reached the final interval's count
     if (__any(bad) && lane == 0) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
-    if (lane == 0) b.seg_fix[s] = 0u;
+    if (threadIdx.x == 0) b.seg_fix[s] = 0u;
 }
 
-__global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
+__global__ __launch_bounds__(kBigThreads) void k_chain_big(BatchDev b) {
     JD_PRIO_CRIT();
     // (small batches only: the table set is staged in LDS, as in k_piece -- the re-walks of each
     // round are serial chains of lookups, ~1 us each from global memory)
     extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];
+    __shared__ unsigned long long s_mask[2];  // [0] this round's dirty chunks (< 64), [1] the next round's
+    __shared__ uint32_t s_state;              // bit 0: dirty chunks >= 64, 1: next round's, 2: a start disagreed
+    __shared__ uint32_t s_sum[kBigWaves], s_jl[2];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
-    const uint32_t lane = threadIdx.x;
-    const uint32_t li = blockIdx.x * kRedoThreads + lane;
-    const uint32_t sl = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
-    uint64_t todo = __ballot(sl != kInvalidImage && b.seg_fix[sl] != 0u);
-    if (!todo) return;  // wave-uniform: the common case
-    const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
-    stage_luts(b, ts, s_lut, kRedoThreads);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    // the workgroup's 64 entries of the chain list (as k_chain_fix's 64-lane workgroups)
+    if (wv == 0) {
+        const uint32_t li = blockIdx.x * 64u + lane;
+        const uint32_t sl = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
+        const uint64_t t = __ballot(sl != kInvalidImage && b.seg_fix[sl] != 0u);
+        if (lane == 0) s_mask[0] = t;
+    }
+    __syncthreads();
+    uint64_t todo = s_mask[0];
+    if (!todo) return;  // workgroup-uniform: the common case
+    const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * 64u) / kPieceThreads]];
+    stage_luts(b, ts, s_lut, int(kBigThreads));
     __syncthreads();
     const uint32_t* const luts = reinterpret_cast<const uint32_t*>(s_lut);
-    uint32_t* const row = s_rows + lane * row_words(kWin);
-    uint32_t* const ring = s_rows + kRedoThreads * row_words(kWin) + lane * kRingWords;
-    uint32_t* const rring = s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + lane * kRecRingWords;
-    while (todo) {  // wave-uniform
+    uint32_t* const row = s_rows + tid * row_words(kWin);
+    uint32_t* const ring = s_rows + kBigThreads * row_words(kWin) + tid * kRingWords;
+    uint32_t* const rring = s_rows + kBigThreads * (row_words(kWin) + kRingWords) + tid * kRecRingWords;
+    constexpr uint32_t kStep = 64 * kFixPer;
+    while (todo) {  // workgroup-uniform
         const int L = __builtin_ctzll(todo);
         todo &= todo - 1u;
-        const uint32_t s = uint32_t(__shfl(int(sl), L, 64));
+        const uint32_t s = b.chain_seg[blockIdx.x * 64u + uint32_t(L)];
         SegInfo S;
         seg_info(b, s, S);
         uint32_t dcp, acp;
         table_slots(ts, S, dcp, acp);
         const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
+        // chunks of kStep pieces to (re)check: every chunk in the first round, then only those where
+        // the round before re-walked a piece, and the chunk after each (its first piece follows the
+        // re-walked chunk's last); chunk ci belongs to wave ci mod kBigWaves
+        __syncthreads();  // (the previous interval's last reads of s_mask / s_state)
+        if (tid == 0) {
+            s_mask[0] = ~0ull;
+            s_mask[1] = 0ull;
+            s_state = 1u;
+        }
+        __syncthreads();
         bool agreed = false;
-        // chunks of kRedoThreads * kFixPer pieces to (re)check: every chunk in the first round, then
-        // only those where the round before re-walked a piece, and the chunk after each (its first
-        // piece follows the re-walked chunk's last): bit ci for chunk ci < 64, hi for the rest
-        uint64_t dirty = ~0ull;
-        bool dirty_hi = true;
         for (uint32_t round = 0; round < kFixRounds && !agreed; round++) {
-            agreed = true;
-            uint64_t next = 0;
-            bool next_hi = false;
-            // kFixPer consecutive pieces per lane: their loads in flight together (45 K pieces: 44
-            // wave-iterations per round)
-            for (uint32_t j0 = 0, ci = 0; j0 < n; j0 += kRedoThreads * kFixPer, ci++) {
+            const uint64_t dirty = s_mask[0];
+            const bool dirty_hi = (s_state & 1u) != 0u;
+            bool bad_round = false;  // wave-uniform
+            for (uint32_t ci = wv, j0 = wv * kStep; j0 < n; ci += kBigWaves, j0 += kBigWaves * kStep) {
                 const bool look = ci < 64 ? (((dirty >> ci) & 1u) || (ci > 0 && ((dirty >> (ci - 1)) & 1u)))
                                           : (dirty_hi || (ci == 64 && (dirty >> 63)));
                 if (!look) continue;  // wave-uniform
@@ -1991,9 +2049,11 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
                 for (uint32_t t = 0; t < kFixPer; t++)
                     mis |= (jb + t > 0 && jb + t < n && starts[t] != ends[t]) ? (1u << t) : 0u;
                 if (!__any(mis != 0u)) continue;  // wave-uniform
-                agreed = false;
-                if (ci < 64) next |= 1ull << ci;
-                else next_hi = true;
+                bad_round = true;
+                if (lane == 0) {
+                    if (ci < 64) atomicOr(&s_mask[1], 1ull << ci);
+                    else atomicOr(&s_state, 2u);
+                }
 #pragma unroll
                 for (uint32_t t = 0; t < kFixPer; t++) {
                     const bool need = (mis >> t) & 1u;
@@ -2004,13 +2064,21 @@ __global__ __launch_bounds__(kRedoThreads) void k_chain_big(BatchDev b) {
                     redo_piece<false>(b, S, P, s, u, ends[t], luts, dcp, acp, row, ring, rring, need);
                 }
             }
+            if (bad_round && lane == 0) atomicOr(&s_state, 4u);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this round's ends before the next reads
-            dirty = next;
-            dirty_hi = next_hi;
+            __syncthreads();
+            agreed = (s_state & 4u) == 0u;
+            __syncthreads();
+            if (tid == 0) {
+                s_mask[0] = s_mask[1];
+                s_mask[1] = 0ull;
+                s_state = (s_state >> 1) & 1u;
+            }
+            __syncthreads();
         }
-        if (agreed) {  // the counts, wave-parallel, in one pass
-            chain_counts_onepass(b, s, lane, base, n, S.nblk / S.bpm, seg_is_final(b, s));
-        } else if (lane == 0) {
+        if (agreed) {  // the counts, all waves
+            chain_counts_wg(b, s, base, n, S.nblk / S.bpm, seg_is_final(b, s), s_sum, s_jl);
+        } else if (tid == 0) {
             chain_fix_serial<false>(b, s, S, luts, dcp, acp, row, ring, rring);
         }
     }
@@ -3882,6 +3950,21 @@ static hipError_t allow_lds(size_t lds) {
     return hipSuccess;
 }
 
+// The same for k_chain_big's 16-wave workgroups (their lanes' rows and rings beside the tables).
+static hipError_t allow_lds_big(size_t lds) {
+    constexpr int kMaxDev = 64;
+    static std::mutex m;
+    static size_t allowed[kMaxDev] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+    std::lock_guard<std::mutex> l(m);
+    if (lds <= std::max<size_t>(65536, allowed[dev])) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chain_big),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (e == hipSuccess) allowed[dev] = lds;
+    return e;
+}
+
 hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     if (!b.nimg) return hipSuccess;
     const size_t lds = piece_lds_bytes(b.max_slots, kPieceThreads);
@@ -3925,9 +4008,12 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
         case 6:
             if (!b.nseg) break;
             hipLaunchKernelGGL(k_chain, dim3((b.nseg + 3) / 4), dim3(256), 0, s, b);
-            if (b.nchain && b.big_chain)
-                hipLaunchKernelGGL(k_chain_big, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads),
-                                   size_t(b.max_slots) * sizeof(HuffLut) + kRedoLds, s, b);
+            if (b.nchain && b.big_chain) {
+                const size_t lds_big = size_t(b.max_slots) * sizeof(HuffLut) + kBigLds;
+                const hipError_t e = allow_lds_big(lds_big);
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(k_chain_big, dim3(b.nchain / 64), dim3(kBigThreads), lds_big, s, b);
+            }
             else if (b.nchain)
                 hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
             break;
