@@ -566,9 +566,12 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     const uint32_t adaptive = (ctx->flags & JD_FLAG_FULL_PIECES) ? kPieceBits : adaptive_piece_bits(ecs_bits);
     P.piece_bits = (ctx->flags & JD_FLAG_FORCE_SYNC) ? 1024u : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u : adaptive;
     // shorter pieces also get a shorter warm-up: a lane that has not synchronised by then is
-    // re-scanned (k_rescan / k_chain), which costs less than every lane walking 4096 extra bits
+    // re-walked (k_redo / k_chain_big), which costs less than every lane walking 4096 extra bits.
+    // Three pieces' worth: on the reference's single-image sizes (4:4:4 q95, 200^2 .. 2000^2) as fast
+    // as two at 200^2 and 10 % faster at 2000^2 (fewer failed starts for k_chain_big's rounds); four
+    // were slower on small images (profiles/r05v_*)
     P.piece_overlap = (ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES)) ? kPieceOverlap
-                                                                             : std::min(kPieceOverlap, 2 * adaptive);
+                                                                             : std::min(kPieceOverlap, 3 * adaptive);
     if (ctx->piece_overlap >= 0) P.piece_overlap = uint32_t(ctx->piece_overlap);
     uint64_t sub = 0, entry_cursor = 0;
     P.chain_seg.reserve(seg_cursor + kPieceThreads * P.tablesets.size());
