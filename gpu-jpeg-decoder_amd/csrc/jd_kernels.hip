@@ -2331,42 +2331,46 @@ __global__ __launch_bounds__(256) void k_dc_sum(BatchDev b) {
 }
 
 // Wave per image: segmented exclusive scan over its tiles in raster order, in place: tile_dc
-// becomes the predictor of each component at the tile's first block.
+// becomes the predictor of each component at the tile's first block.  (f, v) o (g, w) = (f | g,
+// g ? w : v + w).  Each lane takes a run of consecutive tiles: its aggregate, a scan of the 64
+// aggregates, then the run again with the lane's carry.  (64 tiles per step with a carry from step
+// to step took ~40 us for the 3 250 tiles of a 2 000 x 2 000 4:4:4 image: 51 steps of dependent
+// loads and shuffles.)
 __global__ __launch_bounds__(64) void k_dc_scan(BatchDev b) {
     JD_PRIO_SHORT();
     const ImgDesc& im = b.imgs[blockIdx.x];
     const uint32_t lane = threadIdx.x, nt = im.tiles_x * im.tiles_y;
-    int c0 = 0, c1 = 0, c2 = 0;
-    for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
-        const uint32_t t = t0 + lane;
-        const DcPred a = t < nt ? b.tile_dc[im.tile_base + t] : DcPred{0, 0, 0, 0};
-        int v0 = a.p0, v1 = a.p1, v2 = a.p2, f = a.flag;
+    const uint32_t per = (nt + 63u) / 64u, t0 = min(nt, lane * per), t1 = min(nt, t0 + per);
+    DcPred* const td = b.tile_dc + im.tile_base;
+    int f = 0, v0 = 0, v1 = 0, v2 = 0;
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; t++) {
+        const DcPred a = td[t];
+        v0 = a.flag ? a.p0 : v0 + a.p0;
+        v1 = a.flag ? a.p1 : v1 + a.p1;
+        v2 = a.flag ? a.p2 : v2 + a.p2;
+        f |= a.flag;
+    }
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {  // (f, v) o (g, w) = (f | g, g ? w : v + w)
-            const int n0 = __shfl_up(v0, d, 64), n1 = __shfl_up(v1, d, 64), n2 = __shfl_up(v2, d, 64);
-            const int nf = __shfl_up(f, d, 64);
-            if (int(lane) >= d && !f) {
-                v0 += n0;
-                v1 += n1;
-                v2 += n2;
-                f = nf;
-            }
+    for (int d = 1; d < 64; d <<= 1) {  // inclusive over the lanes' runs
+        const int n0 = __shfl_up(v0, d, 64), n1 = __shfl_up(v1, d, 64), n2 = __shfl_up(v2, d, 64);
+        const int nf = __shfl_up(f, d, 64);
+        if (int(lane) >= d && !f) {
+            v0 += n0;
+            v1 += n1;
+            v2 += n2;
+            f = nf;
         }
-        if (!f) {  // no interval start in this chunk up to here: continue the carried predictors
-            v0 += c0;
-            v1 += c1;
-            v2 += c2;
-        }
-        int e0 = __shfl_up(v0, 1, 64), e1 = __shfl_up(v1, 1, 64), e2 = __shfl_up(v2, 1, 64);
-        if (lane == 0) {
-            e0 = c0;
-            e1 = c1;
-            e2 = c2;
-        }
-        if (t < nt) b.tile_dc[im.tile_base + t] = DcPred{e0, e1, e2, 0};
-        c0 = __shfl(v0, 63, 64);
-        c1 = __shfl(v1, 63, 64);
-        c2 = __shfl(v2, 63, 64);
+    }
+    int r0 = __shfl_up(v0, 1, 64), r1 = __shfl_up(v1, 1, 64), r2 = __shfl_up(v2, 1, 64);  // exclusive
+    if (lane == 0) r0 = r1 = r2 = 0;
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; t++) {
+        const DcPred a = td[t];
+        td[t] = DcPred{r0, r1, r2, 0};
+        r0 = a.flag ? a.p0 : r0 + a.p0;
+        r1 = a.flag ? a.p1 : r1 + a.p1;
+        r2 = a.flag ? a.p2 : r2 + a.p2;
     }
 }
 
