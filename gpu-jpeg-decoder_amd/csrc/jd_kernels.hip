@@ -153,6 +153,14 @@ __device__ void subplan_image(const BatchDev& b, uint32_t img, int lane);  // (b
 __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     JD_PRIO_SHORT();
     __shared__ uint32_t s_wsum[2][kScanThreads / 64];
+    // every piece slot reads invalid until k_subplan (or k_compact's subplan) claims it for an
+    // interval: the slots of per-image slack and padding stay so.  A slot per thread of the grid (a
+    // memset launch cost a single-image decode ~5 us on its critical path)
+    {
+        const uint32_t g = (blockIdx.y * gridDim.x + blockIdx.x) * kScanThreads + threadIdx.x;
+        const uint32_t stride = gridDim.x * gridDim.y * kScanThreads;
+        for (uint32_t u = g; u < b.nsub; u += stride) b.sub_seg[u] = kInvalidImage;
+    }
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t c = blockIdx.x;
     if (c >= im.nchunks) return;
@@ -317,6 +325,7 @@ __device__ __forceinline__ uint32_t fill_before(uintptr_t file, uint32_t lo, uin
 __global__ __launch_bounds__(64) void k_index(BatchDev b) {
     JD_PRIO_SHORT();
     const uint32_t ii = blockIdx.x;
+
     const ImgDesc& im = b.imgs[ii];
     const uintptr_t file = uintptr_t(im.jpeg);
     const uint32_t lo = im.ecs_off;
@@ -3995,13 +4004,12 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
     }
     switch (k) {
         case 0:
-            if (b.nsub) {  // (k_subplan / k_compact's subplan fill it) every slot not claimed by an
-                           // interval (per-image slack, padding) must read invalid; here, at the
-                           // front-end's start, the fill runs beside the other batch's kernels
+            if (b.max_chunks) {
+                hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);  // (fills sub_seg)
+            } else if (b.nsub) {  // no entropy-coded bytes at all: no k_scan to fill the piece slots
                 const hipError_t e = hipMemsetAsync(b.sub_seg, 0xFF, size_t(b.nsub) * 4, s);
                 if (e != hipSuccess) return e;
             }
-            if (b.max_chunks) hipLaunchKernelGGL(k_scan, dim3(b.max_chunks, b.nimg), dim3(kScanThreads), 0, s, b);
             break;
         case 1: hipLaunchKernelGGL(k_index, dim3(b.nimg), dim3(64), 0, s, b); break;
         case 2:
