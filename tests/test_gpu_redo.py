@@ -152,3 +152,27 @@ def test_big_interval_rounds_vs_oracle(monkeypatch, overlap, spare):
         assert np.array_equal(out, ref)
     finally:
         dec.close()
+
+
+@pytest.mark.parametrize("overlap", ["default", "256"])
+def test_big_intervals_with_dri_vs_oracle(monkeypatch, overlap):
+    """Several big intervals in one image (2000 x 2000 4:4:4 q95, an RSTn every 50 MCU rows: five
+    intervals of ~14 K 512-bit pieces): k_chain_big's rounds and counts on intervals that end at an
+    RSTn (every piece counts, the last one takes the rest) as well as the final one (bytes after its
+    last MCU ignored), with re-walk rounds forced by a short warm-up."""
+    px = jd_synth.synth_pixels(2000, 2000, 4242)
+    data = jd_synth.encode(px, 95, "4:4:4", restart_rows=50)
+    h = jdamd.parse(data)
+    assert h.restart_interval and -(-h.mcux * h.mcuy // h.restart_interval) == 5
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    if overlap != "default":
+        monkeypatch.setenv("JD_PIECE_OVERLAP_BITS", overlap)
+    dec = jdamd.Decoder(0)
+    try:
+        out = dec.decode(data)
+        nsub = int((dec.debug_fetch("sub_seg") != 0xFFFFFFFF).sum())
+        assert nsub > 5 * 1024  # intervals of thousands of pieces each (kBigInterval = 256)
+        assert np.array_equal(out, ref)
+    finally:
+        dec.close()
