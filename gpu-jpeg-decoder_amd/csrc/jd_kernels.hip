@@ -157,9 +157,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     // interval: the slots of per-image slack and padding stay so.  A slot per thread of the grid (a
     // memset launch cost a single-image decode ~5 us on its critical path)
     {
-        const uint32_t g = (blockIdx.y * gridDim.x + blockIdx.x) * kScanThreads + threadIdx.x;
-        const uint32_t stride = gridDim.x * gridDim.y * kScanThreads;
-        for (uint32_t u = g; u < b.nsub; u += stride) b.sub_seg[u] = kInvalidImage;
+        const uint64_t g = (uint64_t(blockIdx.y) * gridDim.x + blockIdx.x) * kScanThreads + threadIdx.x;
+        const uint64_t stride = uint64_t(gridDim.x) * gridDim.y * kScanThreads;  // (64-bit: never wraps)
+        for (uint64_t u = g; u < b.nsub; u += stride) b.sub_seg[u] = kInvalidImage;
     }
     const ImgDesc& im = b.imgs[blockIdx.y];
     const uint32_t c = blockIdx.x;
