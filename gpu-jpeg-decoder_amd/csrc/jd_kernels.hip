@@ -3190,6 +3190,10 @@ __device__ __forceinline__ void load_entry_quads(const EntryRange& r, uint4 (&E)
 // Per slot one compare against the quad's limit (slot q is the block's when q < lead + cnt - 8 qi,
 // and, in quad 0, q >= lead); both values of a word by one packed arithmetic shift, the high one
 // stored from the word's upper half (ds_write_b16_d16_hi).
+#ifndef JD_ABL_PHASE
+#define JD_ABL_PHASE 0  // diagnostic builds (wrong pixels): k_idct_color stops after the IDCT's plane
+                        // stores (1) or after the entry scatter (2): SQ counters of the phases
+#endif
 #ifndef JD_ABL_SCATTER
 #define JD_ABL_SCATTER 0  // diagnostic builds (wrong pixels): 1 = every slot to a fixed, bank-conflict-free
                           // position of its row; 2 = no scatter stores
@@ -3440,6 +3444,7 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         }
     }
     __syncthreads();
+    if (JD_ABL_PHASE == 1) return true;  // diagnostic builds: no colour stage (the planes are kept)
 
     // upsample + colour: 8 pixels of one row per lane-step, or of two rows when both chroma
     // planes are vertically subsampled (the two rows share their chroma samples and terms)
@@ -3595,6 +3600,7 @@ __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDe
     __syncthreads();
     scatter_entries(s_buf, staging_base(lane), R, E);
     __syncthreads();
+    if (JD_ABL_PHASE == 2) return;  // diagnostic builds: no IDCT and colour (the staging rows are kept)
     JD_STAMP_AT(2);
     idct_colour_tile<false, M>(b, im, img, tile, G, L, dc_pred, R.esc, s_buf, s_qz, [&] { JD_STAMP_AT(3); });
     JD_STAMP_AT(4);
