@@ -1825,17 +1825,17 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
 //    tables in global memory, as k_redo: almost every workgroup exits at once, and with the 73 KB
 //    of LDS a piece workgroup takes, each of them had to wait for a CU's LDS under the other
 //    batch's k_idct_color (1.1 ms instead of 0.02 in a kernel trace).
-//  * k_chain_big: one wave per flagged interval, for batches whose intervals may have thousands of
-//    pieces (an image without DRI in a small batch, in short pieces: one 2000 x 2000 4:4:4 q95
-//    image has 45 K pieces of 512 bits, and the serial walk took 0.3 us per piece, 13 ms).  A
-//    64-lane workgroup covers 64 entries of the chain list and takes its flagged intervals one after
-//    the other:
+//  * k_chain_big: for batches whose intervals may have thousands of pieces (an image without DRI in
+//    a small batch, in short pieces: one 2000 x 2000 4:4:4 q95 image has ~68 K pieces of 512 bits,
+//    and the serial walk took 0.3 us per piece, 13 ms).  One 8-wave workgroup per entry of the chain
+//    list (most exit at once: their interval is not flagged), on its flagged interval:
 //      - rounds: every piece whose start disagrees with its predecessor's end is re-walked from that
 //        end, all of them at once (a round re-walks from the previous round's ends).  A piece whose
 //        predecessors all agree starts at the truth, so each round settles at least the first
 //        disagreement and a run of r consecutive failures takes r rounds;
-//      - then the counts by prefix sums, wave-parallel (chain_interval);
-//      - after kFixRounds rounds without agreement (never seen), the serial walk.
+//      - then the counts by prefix sums over per-wave slices (chain_counts_wg);
+//      - after kFixRounds rounds without agreement (never seen at the shipped piece sizes), the
+//        serial walk.
 constexpr uint32_t kFixRounds = 32;
 constexpr uint32_t kFixPer = 16;
 // A piece's start and its predecessor's end, as this round sees them: loads that another lane of
@@ -2014,17 +2014,11 @@ __global__ __launch_bounds__(kBigThreads) void k_chain_big(BatchDev b) {
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    // the workgroup's 64 entries of the chain list (as k_chain_fix's 64-lane workgroups)
-    if (wv == 0) {
-        const uint32_t li = blockIdx.x * 64u + lane;
-        const uint32_t sl = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
-        const uint64_t t = __ballot(sl != kInvalidImage && b.seg_fix[sl] != 0u);
-        if (lane == 0) s_mask[0] = t;
-    }
-    __syncthreads();
-    uint64_t todo = s_mask[0];
-    if (!todo) return;  // workgroup-uniform: the common case
-    const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * 64u) / kPieceThreads]];
+    // one entry of the chain list per workgroup, so that a small batch's big intervals (a few images
+    // without DRI) are fixed side by side (64 entries per workgroup took them one after the other)
+    const uint32_t sl = (blockIdx.x < b.nchain) ? b.chain_seg[blockIdx.x] : kInvalidImage;
+    if (sl == kInvalidImage || b.seg_fix[sl] == 0u) return;  // workgroup-uniform: the common case
+    const TableSet& ts = b.tablesets[b.chain_wg_tableset[blockIdx.x / kPieceThreads]];
     stage_luts(b, ts, s_lut, int(kBigThreads));
     __syncthreads();
     const uint32_t* const luts = reinterpret_cast<const uint32_t*>(s_lut);
@@ -2032,10 +2026,8 @@ __global__ __launch_bounds__(kBigThreads) void k_chain_big(BatchDev b) {
     uint32_t* const ring = s_rows + kBigThreads * row_words(kWin) + tid * kRingWords;
     uint32_t* const rring = s_rows + kBigThreads * (row_words(kWin) + kRingWords) + tid * kRecRingWords;
     constexpr uint32_t kStep = 64 * kFixPer;
-    while (todo) {  // workgroup-uniform
-        const int L = __builtin_ctzll(todo);
-        todo &= todo - 1u;
-        const uint32_t s = b.chain_seg[blockIdx.x * 64u + uint32_t(L)];
+    {
+        const uint32_t s = sl;
         SegInfo S;
         seg_info(b, s, S);
         uint32_t dcp, acp;
@@ -2044,7 +2036,6 @@ __global__ __launch_bounds__(kBigThreads) void k_chain_big(BatchDev b) {
         // chunks of kStep pieces to (re)check: every chunk in the first round, then only those where
         // the round before re-walked a piece, and the chunk after each (its first piece follows the
         // re-walked chunk's last); chunk ci belongs to wave ci mod kBigWaves
-        __syncthreads();  // (the previous interval's last reads of s_mask / s_state)
         if (tid == 0) {
             s_mask[0] = ~0ull;
             s_mask[1] = 0ull;
@@ -4076,7 +4067,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
                 const size_t lds_big = size_t(b.max_slots) * sizeof(HuffLut) + kBigLds;
                 const hipError_t e = allow_lds_big(lds_big);
                 if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(k_chain_big, dim3(b.nchain / 64), dim3(kBigThreads), lds_big, s, b);
+                hipLaunchKernelGGL(k_chain_big, dim3(b.nchain), dim3(kBigThreads), lds_big, s, b);
             }
             else if (b.nchain)
                 hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
