@@ -2412,6 +2412,8 @@ __global__ __launch_bounds__(64) void k_dc_scan(BatchDev b) {
 enum { kC1 = 2841, kC2 = 2676, kC3 = 2408, kC5 = 1609, kC6 = 1108, kC7 = 565 };
 
 __device__ __forceinline__ int clip256(int v) { return min(max(v, -256), 255); }
+// clip256(v >> 14) before the shift: v clamped to [-256 * 2^14, 255 * 2^14 + 2^14 - 1]
+__device__ __forceinline__ int clip256_pre(int v) { return min(max(v, -256 * 16384), 255 * 16384 + 16383); }
 
 // idct.cpp:34-77 without the DC shortcut (identical results: SURVEY.md App. B P7, and
 // tests/test_gpu.py::test_idct_kat).
@@ -2523,7 +2525,7 @@ __device__ __forceinline__ int mad24v(int a, int k, int c) {
 // and 4 leave their outputs unshifted with the low byte cleared (idct_row_dot2<true>), because
 // ((v >> 8) << 8) + 8192 = (v + 8192) & ~255 (8192 a multiple of 256; no overflow: |v| < 2^31 - 8192
 // in the fast form's range), the 8192 riding in row 0's rounding constant.
-__device__ __forceinline__ void idct_col_fast(int* blk) {
+__device__ __forceinline__ void idct_col_fast(const int* blk, int (&o)[8]) {
     const int x1 = blk[8 * 4], x0 = blk[0];
     const int b1 = blk[8 * 1], b2 = blk[8 * 2], b3 = blk[8 * 3], b5 = blk[8 * 5], b6 = blk[8 * 6], b7 = blk[8 * 7];
     // (the rounding 4 rides in the inner multiply-add: two v_mad_i32_i24 per term, forced through
@@ -2548,15 +2550,25 @@ __device__ __forceinline__ void idct_col_fast(int* blk) {
     y0 -= x2;
     x2 = (181 * (x4 + x5) + 128) >> 8;
     x4 = (181 * (x4 - x5) + 128) >> 8;
-    blk[8 * 0] = clip256((x7 + y1) >> 14);
-    blk[8 * 1] = clip256((x3 + x2) >> 14);
-    blk[8 * 2] = clip256((y0 + x4) >> 14);
-    blk[8 * 3] = clip256((x8 + x6) >> 14);
-    blk[8 * 4] = clip256((x8 - x6) >> 14);
-    blk[8 * 5] = clip256((y0 - x4) >> 14);
-    blk[8 * 6] = clip256((x3 - x2) >> 14);
-    blk[8 * 7] = clip256((x7 - y1) >> 14);
+    o[0] = clip256_pre(x7 + y1);
+    o[1] = clip256_pre(x3 + x2);
+    o[2] = clip256_pre(y0 + x4);
+    o[3] = clip256_pre(x8 + x6);
+    o[4] = clip256_pre(x8 - x6);
+    o[5] = clip256_pre(y0 - x4);
+    o[6] = clip256_pre(x3 - x2);
+    o[7] = clip256_pre(x7 - y1);
 }
+// The column pass's outputs of columns 2p and 2p + 1 as one int16 pair: clip256(v >> 14) is
+// clip256_pre(v) >> 14, and the second shift writes its low 16 bits straight into the pair's high
+// half (SDWA destination), so no v_perm packs the pair (32 per block).
+__device__ __forceinline__ uint32_t pair14(int lo, int hi) {
+    uint32_t r = uint32_t(lo >> 14);
+    asm("v_ashrrev_i32_sdwa %0, 14, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(r) : "v"(hi));
+    return r;
+}
+
 
 __device__ __forceinline__ void idct_row_exact(int* blk) {
     const bool dc_only = ((blk[4] << 11) | blk[6] | blk[2] | blk[1] | blk[7] | blk[5] | blk[3]) == 0;
@@ -2649,8 +2661,10 @@ __device__ __forceinline__ void idct_row_dot2(const uint32_t (&dw)[32], int r, i
 // (their row outputs are 0: (0 + 128) >> 8), so their row passes are skipped and the column pass's
 // products with them fold away at compile time.
 // skip7 (wave-uniform): row 7 is zero in every lane, its row pass is skipped at run time.
+// pk[4 r + p]: row r's samples 2p, 2p + 1 as an int16 pair (the planes' layout).
 template <int NR = 8>
-__device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], int (&blk)[64], bool skip7 = false) {
+__device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], uint32_t (&pk)[32], bool skip7 = false) {
+    int blk[64];  // the row pass's outputs
     int c128, c8320;
     asm("v_mov_b32 %0, 0x80" : "=v"(c128));  // one VGPR holding the row pass's rounding term
     asm("v_mov_b32 %0, 0x2080" : "=v"(c8320));  // row 0: + the column pass's 8192 (idct_col_fast)
@@ -2666,7 +2680,13 @@ __device__ __forceinline__ void idct_block_dot2(const uint32_t (&dw)[32], int (&
         }
     }
 #pragma unroll
-    for (int c = 0; c < 8; c++) idct_col_fast(blk + c);
+    for (int c = 0; c < 8; c += 2) {
+        int lo[8], hi[8];
+        idct_col_fast(blk + c, lo);
+        idct_col_fast(blk + c + 1, hi);
+#pragma unroll
+        for (int r = 0; r < 8; r++) pk[4 * r + (c >> 1)] = pair14(lo[r], hi[r]);
+    }
 }
 // OR of the natural row r's eight zig-zag-ordered int16 coefficients held in the pair words dw.
 template <int R>
@@ -3345,7 +3365,7 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             return false;
         }
     }
-    int blk[64];
+    uint32_t pk[32];  // row r's int16 pairs: pk[4 r] .. pk[4 r + 3]
     if (!EXACT) {
         // every dequantised coefficient fits int16: packed multiplies in zig-zag order, DC in place
         typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -3361,8 +3381,9 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         dw[0] = __builtin_amdgcn_perm(dw[0], uint32_t(dq0), 0x07060100u);
         // row 7 is zero across a whole C2 tile in 96 % of tiles: its row pass is skipped by a
         // wave-uniform branch (a second copy of the IDCT without it made the kernel spill)
-        idct_block_dot2<8>(dw, blk, __all(!have || row_bits<7>(dw) == 0u));
+        idct_block_dot2<8>(dw, pk, __all(!have || row_bits<7>(dw) == 0u));
     } else {
+        int blk[64];
 #pragma unroll
         for (int p4 = 0; p4 < 8; p4++) {
             const uint4 qv = qz4[p4];
@@ -3376,6 +3397,8 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             }
         }
         idct_block_exact(blk);
+#pragma unroll
+        for (int q = 0; q < 32; q++) pk[q] = pair16(blk[2 * q], blk[2 * q + 1]);
     }
     mid();  // (k_idct_color: the next tile's entry loads, issued here so they are not live across the IDCT)
     if (b.fancy) {  // wave-uniform: component planes to HBM, k_colour_fancy takes it from there
@@ -3390,12 +3413,7 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
                            size_t(((r0 + mr) * vc + tyb) * 8) * ppc + ((m0 + mi) * hc + txb) * 8;
 #pragma unroll
             for (int r = 0; r < 8; r++) {
-                uint4 q;  // one v_perm per int16 pair
-                q.x = pair16(blk[8 * r + 0], blk[8 * r + 1]);
-                q.y = pair16(blk[8 * r + 2], blk[8 * r + 3]);
-                q.z = pair16(blk[8 * r + 4], blk[8 * r + 5]);
-                q.w = pair16(blk[8 * r + 6], blk[8 * r + 7]);
-                *gptr(reinterpret_cast<u32x4*>(dst)) = u32x4{q.x, q.y, q.z, q.w};
+                *gptr(reinterpret_cast<u32x4*>(dst)) = u32x4{pk[4 * r], pk[4 * r + 1], pk[4 * r + 2], pk[4 * r + 3]};
                 dst += ppc;
             }
         }
@@ -3425,14 +3443,8 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
         const uint32_t base = comp == 0 ? pbase[0] : (comp == 1 ? pbase[1] : pbase[2]);
         int16_t* dst = s_pl + base + ((mr * TM_::v(im, comp) + tyb) * 8) * pitch + (mi * hc + txb) * 8;
 #pragma unroll
-        for (int r = 0; r < 8; r++) {
-            uint4 q;  // one v_perm per int16 pair
-            q.x = pair16(blk[8 * r + 0], blk[8 * r + 1]);
-            q.y = pair16(blk[8 * r + 2], blk[8 * r + 3]);
-            q.z = pair16(blk[8 * r + 4], blk[8 * r + 5]);
-            q.w = pair16(blk[8 * r + 6], blk[8 * r + 7]);
-            *reinterpret_cast<uint4*>(dst + r * pitch) = q;
-        }
+        for (int r = 0; r < 8; r++)
+            *reinterpret_cast<uint4*>(dst + r * pitch) = uint4{pk[4 * r], pk[4 * r + 1], pk[4 * r + 2], pk[4 * r + 3]};
     }
     __syncthreads();
     if (JD_ABL_PHASE == 1) return true;  // diagnostic builds: no colour stage (the planes are kept)
@@ -3926,8 +3938,17 @@ __global__ void k_test_idct(const int32_t* in_zz, int32_t* out, int n, int exact
         in_range = in_range && uint32_t(v + 32768) <= 65535u;
         if (z & 1) dw[z >> 1] = pk16(blk[kNatOfZz[z - 1]], v);
     }
-    if (in_range) idct_block_dot2(dw, blk);
-    else idct_block_exact(blk);
+    if (in_range) {
+        uint32_t pk[32];
+        idct_block_dot2(dw, pk);
+#pragma unroll
+        for (int q = 0; q < 32; q++) {
+            blk[2 * q] = int(int16_t(pk[q] & 0xFFFFu));
+            blk[2 * q + 1] = int32_t(pk[q]) >> 16;
+        }
+    } else {
+        idct_block_exact(blk);
+    }
 #pragma unroll
     for (int z = 0; z < 64; z++) out[size_t(i) * 64 + z] = blk[z];
 }
