@@ -2987,6 +2987,73 @@ __device__ __forceinline__ void row_rgb_packed(const uint4& Yq, const uint32_t (
     w[5] = __builtin_amdgcn_perm(B[3], RG[3], 0x05030104u);                                            // b6 r7 g7 b7
 }
 
+// The same 24 bytes with the channels interleaved by the adds themselves: pixels 2u, 2u + 1 are
+// the int16 pairs (r0 g0) (b0 r1) (g1 b1), each y + t of its lanes with y taken from the pixel word's
+// low or high half (op_sel), against the term words A = (tr0, tg0), B = (tb0, tr1), C = (tg1, tb1)
+// (terms_il).  Output word k is pairs 2k and 2k + 1, saturated straight into its two halves: 12
+// adds and 12 saturations per 8 pixels, no byte shuffles (row_rgb_packed: 12 + 12 + 8 v_perm).
+__device__ __forceinline__ uint32_t pk_add_ll(uint32_t y, uint32_t t) {  // (y.lo + t.lo, y.lo + t.hi)
+    uint32_t s;
+    asm("v_pk_add_u16 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(s) : "v"(y), "v"(t));
+    return s;
+}
+__device__ __forceinline__ uint32_t pk_add_hh(uint32_t y, uint32_t t) {  // (y.hi + t.lo, y.hi + t.hi)
+    uint32_t s;
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(s) : "v"(y), "v"(t));
+    return s;
+}
+__device__ __forceinline__ uint32_t sat_lo(uint32_t x) {  // bytes 0, 1 (2, 3 zero)
+    uint32_t o;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(o) : "v"(x));
+    return o;
+}
+__device__ __forceinline__ uint32_t sat_hi(uint32_t lo2, uint32_t x) {  // bytes 2, 3 of lo2
+    asm("v_sat_pk_u8_i16_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD" : "+v"(lo2) : "v"(x));
+    return lo2;
+}
+__device__ __forceinline__ void row_rgb_il(const uint4& Yq, const uint32_t (&A)[4], const uint32_t (&B)[4],
+                                           const uint32_t (&C)[4], uint32_t (&w)[6]) {
+    const uint32_t Y[4] = {Yq.x, Yq.y, Yq.z, Yq.w};
+    uint32_t P[12];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        P[3 * u] = pk_add_ll(Y[u], A[u]);
+        P[3 * u + 1] = pk_add16<false>(Y[u], B[u]);
+        P[3 * u + 2] = pk_add_hh(Y[u], C[u]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = sat_hi(sat_lo(P[2 * k]), P[2 * k + 1]);
+}
+// The term words of row_rgb_il for the 8 >> SH chroma samples under 8 pixels (word u = pixels 2u,
+// 2u + 1): R and B straight from the high halves of their multiply-add sums (rb_pair), G's low half.
+// Returns the mask of samples (bit u) whose G needs the reference's double-precision path.
+template <int SH>
+__device__ __forceinline__ uint32_t terms_il(const int16_t* s_pl, uint32_t cboff, uint32_t croff, uint32_t (&A)[4],
+                                             uint32_t (&B)[4], uint32_t (&C)[4]) {
+    constexpr int NU = 8 >> SH;
+    int cb[8], cr[8];
+    load_plane<SH>(s_pl, cboff, cb);
+    load_plane<SH>(s_pl, croff, cr);
+    uint32_t xr[NU], xb[NU], tg[NU];
+    uint32_t ex = 0;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const ChromaTerms t = chroma_terms(cb[u], cr[u]);
+        ex |= t.exact ? (1u << u) : 0u;
+        xr[u] = uint32_t(mad24(cr[u], 91881, 128 << 16));
+        xb[u] = uint32_t(mad24(cb[u], 116130, (128 << 16) + 64));
+        tg[u] = uint32_t(t.g);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int a0 = SH == 0 ? 2 * w : (SH == 1 ? w : w >> 1), a1 = SH == 0 ? 2 * w + 1 : a0;  // samples of pixels 2w, 2w + 1
+        A[w] = __builtin_amdgcn_perm(tg[a0], xr[a0], 0x05040302u);  // (tr0, tg0)
+        B[w] = __builtin_amdgcn_perm(xr[a1], xb[a0], 0x07060302u);  // (tb0, tr1)
+        C[w] = __builtin_amdgcn_perm(xb[a1], tg[a1], 0x07060100u);  // (tg1, tb1)
+    }
+    return ex;
+}
+
 // The 4:2:0 tail step: 4 pixels of two rows that share their two chroma samples (both chroma
 // planes subsampled 2x2).  A 4:2:0 tile of 10 MCUs has 160 8-pixel row-pair groups, two and a half
 // lane-steps: the last half step is done as 64 4-pixel halves, so no lane idles (k_idct_color).
@@ -3484,20 +3551,18 @@ __device__ __forceinline__ bool idct_colour_tile(const BatchDev& b, const ImgDes
             // packed integer colour for every pixel; G of the few pixels whose chroma sample needs
             // the reference's double-precision path is patched afterwards (about 5 % of the
             // lane-steps have one such sample in some lane)
-            uint32_t TR[4], TG[4], TB[4], ex;
+            uint32_t TA[4], TB[4], TC[4], ex;
             switch (cmode) {
-                case 0: ex = terms_words<0>(s_pl, cboff, croff, TR, TG, TB); break;
-                case 1: ex = terms_words<1>(s_pl, cboff, croff, TR, TG, TB); break;
-                default: ex = terms_words<2>(s_pl, cboff, croff, TR, TG, TB); break;
+                case 0: ex = terms_il<0>(s_pl, cboff, croff, TA, TB, TC); break;
+                case 1: ex = terms_il<1>(s_pl, cboff, croff, TA, TB, TC); break;
+                default: ex = terms_il<2>(s_pl, cboff, croff, TA, TB, TC); break;
             }
             const uint4 Y0q = *reinterpret_cast<const uint4*>(s_pl + yoff);
-            if (cmode == 0u) row_rgb_packed<false>(Y0q, TR, TG, TB, w0);
-            else row_rgb_packed<true>(Y0q, TR, TG, TB, w0);
+            row_rgb_il(Y0q, TA, TB, TC, w0);
             uint4 Y1q = make_uint4(0, 0, 0, 0);
             if (pair) {
                 Y1q = *reinterpret_cast<const uint4*>(s_pl + yoff + ppitch[0]);
-                if (cmode == 0u) row_rgb_packed<false>(Y1q, TR, TG, TB, w1);  // (h1v2 chroma)
-                else row_rgb_packed<true>(Y1q, TR, TG, TB, w1);
+                row_rgb_il(Y1q, TA, TB, TC, w1);  // (shares the term words: vertically subsampled chroma)
             }
             if (__any(ex != 0u)) {  // uniform over the lanes in this step
                 switch (cmode) {
