@@ -2738,16 +2738,17 @@ __device__ __forceinline__ ChromaTerms chroma_terms(int cb, int cr) {
     ChromaTerms t;
     t.r = mad24(cr, 91881, 128 << 16) >> 16;
     t.b = mad24(cb, 58065, (128 << 15) + 32) >> 15;
-    // n' = n + 271 * 587000 is in [0, 2^29): floor(n' / 587000) = mulhi(n', M) >> 19 with
-    // M = ceil(2^51 / 587000) for every n' of the domain (checked exhaustively), two integer
-    // instructions instead of the float convert / multiply / floor / convert
-    constexpr int kOff = 271 * 587000;
-    const uint32_t np = uint32_t(mad24(cb, 202008, mad24(cr, 419198, kOff)));
-    const uint32_t qp = __umulhi(np, 3836115526u) >> 19;  // q + 271
-    const int rem = mad24(int(qp), -587000, int(np));
-    const bool nz = np != uint32_t(kOff);
-    t.exact = nz && (rem < 64 || rem > 587000 - 64);
-    t.g = nz ? 127 + 271 - int(qp) : 128;
+    // G = clamp(y + 128 - ceil(n / 587000)) (the N == 0 case of the definition above included):
+    // m = 272 * 587000 - n is in [0, 2^29), and floor(m / 587000) = 272 - ceil(n / 587000) =
+    // mulhi(m, M) >> 19 with M = ceil(2^51 / 587000) for every m of the domain (checked
+    // exhaustively): the term is that quotient - 144, with no select for n == 0.  The remainder
+    // of m is within 64 of 0 or 587000 exactly when n's is (n != 0: m != 272 * 587000).
+    constexpr int kOff = 272 * 587000;
+    const uint32_t m = uint32_t(mad24(cb, -202008, mad24(cr, -419198, kOff)));
+    const uint32_t qm = __umulhi(m, 3836115526u) >> 19;
+    const int rem = mad24(int(qm), -587000, int(m));
+    t.exact = m != uint32_t(kOff) && (rem < 64 || rem > 587000 - 64);
+    t.g = int(qm) - 144;
     return t;
 }
 __device__ __forceinline__ uint32_t clamp_u8(int v) { return uint32_t(min(max(v, 0), 255)); }  // v_med3_i32
@@ -3100,6 +3101,29 @@ __device__ __forceinline__ void store12(uint8_t* dst, const uint32_t (&w)[3], ui
             if (uint32_t(k) < 3 * n) d[k] = uint8_t(w[k / 4] >> (8 * (k % 4)));
     }
 }
+// 4 pixels (2 words of Y) -> 12 bytes, row_rgb_il's form
+__device__ __forceinline__ void rgb4_il(const uint2& Yq, const uint32_t (&A)[2], const uint32_t (&B)[2],
+                                        const uint32_t (&C)[2], uint32_t (&w)[3]) {
+    const uint32_t Y[2] = {Yq.x, Yq.y};
+    uint32_t P[6];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        P[3 * u] = pk_add_ll(Y[u], A[u]);
+        P[3 * u + 1] = pk_add16<false>(Y[u], B[u]);
+        P[3 * u + 2] = pk_add_hh(Y[u], C[u]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) w[k] = sat_hi(sat_lo(P[2 * k]), P[2 * k + 1]);
+}
+// term words (terms_il) of pixels 2w, 2w + 1 on chroma samples a0, a1
+__device__ __forceinline__ void term_words_of(const ChromaTerms& t0, int cb0, int cr0, const ChromaTerms& t1, int cb1,
+                                              int cr1, uint32_t& A, uint32_t& B, uint32_t& C) {
+    const uint32_t xr0 = uint32_t(mad24(cr0, 91881, 128 << 16)), xr1 = uint32_t(mad24(cr1, 91881, 128 << 16));
+    const uint32_t xb0 = uint32_t(mad24(cb0, 116130, (128 << 16) + 64)), xb1 = uint32_t(mad24(cb1, 116130, (128 << 16) + 64));
+    A = __builtin_amdgcn_perm(uint32_t(t0.g), xr0, 0x05040302u);
+    B = __builtin_amdgcn_perm(xr1, xb0, 0x07060302u);
+    C = __builtin_amdgcn_perm(xb1, uint32_t(t1.g), 0x07060100u);
+}
 __device__ __forceinline__ void colour4x2(const int16_t* s_pl, uint32_t yoff, uint32_t ypitch, uint32_t cboff,
                                           uint32_t croff, uint32_t (&w0)[3], uint32_t (&w1)[3]) {
     const uint32_t cbw = *reinterpret_cast<const uint32_t*>(s_pl + cboff);
@@ -3107,13 +3131,13 @@ __device__ __forceinline__ void colour4x2(const int16_t* s_pl, uint32_t yoff, ui
     const int cb[2] = {int(int16_t(cbw & 0xFFFFu)), int32_t(cbw) >> 16};
     const int cr[2] = {int(int16_t(crw & 0xFFFFu)), int32_t(crw) >> 16};
     const ChromaTerms t0 = chroma_terms(cb[0], cr[0]), t1 = chroma_terms(cb[1], cr[1]);
-    const uint32_t TR[2] = {uint32_t(t0.r), uint32_t(t1.r)};
-    const uint32_t TG[2] = {uint32_t(t0.g), uint32_t(t1.g)};
-    const uint32_t TB[2] = {uint32_t(t0.b), uint32_t(t1.b)};
+    uint32_t A[2], B[2], C[2];  // word u = pixels 2u, 2u + 1 on sample u
+    term_words_of(t0, cb[0], cr[0], t0, cb[0], cr[0], A[0], B[0], C[0]);
+    term_words_of(t1, cb[1], cr[1], t1, cb[1], cr[1], A[1], B[1], C[1]);
     const uint32_t ex = (t0.exact ? 1u : 0u) | (t1.exact ? 2u : 0u);
     const uint2 Y0 = *reinterpret_cast<const uint2*>(s_pl + yoff), Y1 = *reinterpret_cast<const uint2*>(s_pl + yoff + ypitch);
-    rgb4_packed(Y0, TR, TG, TB, w0);
-    rgb4_packed(Y1, TR, TG, TB, w1);
+    rgb4_il(Y0, A, B, C, w0);
+    rgb4_il(Y1, A, B, C, w1);
     if (__any(ex != 0u)) {
         fix_g4_exact(Y0, cb, cr, ex, w0);
         fix_g4_exact(Y1, cb, cr, ex, w1);
@@ -3135,11 +3159,11 @@ __device__ __forceinline__ void colour4x1(const int16_t* s_pl, uint32_t yoff, ui
         t[u] = chroma_terms(cb[u], cr[u]);
         ex |= t[u].exact ? (1u << u) : 0u;
     }
-    const uint32_t TR[2] = {r_pair(cr[0], cr[1]), r_pair(cr[2], cr[3])};
-    const uint32_t TG[2] = {pair16(t[0].g, t[1].g), pair16(t[2].g, t[3].g)};
-    const uint32_t TB[2] = {b_pair(cb[0], cb[1]), b_pair(cb[2], cb[3])};
+    uint32_t A[2], B[2], C[2];  // word u = pixels 2u, 2u + 1 on samples 2u, 2u + 1
+    term_words_of(t[0], cb[0], cr[0], t[1], cb[1], cr[1], A[0], B[0], C[0]);
+    term_words_of(t[2], cb[2], cr[2], t[3], cb[3], cr[3], A[1], B[1], C[1]);
     const uint2 Y0 = *reinterpret_cast<const uint2*>(s_pl + yoff);
-    rgb4_packed<false>(Y0, TR, TG, TB, w);
+    rgb4_il(Y0, A, B, C, w);
     if (__any(ex != 0u)) {
         const uint32_t Y[2] = {Y0.x, Y0.y};
 #pragma unroll

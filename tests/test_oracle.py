@@ -175,6 +175,18 @@ def test_chroma_terms_exhaustive():
     ex_i = (n != 0) & ((rem_i < 64) | (rem_i > 587000 - 64))
     ex_f = (n != 0) & ((rem_f < 64) | (rem_f > 587000 - 64))
     assert (ex_i == ex_f).all()
+    # the kernel's form: m = 272 * 587000 - n, G's term = (mulhi(m, M) >> 19) - 144, which is
+    # 127 - floor(n / 587000) for n != 0 and 128 for n == 0 wherever G is not taken from the
+    # reference's double path (ex_i), and the same exact-path flags from m's remainder
+    m = 272 * 587000 - n
+    assert m.min() >= 0 and m.max() < 2**29
+    qm = (m * 3836115526) >> 51
+    assert (qm == m // 587000).all()
+    rem_m = m - qm * 587000
+    ex_m = (m != 272 * 587000) & ((rem_m < 64) | (rem_m > 587000 - 64))
+    assert (ex_m == ex_i).all()
+    tg_old = np.where(n != 0, 127 - q_i, 128)
+    assert ((qm - 144) == tg_old)[~ex_i].all()
 
 
 def test_color_fast_path_exhaustive():
