@@ -343,7 +343,8 @@ struct BatchDev {
     uint32_t* entries;
     uint64_t entries_cap;         // entry slots allocated
     uint32_t* status;             // per image
-    unsigned long long* counters; // [0] AC entries written, [1] slow_tiles entries, [2] k_idct_color's tile queue
+    unsigned long long* counters; // [0] AC entries written, [1] slow_tiles entries, [2] k_idct_color's tile queue,
+                                  // [3] k_pieceplan's choice, [4] k_piece workgroups started (walk order)
     uint32_t max_tiles;
     TileRef* slow_tiles;          // (image, tile) k_idct_color left to k_idct_color_exact; count in counters[1]
     uint32_t total_tiles;

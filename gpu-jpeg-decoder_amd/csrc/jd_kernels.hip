@@ -700,16 +700,22 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     }
     return x;
 }
-__global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
+// One workgroup of kPlanThreads (JD_PLAN_THREADS): 1024 by default; 256 fit beside a walk or the
+// colour stage (one wave per SIMD), which the 1024-lane form does not.
+#ifndef JD_PLAN_THREADS
+#define JD_PLAN_THREADS 1024
+#endif
+constexpr uint32_t kPlanThreads = JD_PLAN_THREADS, kPlanWaves = kPlanThreads / 64;
+__global__ __launch_bounds__(kPlanThreads) void k_pieceplan(BatchDev b) {
     JD_PRIO_SHORT();
     __shared__ unsigned long long s_cnt[kPlanCands];
-    __shared__ uint32_t s_ws[16], s_wm[16], s_choice;
+    __shared__ uint32_t s_ws[kPlanWaves], s_wm[kPlanWaves], s_choice;
     const uint32_t t = threadIdx.x;
     const int lane = int(t & 63u), wv = int(t >> 6);
     if (t < kPlanCands) s_cnt[t] = 0;
     __syncthreads();
     uint32_t cnt[kPlanCands] = {};
-    for (uint32_t img = t; img < b.nimg; img += 1024) {
+    for (uint32_t img = t; img < b.nimg; img += kPlanThreads) {
         const u32x4* src = reinterpret_cast<const u32x4*>(b.img_cand + size_t(img) * kPlanCands);
 #pragma unroll
         for (int q = 0; q < kPlanCands / 4; q++) {
@@ -747,7 +753,7 @@ __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
     __syncthreads();
     const uint32_t c = s_choice;
     uint32_t run = 0, mrun = 0;
-    for (uint32_t i0 = 0; i0 < b.nimg; i0 += 1024) {
+    for (uint32_t i0 = 0; i0 < b.nimg; i0 += kPlanThreads) {
         const uint32_t i = i0 + t;
         const bool v = i < b.nimg;
         uint32_t img = 0, ts = 0, used = 0;
@@ -765,7 +771,7 @@ __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
         __syncthreads();
         uint32_t excl = run + incl - used, tot = 0;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < int(kPlanWaves); j++) {
             if (j < wv) excl += s_ws[j];
             tot += s_ws[j];
         }
@@ -776,7 +782,7 @@ __global__ __launch_bounds__(1024) void k_pieceplan(BatchDev b) {
         __syncthreads();
         uint32_t m = max(mrun, mk), mt = mrun;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < int(kPlanWaves); j++) {
             if (j < wv) m = max(m, s_wm[j]);
             mt = max(mt, s_wm[j]);
         }
@@ -904,6 +910,15 @@ constexpr uint32_t kBlkStep = 4u;
 constexpr int kRedoThreads = 64;
 static_assert(kPieceThreads % kRedoThreads == 0, "a redo workgroup lies inside one piece workgroup");
 constexpr size_t kRedoLds = size_t(kRedoThreads) * (row_words(kWin) + kRingWords + kRecRingWords) * 4;
+// Large-batch re-walks (k_redo<false>, k_chain_fix) as direct walks (walk_piece DR: no LDS, <= 64
+// VGPRs), for builds whose walk workgroup fills a CU (JD_PIECE_THREADS=1024 with 11-bit tables:
+// the LDS rows would keep them from running beside it).  Off with the default 512-lane walk, where
+// the LDS form measured 1-4 % faster per step.
+#ifndef JD_REWALK_DIRECT
+#define JD_REWALK_DIRECT (JD_PIECE_THREADS >= 1024)
+#endif
+constexpr bool kRewalkDirect = JD_REWALK_DIRECT;
+constexpr size_t kRewalkLds = kRewalkDirect ? 0 : kRedoLds;
 static_assert((kRedoThreads * row_words(kWin) * 4) % 32 == 0, "redo rings must start 32-byte aligned (ring_put)");
 size_t piece_lds_bytes(uint32_t max_slots, int nt) {
     return size_t(max_slots) * sizeof(HuffLut) + size_t(nt) * (row_words(kWin) + kRingWords + kRecRingWords) * 4;
@@ -959,6 +974,47 @@ struct BitRow {
         rp -= uint32_t(WIN);
         wb += uint32_t(WIN * 8);
     }
+};
+
+// The same reader straight over the un-stuffed stream in global memory, for the re-walks that run
+// beside a walk which holds a CU's whole LDS (k_redo<false>, k_chain_fix: DR walks).  rp is a byte
+// offset from `base`, the walk's first 16-byte aligned window, so the arithmetic (and the window
+// rounds: lim moves instead of rp) is BitRow's; each word is a clamped dword load + byte swap.
+struct BitStream {
+    uint32_t A, B, nextw, rp, lim, wb;
+    int s;
+    uintptr_t base, lastw;
+    __device__ __forceinline__ uint32_t word(uint32_t off) const {
+        const uintptr_t a = base + off;
+        return __builtin_bswap32(*reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(a < lastw ? a : lastw));
+    }
+    __device__ __forceinline__ void init(uintptr_t wa, uintptr_t last, uint32_t off, uint32_t start) {
+        base = wa;
+        lastw = last + 12u;  // the last mapped dword (last: the image's last mapped 16-byte chunk)
+        const uint32_t w0 = off >> 5, o = off & 31u;
+        A = o ? word(4u * w0) : 0u;
+        B = word(4u * (w0 + (o ? 1u : 0u)));
+        const uint32_t r = w0 + (o ? 2u : 1u);
+        nextw = word(4u * r);
+        rp = 4u * r;
+        lim = uint32_t(kWin);
+        s = int((32u - o) & 31u);
+        wb = start - off - 32u;
+    }
+    __device__ __forceinline__ uint32_t peek() const { return __builtin_amdgcn_alignbit(A, B, uint32_t(s)); }
+    __device__ __forceinline__ void skip(uint32_t L) {
+        s -= int(L);
+        const int m = s >> 31;
+        s &= 31;
+        A = bfi_sel(uint32_t(m), B, A);
+        B = bfi_sel(uint32_t(m), nextw, B);
+        asm("v_mad_i32_i24 %0, %1, -4, %0" : "+v"(rp) : "v"(m));
+        nextw = word(rp);
+    }
+    __device__ __forceinline__ uint32_t bit() const { return rp * 8u + wb - uint32_t(s); }
+    __device__ __forceinline__ bool in_window() const { return rp <= lim; }
+    template <int WIN>
+    __device__ __forceinline__ void next_window() { lim += uint32_t(WIN); }
 };
 
 // Load q of a window at a (the last one is the overlap: 8 or 16 bytes), and its row words.
@@ -1111,19 +1167,26 @@ __device__ __forceinline__ void st_ent(uint4* p, const uint4& v) { *p = v; }
 #define JD_PSTAT 0  // diagnostic builds: k_piece walk statistics summed into BatchDev::stamps[0..15]
 #endif
 
-template <int KIND, bool GL = false>
+// DR (direct): the stream read from global memory (BitStream) and every entry slot and block record
+// stored straight into the region, so the walk needs no LDS at all (row, ring and rring unused):
+// the re-walks that must fit beside a walk holding a CU's whole LDS (k_redo<false>, k_chain_fix).
+template <int KIND, bool GL = false, bool DR = false>
 __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp,
                                            uint32_t* row, uint32_t* ring, uint32_t* rring, bool active_in, PWalk& W, CpRec* cp,
                                            uint32_t cp_bits, const uint32_t (&cpb)[kCpMax]) {
     const uintptr_t a_start = S.data + (W.start >> 3);
     uintptr_t wa = a_start & ~uintptr_t(15);
+    typename std::conditional<DR, BitStream, BitRow>::type R;
+    if constexpr (DR) {
+        R.init(wa, S.last, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
+    } else {
 #pragma unroll
-    for (int q = 0; q < win_loads(kWin); q++) {
-        const u32x4 v = win_load(wa, q, S.last);
-        JD_ROW_FILL(row, v, q);
+        for (int q = 0; q < win_loads(kWin); q++) {
+            const u32x4 v = win_load(wa, q, S.last);
+            JD_ROW_FILL(row, v, q);
+        }
+        R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
     }
-    BitRow R;
-    R.init(row, uint32_t(a_start & 15) * 8 + (W.start & 7u), W.start);
     const uint32_t sbits = S.bits;
     const uint32_t bpm3 = 3u * S.bpm;
     typedef TabSpace<GL> TS;
@@ -1132,7 +1195,13 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     const TabT tab_dc0 = lbase + (dcp & 7u) * kLutBytes;
     uint32_t* const reg = W.reg;
     uint32_t* const rec_top = W.reg + (W.rw - 1u);  // block record k at rec_top[-k]
-    const uint32_t ringb = lds_addr(ring);  // 32-byte aligned: slot address = ringb | (ent2 & 30)
+    const uint32_t ringb = DR ? 0u : lds_addr(ring);  // 32-byte aligned: slot address = ringb | (ent2 & 30)
+    uint16_t* const reg16 = reinterpret_cast<uint16_t*>(W.reg);  // (DR: slot i straight to reg16[i])
+    // a 16-bit slot at 2 x slot index e2: into the lane's ring, or (DR) straight into the region
+    auto put_slot = [&](uint32_t e2, uint32_t v) {
+        if constexpr (DR) reg16[e2 >> 1] = uint16_t(v);
+        else ring_put(ringb, e2, v);
+    };
     uint32_t z = 0, b3 = 0;
     TabT tab = tab_dc0;
     bool active = active_in;
@@ -1176,7 +1245,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // block record k goes to ring word 3 - (k & 3), so that the ring reads as the records' memory
     // order (descending from rec_top); group fr (records 4fr .. 4fr + 3) is stored when complete,
     // at most one group pending (a block takes >= 2 iterations, a flush comes every other one)
-    const uint32_t rrb = lds_addr(rring);  // 16-byte aligned
+    const uint32_t rrb = DR ? 0u : lds_addr(rring);  // 16-byte aligned
     uint32_t fr = 0;  // record groups stored
     uint4* rgp = reinterpret_cast<uint4*>(rec_top - 3u);  // where group fr goes (a pointer stepped down)
     // an even quad is held in registers and stored with the odd one after it: 32 contiguous bytes
@@ -1207,7 +1276,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     WinGroup<kGroup> nx;
     uint32_t gi = 0;  // window round within the group, wave-uniform
     while (true) {
-        if (gi == 0) nx.load(wa + kWin, S.last);
+        if (!DR && gi == 0) nx.load(wa + kWin, S.last);
         uint32_t it = 0;  // equal in every lane still in the loop (lanes only leave it)
         while (active && R.in_window()) {
             it++;
@@ -1229,7 +1298,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             uint32_t L = __builtin_amdgcn_ubfe(lo, kLoL1Shift, 5u);
             // a slot is written for every symbol; a stored coefficient (E1, zn < 64: bit 6 of
             // lo & ~zn) advances ent
-            ring_put(ringb, ent2, (uint32_t(v1) << 6) | zn);
+            put_slot(ent2, (uint32_t(v1) << 6) | zn);
             uint32_t e1 = __builtin_amdgcn_ubfe(lo & ~zn, 6u, 1u);
             asm("" : "+v"(e1));  // keeps bfe + lshl_add (not lshr + and + add)
             ent2 += e1 << 1;
@@ -1245,7 +1314,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             // pair's total length L1 + L2.
             const bool pr = (lo & kLoPair) && zn < 63u;
             const uint32_t zn2 = zn + __builtin_amdgcn_ubfe(hi, 12u, 7u);
-            ring_put(ringb, ent2, (uint32_t(int(hi) >> 23) << 6) | zn2);
+            put_slot(ent2, (uint32_t(int(hi) >> 23) << 6) | zn2);
             // E2 (bit 7 of lo) and zn2 < 64 (zn2 <= 127: bit 6 clear) as bit 7 of lo & ~(zn2 << 1)
             uint32_t zs = zn2 << 1;
             asm("" : "+v"(zs));  // (else not + shift + and instead of shift + one v_bitop3)
@@ -1277,8 +1346,8 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 // the escaped value goes to the next slot unconditionally (a free slot, overwritten
                 // by the next entry unless the value needed it)
                 const bool big = entry_big(val);
-                ring_put(ringb, ent2, entry16(val, zn, big));
-                ring_put(ringb, ent2 + 2u, uint32_t(val));
+                put_slot(ent2, entry16(val, zn, big));
+                put_slot(ent2 + 2u, uint32_t(val));
                 ent_blk2 = (emit && big) ? esc_mark(ent_blk2) : ent_blk2;
                 ent2 += emit ? (big ? 4u : 2u) : 0u;
                 if (e & kEntBad) {  // the next MCU end takes the branch below
@@ -1292,13 +1361,13 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             // the block's end: its record to the ring and the per-block counters, in the branch the
             // record store needs anyway (exec-masked increments instead of select + add outside it)
             if (fin) {
-                *(__attribute__((address_space(3))) uint32_t*)size_t(rrb | (~blk & 12u)) =
-                    block_rec(ent2 - ent_blk2, dcd);
+                if constexpr (DR) rec_top[-int(blk >> 2)] = block_rec(ent2 - ent_blk2, dcd);
+                else *(__attribute__((address_space(3))) uint32_t*)size_t(rrb | (~blk & 12u)) = block_rec(ent2 - ent_blk2, dcd);
                 blk += 4u;
                 b3 += 3u;
                 ent_blk2 = ent2;
             }
-            if ((it & 1u) == 0u) {
+            if (!DR && (it & 1u) == 0u) {
                 JD_FLUSH_Q();
                 JD_FLUSH_B();
             }
@@ -1356,8 +1425,10 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
                 thr = min(min(W.stop_at, end_thr), nxt);
             }
         }
-        JD_FLUSH_Q();
-        JD_FLUSH_B();
+        if (!DR) {
+            JD_FLUSH_Q();
+            JD_FLUSH_B();
+        }
         if (active && R.bit() > sbits) {  // past the data
             if (m_end < end_thr) {  // (else in an MCU begun in the last byte, at m_end: padding)
                 m_end = R.bit();
@@ -1376,18 +1447,20 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             st_rounds++;
         }
         if (__ballot(active) == 0) break;  // wave-uniform
-        nx.fill_next(row);
+        if (!DR) nx.fill_next(row);
         gi = __builtin_amdgcn_readfirstlane(gi + 1u == uint32_t(kGroup) ? 0u : gi + 1u);
         R.template next_window<kWin>();
         wa += kWin;
     }
 #undef JD_FLUSH_Q
 #undef JD_FLUSH_B
-    if (fq & 1u) st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);  // a held quad
-    if (ent2 & 15u)  // the last, partial quad (every complete one is stored; the region has room for all of it)
-        st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)));
-    // the last, partial record group (every complete one is stored: the window round's flush)
-    for (uint32_t r = 0; r < ((blk >> 2) & 3u); r++) rec_top[-int(4u * fr + r)] = rring[3u - r];
+    if constexpr (!DR) {
+        if (fq & 1u) st_ent(reinterpret_cast<uint4*>(reg + 4u * fq - 4u), hq);  // a held quad
+        if (ent2 & 15u)  // the last, partial quad (every complete one is stored; the region has room for all of it)
+            st_ent(reinterpret_cast<uint4*>(reg + 4u * fq), *reinterpret_cast<const uint4*>(ring + 4u * (fq & 1u)));
+        // the last, partial record group (every complete one is stored: the window round's flush)
+        for (uint32_t r = 0; r < ((blk >> 2) & 3u); r++) rec_top[-int(4u * fr + r)] = rring[3u - r];
+    }
     W.m_start = m_start;
     W.m_end = m_end;
     W.mcus = mcus;
@@ -1586,7 +1659,7 @@ __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
 // spare region of the image when one is left (joining the speculative walk at a checkpoint),
 // else over its own region (no join: that overwrites what the checkpoints describe).
 // Returns the piece's new end.
-template <bool GL>
+template <bool GL, bool DR = false>
 __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceGeo& P, uint32_t s, uint32_t u,
                                uint32_t expect, const uint32_t* s_lutw, uint32_t dcp, uint32_t acp, uint32_t* row,
                                uint32_t* ring, uint32_t* rring, bool need) {
@@ -1612,7 +1685,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
     W.stop_at = piece_stop(P);
     W.reg = S.eimg + base;
     W.rw = P.rw;
-    walk_piece<kRedo, GL>(S, s_lutw, dcp, acp, row, ring, rring, need, W, cp, 0xFFFFFFFFu, cpb);
+    walk_piece<kRedo, GL, DR>(S, s_lutw, dcp, acp, row, ring, rring, need, W, cp, 0xFFFFFFFFu, cpb);
     if (!need) return 0;
     uint32_t end = W.m_end, mcus = W.mcus, ents = W.ents, emcu = W.emcu, tail = W.tail;
     if (W.join) {  // (checkpoints lie before the last byte: the tail, if any, is the speculative walk's)
@@ -1648,9 +1721,9 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
 // lookups are a serial chain, ~1 us each from global memory); else read from global memory, so the
 // workgroups need little LDS and fit beside the other batch's big kernels.
 template <bool LT>
-__global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
+__global__ __launch_bounds__(kRedoThreads, (!LT && kRewalkDirect) ? 8 : 1) void k_redo(BatchDev b) {
     JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // [tables,] the lanes' rows and rings
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // (LT) the tables, the lanes' rows and rings
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + (LT ? size_t(b.max_slots) * sizeof(HuffLut) : 0));
     const uint32_t u = blockIdx.x * kRedoThreads + threadIdx.x;
@@ -1661,7 +1734,7 @@ __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
         expect = b.piece_end[u - 1];
         need = b.piece_bit[u] != expect;
     }
-    if (!__syncthreads_or(need)) return;  // workgroup-uniform
+    if (__ballot(need) == 0) return;  // wave-uniform (one wave per workgroup)
     // the piece workgroup (kPieceThreads lanes, one table set) this one is part of
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
     if (LT) {
@@ -1678,11 +1751,14 @@ __global__ __launch_bounds__(kRedoThreads) void k_redo(BatchDev b) {
     }
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    redo_piece<!LT>(b, S, P, s, u, expect,
-                    LT ? reinterpret_cast<const uint32_t*>(s_lut) : reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0),
-                    dcp, acp, s_rows + threadIdx.x * row_words(kWin),
-                    s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
-                    s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords, need);
+    if constexpr (!LT && kRewalkDirect)  // no LDS at all: fits beside a walk that holds a CU's whole LDS
+        redo_piece<true, true>(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
+                               nullptr, nullptr, nullptr, need);
+    else
+        redo_piece<!LT>(b, S, P, s, u, expect,
+                        LT ? reinterpret_cast<const uint32_t*>(s_lut) : reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0),
+                        dcp, acp, s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
+                        s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords, need);
 }
 
 // The MCUs piece j contributes, given its first MCU m0 (the interval has nmcu_seg): a piece before
@@ -1843,7 +1919,7 @@ constexpr uint32_t kFixPer = 16;
 __device__ __forceinline__ uint32_t ld_wg(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-template <bool GL>
+template <bool GL, bool DR = false>
 __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S, const uint32_t* luts, uint32_t dcp,
                                  uint32_t acp, uint32_t* row, uint32_t* ring, uint32_t* rring) {
     const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
@@ -1861,7 +1937,7 @@ __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S
         uint32_t pend = ld_wg(b.piece_end + u);
         if (ld_wg(b.piece_bit + u) != expect) {  // the start had not synchronised: re-walk from the truth
             const PieceGeo P = piece_geo(b, S, s, u);
-            pend = redo_piece<GL>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, rring, true);
+            pend = redo_piece<GL, DR>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, rring, true);
         }
         const uint32_t pm = b.piece_nmcu[u], em = b.piece_emcu[u];
         const bool last = j + 1 == n || (final_seg && mcu_run + pm >= nmcu_seg);
@@ -1876,24 +1952,28 @@ __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S
     b.seg_fix[s] = 0u;
 }
 
-__global__ __launch_bounds__(kRedoThreads) void k_chain_fix(BatchDev b) {
+__global__ __launch_bounds__(kRedoThreads, kRewalkDirect ? 8 : 1) void k_chain_fix(BatchDev b) {
     JD_PRIO_CRIT();
-    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings only
+    extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // the lanes' rows and rings (none when direct)
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn);
     const uint32_t li = blockIdx.x * kRedoThreads + threadIdx.x;
     uint32_t s = (li < b.nchain) ? b.chain_seg[li] : kInvalidImage;
     if (s != kInvalidImage && !b.seg_fix[s]) s = kInvalidImage;
     const bool need = s != kInvalidImage;
-    if (!__syncthreads_or(need)) return;  // workgroup-uniform: the common case
+    if (__ballot(need) == 0) return;  // wave-uniform (one wave per workgroup): the common case
     const TableSet& ts = b.tablesets[b.chain_wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
     if (!need) return;
     SegInfo S;
     seg_info(b, s, S);
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    chain_fix_serial<true>(b, s, S, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
-                     s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
-                     s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords);
+    const uint32_t* luts = reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0);
+    if constexpr (kRewalkDirect)
+        chain_fix_serial<true, true>(b, s, S, luts, dcp, acp, nullptr, nullptr, nullptr);
+    else
+        chain_fix_serial<true>(b, s, S, luts, dcp, acp, s_rows + threadIdx.x * row_words(kWin),
+                               s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
+                               s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords);
 }
 
 // k_chain_big's workgroup: 8 waves on one interval at a time (16 would leave 128 VGPRs a lane and
@@ -4153,7 +4233,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
             break;
         case 3: {
             if (!b.nsub || b.small_fold) break;
-            if (b.piece_plan) hipLaunchKernelGGL(k_pieceplan, dim3(1), dim3(1024), 0, s, b);
+            if (b.piece_plan) hipLaunchKernelGGL(k_pieceplan, dim3(1), dim3(kPlanThreads), 0, s, b);
             hipLaunchKernelGGL(k_subplan, dim3(b.nimg), dim3(64), 0, s, b);
             break;
         }
@@ -4168,7 +4248,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
                 hipLaunchKernelGGL(k_redo<true>, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads),
                                    size_t(b.max_slots) * sizeof(HuffLut) + kRedoLds, s, b);
             else if (b.nsub)
-                hipLaunchKernelGGL(k_redo<false>, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
+                hipLaunchKernelGGL(k_redo<false>, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads), kRewalkLds, s, b);
             break;
         case 6:
             if (!b.nseg) break;
@@ -4180,7 +4260,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
                 hipLaunchKernelGGL(k_chain_big, dim3(b.nchain), dim3(kBigThreads), lds_big, s, b);
             }
             else if (b.nchain)
-                hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRedoLds, s, b);
+                hipLaunchKernelGGL(k_chain_fix, dim3(b.nchain / kRedoThreads), dim3(kRedoThreads), kRewalkLds, s, b);
             break;
         case 7:
             if (b.nsub) hipLaunchKernelGGL(k_gather, dim3((b.nsub + 255) / 256), dim3(256), 0, s, b);  // 64 pieces per wave

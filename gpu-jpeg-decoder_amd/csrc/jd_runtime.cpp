@@ -189,11 +189,13 @@ struct Pending {
     double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0, piece_overlap = 0;
     double t_plan = 0, t_upload = 0;
 };
+// launch records (>= the async depth + 2: a record is reused 4 launches later)
 constexpr int kNumPending = 4;
+// timing slot of k_idct_color (jd_kernel_name): the colour stage starts here
 constexpr int kIdctSlot = 9;
 // batches of at most this many images without a piece plan fold the subplan into k_compact
 // (jd_kernels.hip subplan_image: a launch saved on a small batch's critical path)
-constexpr uint32_t kSmallFoldImages = 64;    // timing slot of k_idct_color (jd_kernel_name): the colour stage starts here  // records (>= the async depth + 2: a record is reused 4 launches later)
+constexpr uint32_t kSmallFoldImages = 64;
 
 struct jd_ctx {
     int device = 0;
@@ -846,7 +848,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_chts = put(blob, P.chain_wg_tableset);
         const size_t o_modes = put(blob, P.mode_imgs);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
-        const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // entries, slow tiles, IDCT queue
+        const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // BatchDev::counters
         const size_t o_tscur = put(blob, P.ts_slot0);
         const size_t o_order = put(blob, P.img_order);
         const size_t upload = blob.size();
@@ -1220,6 +1222,7 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
         return v > 0 ? prio_greatest : v < 0 ? prio_least : 0;
     };
     const bool idct_stream = std::getenv("JD_IDCT_STREAM") && std::strtol(std::getenv("JD_IDCT_STREAM"), nullptr, 0) != 0;
+
     for (Slot& sl : ctx->slots) {
         bool ok = hipStreamCreateWithPriority(&sl.stream, hipStreamNonBlocking, prio_of("JD_SLOT_PRIO")) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&sl.h2d_done, hipEventDisableTiming) == hipSuccess;

@@ -22,7 +22,7 @@ for r in $(seq 1 "$reps"); do
     lib=gpu-jpeg-decoder_amd/libjdamd_$v.so; [ "$v" = cur ] && lib=gpu-jpeg-decoder_amd/libjdamd.so
     ver=1; case "$v" in abl*) ver=0;; esac  # ablation builds compute wrong pixels on purpose
     tag=$(echo "$spec" | tr '@,=/' '____')_$r
-    env JDAMD_LIB=$PWD/$lib JDAMD_ALLOW_ABI_MISMATCH=1 ${envs//,/ } timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-sample 0 \
+    env JDAMD_LIB=$PWD/$lib JDAMD_ALLOW_ABI_MISMATCH=1 ${envs//,/ } timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-sample 0 \
       --e2e-steps 0 --copy-peak 0 --verify $ver ${AB_ARGS:-} > "$out/$tag.json" 2> "$out/$tag.err" || { tail -20 "$out/$tag.err"; exit 1; }
     python - "$out/$tag.json" "$spec" <<'PY'
 import json, sys
