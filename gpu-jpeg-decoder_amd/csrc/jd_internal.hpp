@@ -283,6 +283,12 @@ struct TileRef {
     uint32_t img, tile;
 };
 
+// BatchDev::counters after the first four (jd_stats): pieces k_redo re-walked; intervals k_chain_fix /
+// k_chain_big fixed, their rounds (a serial k_chain_fix pass counts one) and re-walked pieces, and the
+// k_chain_big intervals that stopped early at a right piece with an error
+constexpr int kCtrRedo = 4, kCtrFixIntervals = 5, kCtrFixRounds = 6, kCtrFixRewalks = 7, kCtrFixEarly = 8;
+constexpr int kNumCounters = 10;
+
 struct BatchDev {
     const ImgDesc* imgs;
     uint32_t nimg;
@@ -343,8 +349,8 @@ struct BatchDev {
     uint32_t* entries;
     uint64_t entries_cap;         // entry slots allocated
     uint32_t* status;             // per image
-    unsigned long long* counters; // [0] AC entries written, [1] slow_tiles entries, [2] k_idct_color's tile queue,
-                                  // [3] k_pieceplan's choice, [4] k_piece workgroups started (walk order)
+    unsigned long long* counters; // kNumCounters: [0] AC entries written, [1] slow_tiles entries, [2] k_idct_color's
+                                  // tile queue, [3] k_pieceplan's choice, then the re-walk counters (kCtr*), [4] k_piece workgroups started (walk order)
     uint32_t max_tiles;
     TileRef* slow_tiles;          // (image, tile) k_idct_color left to k_idct_color_exact; count in counters[1]
     uint32_t total_tiles;
@@ -359,6 +365,8 @@ struct BatchDev {
     unsigned long long* stamps;   // diagnostic builds (JD_STAMP): 8 s_memtime stamps per IDCT tile, else null
     uint32_t fancy;
     uint32_t max_fancy_wgs;       // k_colour_fancy bands per image: x in bits 0..15, y in 16..31
+    uint32_t fix_round_cap;       // diagnostics (JD_FIX_ROUND_CAP): k_chain_big gives up (corrupt) after this many rounds; 0: never
+    uint32_t skip_redo;           // diagnostics (JD_SKIP_REDO): no k_redo (the speculative starts stay as k_piece left them)
 };
 
 }  // namespace jd

@@ -293,6 +293,11 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
     for (int o = 32; o > 0; o >>= 1) x = max(x, uint32_t(__shfl_xor(int(x), o, 64)));
     return x;
 }
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, uint32_t(__shfl_xor(int(x), o, 64)));
+    return x;
+}
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += uint32_t(__shfl_xor(int(x), o, 64));
@@ -409,7 +414,12 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
     // allocation atomic (1 024 images on one table set's cursor took ~60 us, serialised)
     // this wave's seg_cstart / seg_cend stores are read back by other lanes of the wave: wait until
     // the L2 has them (vmcnt(0); __threadfence's L2 write-back cost ~20 us here) and read past the L1
+    // (the immediate is gfx9's vmcnt(0) encoding, where stores count on vmcnt too: ADVICE r05)
+#if !defined(__HIP_DEVICE_COMPILE__) || defined(__GFX9__)
     __builtin_amdgcn_s_waitcnt(0x0F70);
+#else
+#error "k_index: the vmcnt(0) wait is written for gfx9 (gfx950)"
+#endif
     // lane = candidate c (lane & 15) over every 4th interval (lane >> 4): few registers, so that
     // k_index still fits beside a walk (64 VGPRs per SIMD left)
     const uint32_t p = plan_cand(b.piece_bits, lane & 15);
@@ -1207,6 +1217,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     bool active = active_in;
     uint32_t m_start = W.start, m_end = W.start;
     if (W.start >= sbits) active = false;  // starts at the data end: empty
+    // No MCU begins in the piece's share (an MCU longer than a piece: 4:4:4 q95 MCUs take ~450 bits,
+    // 256-bit pieces were tried in round 5): the piece is empty, its end its start, which is then the
+    // next piece's start too.  (Walking one MCU regardless made every piece after such a share start
+    // one MCU late against its successor, so nearly every start disagreed and the chain could only be
+    // repaired piece by piece: the r05ac run that went silent, profiles/r06j_*.)
+    if (W.start >= W.stop_at) active = false;
     uint32_t next_cp = W.start + cp_bits, ncp = 0, join = 0;
     // The last byte: an MCU end at/after end_thr leaves fewer than 8 bits, which are padding (1-bits
     // before RSTn / EOI) or, where an MCU can be that short (a grayscale block: DC "00" + EOB
@@ -1581,6 +1597,56 @@ __device__ __forceinline__ uint32_t piece_stop(const PieceGeo& P) {
     return (P.j + 1 == P.npc) ? 0xFFFFFFFFu : uint32_t(min<uint64_t>(uint64_t(P.j + 1) * P.plen, 0xFFFFFFFEu));
 }
 
+// A piece's speculative walk (k_piece's lane, and k_redo's re-speculation with a longer warm-up):
+// for piece j > 0 first the warm-up (sync_piece, every lane of the wave together) from `overlap`
+// bits before its nominal start, then the writing walk into the piece's own region, with
+// checkpoints.  Piece 0 of an interval starts at bit 0 in the true state.  luts: the table set in LDS.
+__device__ __forceinline__ void spec_piece(const BatchDev& b, const SegInfo& S, const PieceGeo& P, uint32_t u, bool valid,
+                                           const uint32_t* luts, uint32_t dcp, uint32_t acp, uint32_t* row, uint32_t* ring,
+                                           uint32_t* rring, uint32_t overlap, unsigned long long* stats) {
+    PWalk W;
+    // piece j > 0 synchronises from piece_overlap bits before its nominal start (from bit 0,
+    // exactly, when that is closer) to the first MCU boundary at/after it
+    const uint64_t pstart = uint64_t(P.j) * P.plen;
+    const uint32_t warm_to = (P.j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
+    W.start = (pstart <= overlap) ? 0u : min(uint32_t(pstart - overlap), warm_to);
+    bool live = valid;
+    uint32_t sync_end = 0;
+    const bool spec = valid && P.j != 0;
+    const uint32_t m = sync_piece(S, luts, dcp, acp, row, W.start, warm_to, spec, sync_end);
+    if (spec) {
+        live = m != kNoPiece;
+        W.start = live ? m : 0u;
+    }
+    W.stop_at = piece_stop(P);
+    W.reg = S.eimg + P.own;
+    W.rw = P.rw;
+    W.stats = stats;
+    CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
+    const uint32_t none[kCpMax] = {};
+    walk_piece<kSpec>(S, luts, dcp, acp, row, ring, rring, live, W, cp, max(1u, P.plen / kCpMax), none);
+    if (!valid) return;
+    if (!live) {  // as a warm-up that runs past the data: no piece, an error at its first MCU
+        W.m_start = kNoPiece;
+        W.m_end = sync_end;
+        W.emcu = 0u;
+    }
+    b.piece_bit[u] = (P.j == 0) ? 0u : W.m_start;
+    b.piece_end[u] = W.m_end;
+    b.piece_nmcu[u] = W.mcus;
+    b.piece_nent[u] = W.ents;
+    // W.emcu: the first error after the last checkpoint; each checkpoint holds its segment's
+    uint32_t emcu = W.emcu;
+#pragma unroll
+    for (int k = 0; k < kCpMax; k++)
+        if (uint32_t(k) < W.ncp) emcu = min(emcu, cp[k].flags);
+    b.piece_emcu[u] = piece_emcu_code(emcu, W.tail);
+    b.piece_abase[u] = P.own;
+    b.piece_amcu[u] = W.mcus;
+    b.piece_join[u] = (min(W.tail, 255u) << 24) | (W.ncp << 16);
+    cp[kCpMax] = CpRec{W.m_end, W.mcus, W.ents, W.emcu};
+}
+
 // Lane per piece slot: the speculative walk -- for a piece j > 0 first the warm-up (sync_piece,
 // every lane of the wave together), then the writing walk into the piece's own region.  Piece 0 of an interval starts at bit 0 in the true state.
 // NT = kPieceThreads, or 64 for batches with few pieces (one small image: a few 512-lane
@@ -1608,51 +1674,9 @@ __global__ __launch_bounds__(NT) void k_piece(BatchDev b) {
     }
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    PWalk W;
-    // piece j > 0 synchronises from piece_overlap bits before its nominal start (from bit 0,
-    // exactly, when that is closer) to the first MCU boundary at/after it
-    const uint64_t pstart = uint64_t(P.j) * P.plen;
-    const uint32_t warm_to = (P.j == 0) ? 0u : uint32_t(min<uint64_t>(pstart, S.bits));
-    W.start = (pstart <= b.piece_overlap) ? 0u : min(uint32_t(pstart - b.piece_overlap), warm_to);
-    bool live = valid;
-    uint32_t sync_end = 0;
-    const bool spec = valid && P.j != 0;
-    const uint32_t m = sync_piece(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp,
-                                  s_rows + threadIdx.x * row_words(kWin), W.start, warm_to, spec, sync_end);
-    if (spec) {
-        live = m != kNoPiece;
-        W.start = live ? m : 0u;
-    }
-    W.stop_at = piece_stop(P);
-    W.reg = S.eimg + P.own;
-    W.rw = P.rw;
-    W.stats = b.stamps;
-    CpRec* const cp = b.piece_cp + size_t(u) * kCpRecords;
-    const uint32_t none[kCpMax] = {};
-    walk_piece<kSpec>(S, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWin),
-                      s_rows + NT * row_words(kWin) + threadIdx.x * kRingWords,
-                      s_rows + NT * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords, live, W, cp,
-                      max(1u, P.plen / kCpMax), none);
-    if (!valid) return;
-    if (!live) {  // as a warm-up that runs past the data: no piece, an error at its first MCU
-        W.m_start = kNoPiece;
-        W.m_end = sync_end;
-        W.emcu = 0u;
-    }
-    b.piece_bit[u] = (P.j == 0) ? 0u : W.m_start;
-    b.piece_end[u] = W.m_end;
-    b.piece_nmcu[u] = W.mcus;
-    b.piece_nent[u] = W.ents;
-    // W.emcu: the first error after the last checkpoint; each checkpoint holds its segment's
-    uint32_t emcu = W.emcu;
-#pragma unroll
-    for (int k = 0; k < kCpMax; k++)
-        if (uint32_t(k) < W.ncp) emcu = min(emcu, cp[k].flags);
-    b.piece_emcu[u] = piece_emcu_code(emcu, W.tail);
-    b.piece_abase[u] = P.own;
-    b.piece_amcu[u] = W.mcus;
-    b.piece_join[u] = (min(W.tail, 255u) << 24) | (W.ncp << 16);
-    cp[kCpMax] = CpRec{W.m_end, W.mcus, W.ents, W.emcu};
+    spec_piece(b, S, P, u, valid, reinterpret_cast<const uint32_t*>(s_lut), dcp, acp, s_rows + threadIdx.x * row_words(kWin),
+               s_rows + NT * row_words(kWin) + threadIdx.x * kRingWords,
+               s_rows + NT * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords, b.piece_overlap, b.stamps);
 }
 
 // Re-walk piece u of interval s from its true start `expect` (its predecessor's end): into a
@@ -1673,8 +1697,13 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
         stail = pj >> 24;
         tot = cp[kCpMax];
         const uint32_t img = b.seg_img[s];
-        const uint32_t a = b.no_pool ? 0xFFFFFFFFu : atomicAdd(&b.img_pool[img], P.rw);
-        if (uint64_t(a) + P.rw <= b.imgs[img].entry_cap) base = a;
+        const uint32_t cap = b.imgs[img].entry_cap;
+        // (the cursor is only advanced while it is below the cap: many rounds of re-walks would
+        // otherwise wrap it past 2^32 and hand out regions that overlap the image's pieces)
+        const uint32_t a = (b.no_pool || __hip_atomic_load(&b.img_pool[img], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cap)
+                               ? 0xFFFFFFFFu
+                               : atomicAdd(&b.img_pool[img], P.rw);
+        if (uint64_t(a) + P.rw <= cap) base = a;
         else ncp = 0;  // in place
     }
 #pragma unroll
@@ -1714,27 +1743,51 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
 }
 
 // Lane per piece: re-walk, all at once, every piece whose speculative start disagrees with its
-// predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images).
-// Starting from that end is exact when the predecessor is right; a predecessor re-walked in this
-// round keeps its end when it joins its speculative walk, and otherwise k_chain notices.
+// predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images)
+// while that predecessor itself agrees with its own: starting from that end is then exact when the
+// predecessor is right.  A piece whose predecessor disagrees too waits for the next round: re-walked
+// from an end that is likely wrong, it would come out wrong, and its successor re-walked from it
+// next (r06 measured that cascade: with most starts failed, k_chain_big then needed thousands of
+// rounds).  Up to kRedoRounds rounds per workgroup, each only while some lane of the workgroup still
+// has work; a lane's predecessor may belong to another workgroup, whose rounds run at the same time,
+// so what is left, k_chain finds.  A run of r failed starts takes r rounds.
 // LT: the table set staged in LDS (small batches, BatchDev::big_chain or small_fold: the re-walks'
 // lookups are a serial chain, ~1 us each from global memory); else read from global memory, so the
 // workgroups need little LDS and fit beside the other batch's big kernels.
+constexpr uint32_t kRedoRoundsLT = 16;  // small batches: short pieces, runs of failed starts are common
+constexpr uint32_t kRedoRoundsBig = 2;  // large batches: the second round takes the rare double failure
 template <bool LT>
 __global__ __launch_bounds__(kRedoThreads, (!LT && kRewalkDirect) ? 8 : 1) void k_redo(BatchDev b) {
     JD_PRIO_CRIT();
+    constexpr uint32_t kRedoRounds = LT ? kRedoRoundsLT : kRedoRoundsBig;
     extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];  // (LT) the tables, the lanes' rows and rings
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + (LT ? size_t(b.max_slots) * sizeof(HuffLut) : 0));
-    const uint32_t u = blockIdx.x * kRedoThreads + threadIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t u = blockIdx.x * kRedoThreads + lane;
     const uint32_t s = (u < b.nsub) ? b.sub_seg[u] : kInvalidImage;
+    const uint32_t sb = s != kInvalidImage ? b.seg_sub_base[s] : 0u;
+    const bool valid = s != kInvalidImage && u != sb;  // (piece 0 of an interval starts at bit 0)
     uint32_t expect = 0;
-    bool need = false;
-    if (s != kInvalidImage && u != b.seg_sub_base[s]) {
+    bool dis = false;  // this piece's start disagrees with its predecessor's end
+    if (valid) {
         expect = b.piece_end[u - 1];
-        need = b.piece_bit[u] != expect;
+        dis = b.piece_bit[u] != expect;
     }
-    if (__ballot(need) == 0) return;  // wave-uniform (one wave per workgroup)
+    // the predecessor's own agreement: lane - 1's, or (lane 0) read from memory
+    auto pred_dis = [&](bool agent) {
+        const bool up = __shfl_up(int(dis), 1, 64) != 0;
+        bool pd = lane > 0 && up;
+        if (lane == 0 && valid && u - 1u != sb) {
+            const uint32_t pb = agent ? __hip_atomic_load(b.piece_bit + u - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : b.piece_bit[u - 1];
+            const uint32_t pe = agent ? __hip_atomic_load(b.piece_end + u - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : b.piece_end[u - 2];
+            pd = pb != pe;
+        }
+        return pd;
+    };
+    if (__ballot(dis) == 0) return;  // wave-uniform (one wave per workgroup)
+    bool need = dis && !pred_dis(false);
+    uint64_t needm = __ballot(need);
     // the piece workgroup (kPieceThreads lanes, one table set) this one is part of
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
     if (LT) {
@@ -1743,7 +1796,7 @@ __global__ __launch_bounds__(kRedoThreads, (!LT && kRewalkDirect) ? 8 : 1) void 
     }
     SegInfo S;
     PieceGeo P{0u, 1u, 0u, 0u, 0u};
-    if (need) {
+    if (valid) {
         seg_info(b, s, S);
         P = piece_geo(b, S, s, u);
     } else {
@@ -1751,14 +1804,34 @@ __global__ __launch_bounds__(kRedoThreads, (!LT && kRewalkDirect) ? 8 : 1) void 
     }
     uint32_t dcp, acp;
     table_slots(ts, S, dcp, acp);
-    if constexpr (!LT && kRewalkDirect)  // no LDS at all: fits beside a walk that holds a CU's whole LDS
-        redo_piece<true, true>(b, S, P, s, u, expect, reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0), dcp, acp,
-                               nullptr, nullptr, nullptr, need);
-    else
-        redo_piece<!LT>(b, S, P, s, u, expect,
-                        LT ? reinterpret_cast<const uint32_t*>(s_lut) : reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0),
-                        dcp, acp, s_rows + threadIdx.x * row_words(kWin), s_rows + kRedoThreads * row_words(kWin) + threadIdx.x * kRingWords,
-                        s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + threadIdx.x * kRecRingWords, need);
+    const uint32_t* const luts = LT ? reinterpret_cast<const uint32_t*>(s_lut) : reinterpret_cast<const uint32_t*>(b.set_luts + ts.set_lut0);
+    uint32_t rewalks = 0;
+    for (uint32_t r = 0; needm != 0; r++) {  // (needm: wave-uniform)
+        rewalks += uint32_t(__builtin_popcountll(needm));
+        if constexpr (!LT && kRewalkDirect)  // no LDS at all: fits beside a walk that holds a CU's whole LDS
+            redo_piece<true, true>(b, S, P, s, u, expect, luts, dcp, acp, nullptr, nullptr, nullptr, need);
+        else
+            redo_piece<!LT>(b, S, P, s, u, expect, luts, dcp, acp, s_rows + lane * row_words(kWin),
+                            s_rows + kRedoThreads * row_words(kWin) + lane * kRingWords,
+                            s_rows + kRedoThreads * (row_words(kWin) + kRingWords) + lane * kRecRingWords, need);
+        if (r + 1 == kRedoRounds) break;
+        // the next round, from the current starts and ends.  This round's stores are waited for
+        // (vmcnt(0): they are in the L2), and the arrays are read past the L1; a predecessor in a
+        // workgroup on another XCD may be seen late, which only leaves its disagreement to k_chain
+        // (an agent-scope release would write the L2 back, ~20 us, as in k_index).
+#if !defined(__HIP_DEVICE_COMPILE__) || defined(__GFX9__)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+#else
+#error "k_redo: the vmcnt(0) wait is written for gfx9 (gfx950)"
+#endif
+        if (valid) {
+            expect = __hip_atomic_load(b.piece_end + u - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dis = __hip_atomic_load(b.piece_bit + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != expect;
+        }
+        need = dis && !pred_dis(true);
+        needm = __ballot(need);
+    }
+    if (lane == 0) atomicAdd(&b.counters[kCtrRedo], (unsigned long long)rewalks);
 }
 
 // The MCUs piece j contributes, given its first MCU m0 (the interval has nmcu_seg): a piece before
@@ -1794,8 +1867,7 @@ __device__ __forceinline__ uint32_t piece_take(uint32_t pm, uint32_t em, uint32_
 // One wave per interval s of n pieces (k_chain), kPer consecutive pieces per lane: an interval
 // without DRI can have a thousand pieces, and each wave-iteration is a round of dependent global
 // loads (kPer = 4 there; 1 for the short intervals of DRI streams).
-// kAgreed: the caller has just verified every start (k_chain_big's last round): no second check.
-template <uint32_t kPer, bool kAgreed = false>
+template <uint32_t kPer>
 __device__ __forceinline__ void chain_interval(const BatchDev& b, uint32_t s, uint32_t lane, const SegInfo& S,
                                                uint32_t base, uint32_t n, uint32_t nmcu_seg, bool final_seg) {
     // The scan's last interval ends at EOI, and what follows its last MCU is ignored: the piece
@@ -1827,7 +1899,7 @@ __device__ __forceinline__ void chain_interval(const BatchDev& b, uint32_t s, ui
         }
     }
     bool need = false;
-    for (uint32_t j0 = 0; !kAgreed && j0 <= jl; j0 += kStep) {
+    for (uint32_t j0 = 0; j0 <= jl; j0 += kStep) {
 #pragma unroll
         for (uint32_t t = 0; t < kPer; t++) {
             const uint32_t j = j0 + kPer * lane + t;
@@ -1905,14 +1977,21 @@ __global__ __launch_bounds__(256) void k_chain(BatchDev b) {
 //    a small batch, in short pieces: one 2000 x 2000 4:4:4 q95 image has ~68 K pieces of 512 bits,
 //    and the serial walk took 0.3 us per piece, 13 ms).  One 8-wave workgroup per entry of the chain
 //    list (most exit at once: their interval is not flagged), on its flagged interval:
-//      - rounds: every piece whose start disagrees with its predecessor's end is re-walked from that
-//        end, all of them at once (a round re-walks from the previous round's ends).  A piece whose
-//        predecessors all agree starts at the truth, so each round settles at least the first
-//        disagreement and a run of r consecutive failures takes r rounds;
-//      - then the counts by prefix sums over per-wave slices (chain_counts_wg);
-//      - after kFixRounds rounds without agreement (never seen at the shipped piece sizes), the
-//        serial walk.
-constexpr uint32_t kFixRounds = 32;
+//      - rounds, each in two phases split by a workgroup barrier: (A) every piece of the chunks to
+//        check whose start disagrees with its predecessor's end is flagged (piece_mcu0 = the round's
+//        tag: that array is scratch until the counts), then (B) every flagged piece is re-walked
+//        from its predecessor's end, and the lane goes on into the pieces after it for as long as
+//        the new end still disagrees with the next start and that piece is not flagged itself (no
+//        other lane touches it in this round).  The pieces before the first flagged one all agree,
+//        so they are right: each round settles at least the first disagreement, and a run of
+//        pieces whose speculative walks agree with each other in a wrong MCU phase is re-walked by
+//        one lane in one round, not one round per piece;
+//      - it stops when a round flags nothing, or when a piece before the first flagged one (so a
+//        right one) has an error: the counts are then exact already (the error either lies in
+//        the MCUs the interval counts, and the image is corrupt, or after them, in trailing bytes
+//        of the final interval, and the pieces that matter all precede it).  No round limit is
+//        needed (the first disagreement moves on every round), and no serial fallback;
+//      - then the counts by prefix sums over per-wave slices (chain_counts_wg).
 constexpr uint32_t kFixPer = 16;
 // A piece's start and its predecessor's end, as this round sees them: loads that another lane of
 // the wave may have stored in the previous round (a workgroup-scope fence orders the rounds).
@@ -1926,7 +2005,7 @@ __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S
     const uint32_t nmcu_seg = S.nblk / S.bpm;
     const bool final_seg = seg_is_final(b, s);  // trailing bytes after its last MCU are ignored
     bool bad = false, done = false;
-    uint32_t expect = 0, mcu_run = 0;
+    uint32_t expect = 0, mcu_run = 0, rewalks = 0;
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t u = base + j;
         if (done) {  // past the piece that completed the final interval: nothing to take
@@ -1938,6 +2017,7 @@ __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S
         if (ld_wg(b.piece_bit + u) != expect) {  // the start had not synchronised: re-walk from the truth
             const PieceGeo P = piece_geo(b, S, s, u);
             pend = redo_piece<GL, DR>(b, S, P, s, u, expect, luts, dcp, acp, row, ring, rring, true);
+            rewalks++;
         }
         const uint32_t pm = b.piece_nmcu[u], em = b.piece_emcu[u];
         const bool last = j + 1 == n || (final_seg && mcu_run + pm >= nmcu_seg);
@@ -1950,6 +2030,9 @@ __device__ void chain_fix_serial(const BatchDev& b, uint32_t s, const SegInfo& S
     }
     if (bad) atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
     b.seg_fix[s] = 0u;
+    atomicAdd(&b.counters[kCtrFixIntervals], 1ull);  // jd_stats (one serial pass: one round)
+    atomicAdd(&b.counters[kCtrFixRounds], 1ull);
+    if (rewalks) atomicAdd(&b.counters[kCtrFixRewalks], (unsigned long long)rewalks);
 }
 
 __global__ __launch_bounds__(kRedoThreads, kRewalkDirect ? 8 : 1) void k_chain_fix(BatchDev b) {
@@ -2088,16 +2171,18 @@ __global__ __launch_bounds__(kBigThreads) void k_chain_big(BatchDev b) {
     // (small batches only: the table set is staged in LDS, as in k_piece -- the re-walks of each
     // round are serial chains of lookups, ~1 us each from global memory)
     extern __shared__ __attribute__((aligned(32))) uint8_t s_dyn[];
-    __shared__ unsigned long long s_mask[2];  // [0] this round's dirty chunks (< 64), [1] the next round's
-    __shared__ uint32_t s_state;              // bit 0: dirty chunks >= 64, 1: next round's, 2: a start disagreed
+    __shared__ unsigned long long s_mask[2];  // [0] this round's chunks to check (< 64), [1] the next round's
+    __shared__ uint32_t s_state;              // bit 0: chunks >= 64 to check, 1: the next round's
+    __shared__ uint32_t s_jmin, s_jerr;       // this round: first flagged piece; first piece seen with an error
+    __shared__ uint32_t s_nflag;              // this round: pieces flagged (diagnostics: BatchDev::stamps)
     __shared__ uint32_t s_sum[kBigWaves], s_jl[2];
     HuffLut* s_lut = reinterpret_cast<HuffLut*>(s_dyn);
     uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_dyn + size_t(b.max_slots) * sizeof(HuffLut));
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     // one entry of the chain list per workgroup, so that a small batch's big intervals (a few images
     // without DRI) are fixed side by side (64 entries per workgroup took them one after the other)
-    const uint32_t sl = (blockIdx.x < b.nchain) ? b.chain_seg[blockIdx.x] : kInvalidImage;
-    if (sl == kInvalidImage || b.seg_fix[sl] == 0u) return;  // workgroup-uniform: the common case
+    const uint32_t s = (blockIdx.x < b.nchain) ? b.chain_seg[blockIdx.x] : kInvalidImage;
+    if (s == kInvalidImage || b.seg_fix[s] == 0u) return;  // workgroup-uniform: the common case
     const TableSet& ts = b.tablesets[b.chain_wg_tableset[blockIdx.x / kPieceThreads]];
     stage_luts(b, ts, s_lut, int(kBigThreads));
     __syncthreads();
@@ -2106,79 +2191,152 @@ __global__ __launch_bounds__(kBigThreads) void k_chain_big(BatchDev b) {
     uint32_t* const ring = s_rows + kBigThreads * row_words(kWin) + tid * kRingWords;
     uint32_t* const rring = s_rows + kBigThreads * (row_words(kWin) + kRingWords) + tid * kRecRingWords;
     constexpr uint32_t kStep = 64 * kFixPer;
-    {
-        const uint32_t s = sl;
-        SegInfo S;
-        seg_info(b, s, S);
-        uint32_t dcp, acp;
-        table_slots(ts, S, dcp, acp);
-        const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
-        // chunks of kStep pieces to (re)check: every chunk in the first round, then only those where
-        // the round before re-walked a piece, and the chunk after each (its first piece follows the
-        // re-walked chunk's last); chunk ci belongs to wave ci mod kBigWaves
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    SegInfo S;
+    seg_info(b, s, S);
+    uint32_t dcp, acp;
+    table_slots(ts, S, dcp, acp);
+    const uint32_t base = b.seg_sub_base[s], n = b.seg_nsub[s];
+    uint32_t* const flag = b.piece_mcu0 + base;  // round tags (scratch until chain_counts_wg)
+    // chunks of kStep pieces to check: every chunk in the first round, then only those holding a
+    // piece the round before re-walked, and the chunk after each (its first piece follows the
+    // re-walked chunk's last); chunk ci belongs to wave ci mod kBigWaves
+    if (tid == 0) {
+        s_mask[0] = ~0ull;
+        s_mask[1] = 0ull;
+        s_state = 1u;
+    }
+    uint32_t jerr_all = kNone;  // (tid 0) first piece seen with an error in any round, checked again before use
+    uint32_t rewalks = 0, rounds = 0;
+    bool early = false;
+    for (uint32_t round = 0;; round++) {
         if (tid == 0) {
-            s_mask[0] = ~0ull;
-            s_mask[1] = 0ull;
-            s_state = 1u;
+            s_jmin = kNone;
+            s_jerr = kNone;
+            s_nflag = 0;
         }
         __syncthreads();
-        bool agreed = false;
-        for (uint32_t round = 0; round < kFixRounds && !agreed; round++) {
-            const uint64_t dirty = s_mask[0];
-            const bool dirty_hi = (s_state & 1u) != 0u;
-            bool bad_round = false;  // wave-uniform
-            for (uint32_t ci = wv, j0 = wv * kStep; j0 < n; ci += kBigWaves, j0 += kBigWaves * kStep) {
-                const bool look = ci < 64 ? (((dirty >> ci) & 1u) || (ci > 0 && ((dirty >> (ci - 1)) & 1u)))
-                                          : (dirty_hi || (ci == 64 && (dirty >> 63)));
-                if (!look) continue;  // wave-uniform
-                // piece j0 + 64 t + lane: every load of the wave contiguous
-                uint32_t pend[kFixPer], starts[kFixPer];  // the predecessor's end, the piece's start
-#pragma unroll
-                for (uint32_t t = 0; t < kFixPer; t++) {
-                    const uint32_t j = j0 + 64u * t + lane;
-                    starts[t] = j < n ? ld_wg(b.piece_bit + base + j) : 0u;
-                    pend[t] = (j > 0 && j < n) ? ld_wg(b.piece_end + base + j - 1u) : 0u;
+        const uint64_t dirty = s_mask[0];
+        const bool dirty_hi = (s_state & 1u) != 0u;
+        const uint32_t tag = 0x80000000u | round;  // (an MCU index never has the top bit)
+        auto look = [&](uint32_t ci) {
+            return ci < 64 ? (((dirty >> ci) & 1u) || (ci > 0 && ((dirty >> (ci - 1)) & 1u)))
+                           : (dirty_hi || (ci == 64 && (dirty >> 63)));
+        };
+        // (A) flag the disagreeing pieces of the chunks to check; piece j0 + 64 t + lane (every load
+        // of the wave contiguous)
+        uint32_t nfl = 0;
+        for (uint32_t ci = wv, j0 = wv * kStep; j0 < n; ci += kBigWaves, j0 += kBigWaves * kStep) {
+            if (!look(ci)) continue;  // wave-uniform
+            uint32_t jm = kNone, je = kNone;
+#pragma unroll 4
+            for (uint32_t t = 0; t < kFixPer; t++) {
+                const uint32_t j = j0 + 64u * t + lane;
+                if (j >= n) continue;
+                const uint32_t st = ld_wg(b.piece_bit + base + j);
+                const uint32_t pe = j > 0 ? ld_wg(b.piece_end + base + j - 1u) : 0u;  // piece 0 starts at bit 0
+                if (st != pe) {
+                    flag[j] = tag;
+                    jm = min(jm, j);
+                    nfl++;
                 }
-                uint32_t mis = 0;  // bit t: piece j0 + 64 t + lane disagrees (piece 0 starts at bit 0: always right)
-#pragma unroll
-                for (uint32_t t = 0; t < kFixPer; t++) {
-                    const uint32_t j = j0 + 64u * t + lane;
-                    mis |= (j > 0 && j < n && starts[t] != pend[t]) ? (1u << t) : 0u;
-                }
-                if (!__any(mis != 0u)) continue;  // wave-uniform
-                bad_round = true;
-                if (lane == 0) {
-                    if (ci < 64) atomicOr(&s_mask[1], 1ull << ci);
-                    else atomicOr(&s_state, 2u);
-                }
-#pragma unroll
-                for (uint32_t t = 0; t < kFixPer; t++) {
-                    const bool need = (mis >> t) & 1u;
-                    if (!__any(need)) continue;  // wave-uniform
-                    const uint32_t u = base + j0 + 64u * t + lane;
-                    PieceGeo P{0u, 1u, 0u, 0u, 0u};
-                    if (need) P = piece_geo(b, S, s, u);
-                    redo_piece<false>(b, S, P, s, u, pend[t], luts, dcp, acp, row, ring, rring, need);
-                }
+                if (ld_wg(b.piece_emcu + base + j) < kTailErr) je = min(je, j);
             }
-            if (bad_round && lane == 0) atomicOr(&s_state, 4u);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this round's ends before the next reads
-            __syncthreads();
-            agreed = (s_state & 4u) == 0u;
-            __syncthreads();
-            if (tid == 0) {
-                s_mask[0] = s_mask[1];
-                s_mask[1] = 0ull;
-                s_state = (s_state >> 1) & 1u;
+            jm = __builtin_amdgcn_readfirstlane(wave_min_u32(jm));
+            je = __builtin_amdgcn_readfirstlane(wave_min_u32(je));
+            if (lane == 0) {
+                if (jm != kNone) atomicMin(&s_jmin, jm);
+                if (je != kNone) atomicMin(&s_jerr, je);
             }
-            __syncthreads();
         }
-        if (agreed) {  // the counts, all waves
-            chain_counts_wg(b, s, base, n, S.nblk / S.bpm, seg_is_final(b, s), s_sum, s_jl);
-        } else if (tid == 0) {
-            chain_fix_serial<false>(b, s, S, luts, dcp, acp, row, ring, rring);
+        if (b.stamps) {  // diagnostics (JD_STAMPS): per round, the first flagged piece and how many
+            const uint32_t w = uint32_t(__builtin_amdgcn_readlane(wave_scan_dpp(int(nfl)), 63));
+            if (lane == 0 && w) atomicAdd(&s_nflag, w);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the flags before (B) reads them
+        __syncthreads();
+        const uint32_t jmin = s_jmin;
+        if (b.stamps && tid == 0 && round < 4096u) b.stamps[round] = (uint64_t(jmin) << 32) | s_nflag;
+        if (tid == 0) {
+            jerr_all = min(jerr_all, s_jerr);
+            // a right piece (before the first disagreement) with an error: the counts are exact now
+            // (the piece may have been re-walked since its error was seen: checked again)
+            if (jmin != kNone && jerr_all < jmin) {
+                if (ld_wg(b.piece_emcu + base + jerr_all) < kTailErr) s_state |= 4u;
+                else jerr_all = kNone;
+            }
+        }
+        __syncthreads();
+        rounds = round + 1u;
+        early = (s_state & 4u) != 0u;
+        if (jmin == kNone || early || round > n) break;  // workgroup-uniform (round > n: never, see above)
+        if (b.fix_round_cap && round + 1u >= b.fix_round_cap) {  // diagnostics (JD_FIX_ROUND_CAP): give up
+            rounds = n + 2u;
+            break;
+        }
+        // (B) re-walk every flagged piece whose predecessor is not flagged (from that predecessor's
+        // end: a flagged predecessor's end is likely wrong, and a piece re-walked from it would come
+        // out wrong and poison the next one, as k_redo's rule); the re-walk of the first flagged
+        // piece, whose start is right (the front), goes on into the pieces after it.
+        for (uint32_t ci = wv, j0 = wv * kStep; j0 < n; ci += kBigWaves, j0 += kBigWaves * kStep) {
+            if (!look(ci)) continue;  // wave-uniform
+            for (uint32_t t = 0; t < kFixPer; t++) {
+                const uint32_t j = j0 + 64u * t + lane;
+                bool act = j < n && j > 0 && ld_wg(flag + j) == tag && (j == jmin || ld_wg(flag + j - 1u) != tag);
+                if (!__any(act)) continue;  // wave-uniform
+                const bool front = act && j == jmin;
+                uint32_t cur = j, from = act ? ld_wg(b.piece_end + base + j - 1u) : 0u;
+                while (__any(act)) {
+                    PieceGeo P{0u, 1u, 0u, 0u, 0u};
+                    if (act) P = piece_geo(b, S, s, base + cur);
+                    const uint32_t e = redo_piece<false>(b, S, P, s, base + cur, from, luts, dcp, acp, row, ring, rring, act);
+                    if (act) {
+                        rewalks++;
+                        const uint32_t c = cur / kStep;  // the next round checks this chunk and the one after
+                        if (c < 64) atomicOr(&s_mask[1], 1ull << c);
+                        else atomicOr(&s_state, 2u);
+                        // the front goes on while the next start still disagrees: it stops at an
+                        // error (corrupt data, or trailing bytes: the next round decides), where the
+                        // next start agrees, and at a piece another lane re-walks (flagged, with an
+                        // unflagged predecessor: only the front's own predecessor chain is its own)
+                        const uint32_t nx = cur + 1u;
+                        act = front && nx < n && ld_wg(b.piece_emcu + base + cur) >= kTailErr && ld_wg(b.piece_bit + base + nx) != e &&
+                              !(ld_wg(flag + nx) == tag && ld_wg(flag + cur) != tag);
+                        cur = nx;
+                        from = e;
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this round's ends before the next reads them
+        __syncthreads();
+        if (tid == 0) {
+            s_mask[0] = s_mask[1];
+            s_mask[1] = 0ull;
+            s_state = (s_state >> 1) & 1u;
         }
     }
+    {  // jd_stats: intervals fixed, rounds, pieces re-walked, early stops
+        const uint32_t rw = uint32_t(__builtin_amdgcn_readlane(wave_scan_dpp(int(rewalks)), 63));
+        if (lane == 0 && rw) atomicAdd(&b.counters[kCtrFixRewalks], (unsigned long long)rw);
+        if (tid == 0) {
+            atomicAdd(&b.counters[kCtrFixIntervals], 1ull);
+            atomicAdd(&b.counters[kCtrFixRounds], (unsigned long long)rounds);
+            if (early) atomicAdd(&b.counters[kCtrFixEarly], 1ull);
+        }
+    }
+    if (rounds > n + 1u) {  // (unreachable: every round settles the first disagreement) corrupt, nothing counted
+        for (uint32_t j = tid; j < n; j += kBigThreads) {
+            b.piece_mcu0[base + j] = 0u;
+            b.piece_nmcu[base + j] = 0u;
+        }
+        if (tid == 0) {
+            atomicOr(&b.status[b.seg_img[s]], kStCorrupt);
+            b.seg_fix[s] = 0u;
+        }
+        return;
+    }
+    chain_counts_wg(b, s, base, n, S.nblk / S.bpm, seg_is_final(b, s), s_sum, s_jl);
 }
 
 // k_gather: a piece's block records -> BlockInfo at the blocks' global positions, AC-entry offsets
@@ -4196,7 +4354,7 @@ static hipError_t allow_lds(size_t lds) {
     return hipSuccess;
 }
 
-// The same for k_chain_big's 16-wave workgroups (their lanes' rows and rings beside the tables).
+// The same for k_chain_big's 8-wave workgroups (their lanes' rows and rings beside the tables).
 static hipError_t allow_lds_big(size_t lds) {
     constexpr int kMaxDev = 64;
     static std::mutex m;
@@ -4244,6 +4402,7 @@ hipError_t launch_kernel(int k, const BatchDev& b, hipStream_t s) {
                 hipLaunchKernelGGL(k_piece<64>, dim3(b.nsub / 64), dim3(64), piece_lds_bytes(b.max_slots, 64), s, b);
             break;
         case 5:
+            if (b.skip_redo) break;  // (diagnostics)
             if (b.nsub && (b.big_chain || b.small_fold))
                 hipLaunchKernelGGL(k_redo<true>, dim3(b.nsub / kRedoThreads), dim3(kRedoThreads),
                                    size_t(b.max_slots) * sizeof(HuffLut) + kRedoLds, s, b);

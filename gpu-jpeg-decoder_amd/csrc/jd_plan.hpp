@@ -44,9 +44,9 @@ inline uint32_t image_segments(const jd_header& h) {
 // Piece size of a batch of ecs_bits entropy-coded bits (jd_runtime.cpp build_plan): kPieceBits,
 // halved (down to kMinPieceBits) while the batch would have fewer than kPieceTarget pieces.  It
 // grows with the batch, so an image's own bits give a lower bound for any batch holding it.
-inline uint32_t adaptive_piece_bits(uint64_t ecs_bits) {
+inline uint32_t adaptive_piece_bits(uint64_t ecs_bits, uint32_t pmin = kMinPieceBits) {
     uint32_t p = kPieceBits;
-    while (p > kMinPieceBits && ecs_bits / p < kPieceTarget) p >>= 1;
+    while (p > pmin && ecs_bits / p < kPieceTarget) p >>= 1;
     return p;
 }
 

@@ -167,7 +167,7 @@ struct Slot {
 
 // One launched batch whose results are not collected yet.  jd_decode_batch_async returns with the
 // newest async_depth launches in flight: 1 by default (the previous launch is collected before the
-// call returns); with JD_ASYNC_DEPTH=2 the host parses, plans and enqueues batch k+2 on its slot's
+// call returns); with JD_FLAG_ASYNC_DEPTH2 the host parses, plans and enqueues batch k+2 on its slot's
 // stream (behind batch k) before it waits for batch k.  That starts batch k+2's front-end the
 // moment batch k ends, but the two slots' walks then often run together, and the step measured
 // 3-4 % slower.
@@ -221,12 +221,13 @@ struct jd_ctx {
     Pending pend[kNumPending];
     int slot = 0;                        // the slot the next launch uses
     uint64_t seq = 0;                    // launches so far (the next launch's record: pend[seq % kNumPending])
-    int async_depth = 1;                 // batches jd_decode_batch_async leaves in flight (JD_ASYNC_DEPTH: 1 or 2)
+    int async_depth = 1;                 // batches jd_decode_batch_async leaves in flight (2: JD_FLAG_ASYNC_DEPTH2)
     const void* last_stream = nullptr;  // caller stream of the pending launches (nullptr: the slots' own)
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     int max_batch_images = 0;           // items per launched sub-batch (JD_MAX_BATCH_IMAGES)
     int64_t spare_pieces = -1;          // spare re-walk regions per image (JD_SPARE_PIECES; -1: default)
     int64_t piece_overlap = -1;         // warm-up bits (JD_PIECE_OVERLAP_BITS; -1: default)
+    uint32_t min_piece_bits = kMinPieceBits;  // small batches' shortest pieces (JD_MIN_PIECE_BITS: a test knob)
     bool fixed_pieces = false;          // JD_FIXED_PIECES: keep the host's piece size (no k_pieceplan)
     size_t stage_chunk = size_t(128) << 20;  // host-input H2D chunk (JD_STAGE_CHUNK_MB; 0: one copy per batch)
     bool stage_nt = true;                     // streaming-store staging copy (JD_STAGE_NT=0: memcpy)
@@ -424,7 +425,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
         const uint32_t pmin = (ctx->flags & JD_FLAG_FORCE_SYNC)    ? 1024u
                               : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u
                               : (ctx->flags & JD_FLAG_FULL_PIECES) ? kPieceBits
-                                                                   : adaptive_piece_bits(ecs_img * 8);
+                                                                   : adaptive_piece_bits(ecs_img * 8, ctx->min_piece_bits);
         const bool forced = (ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES | JD_FLAG_FULL_PIECES)) != 0;
         if (!image_fits(ecs_img, h, pmin, forced ? pmin : kPieceBits, ctx->spare_pieces, region_divisor(pj))) {
             ctx->pst[it] = JD_ERR_CAPACITY;
@@ -565,7 +566,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     // single-image latency falls with the piece size while the overlap (sync distance) is fixed.
     uint64_t ecs_bits = 0;
     for (const ImgDesc& d : P.imgs) ecs_bits += uint64_t(d.len - d.ecs_off) * 8;
-    const uint32_t adaptive = (ctx->flags & JD_FLAG_FULL_PIECES) ? kPieceBits : adaptive_piece_bits(ecs_bits);
+    const uint32_t adaptive = (ctx->flags & JD_FLAG_FULL_PIECES) ? kPieceBits : adaptive_piece_bits(ecs_bits, ctx->min_piece_bits);
     P.piece_bits = (ctx->flags & JD_FLAG_FORCE_SYNC) ? 1024u : (ctx->flags & JD_FLAG_FORCE_LANES) ? 0x40000000u : adaptive;
     // shorter pieces also get a shorter warm-up: a lane that has not synchronised by then is
     // re-walked (k_redo / k_chain_big), which costs less than every lane walking 4096 extra bits.
@@ -848,7 +849,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_chts = put(blob, P.chain_wg_tableset);
         const size_t o_modes = put(blob, P.mode_imgs);
         const size_t o_status = put(blob, std::vector<uint32_t>(nimg, 0));
-        const size_t o_ctr = put(blob, std::vector<unsigned long long>(4, 0));  // BatchDev::counters
+        const size_t o_ctr = put(blob, std::vector<unsigned long long>(kNumCounters, 0));  // BatchDev::counters
         const size_t o_tscur = put(blob, P.ts_slot0);
         const size_t o_order = put(blob, P.img_order);
         const size_t upload = blob.size();
@@ -966,6 +967,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         }
         b.fancy = fancy ? 1u : 0u;
         b.max_fancy_wgs = max_fancy_wgs;
+        if (const char* e = std::getenv("JD_FIX_ROUND_CAP")) b.fix_round_cap = uint32_t(std::strtoul(e, nullptr, 0));
+        b.skip_redo = std::getenv("JD_SKIP_REDO") ? 1u : 0u;
 
         ctx->last = b;
         ctx->last_blocks = P.total_blocks;
@@ -1004,9 +1007,10 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             for (int k = 0; k < JD_NUM_KERNELS; k++) std::fprintf(stderr, " %.3f", t_k[k]);
             std::fprintf(stderr, "\n");
         }
-        HIPCHK(ctx, ensure_pinned(pd.host, pd.host_cap, 32 + size_t(nimg) * 4));
-        HIPCHK(ctx, hipMemcpyAsync(pd.host, b.counters, 32, hipMemcpyDeviceToHost, s));
-        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(pd.host) + 32, b.status, nimg * 4, hipMemcpyDeviceToHost, s));
+        constexpr size_t kCtrBytes = kNumCounters * 8;
+        HIPCHK(ctx, ensure_pinned(pd.host, pd.host_cap, kCtrBytes + size_t(nimg) * 4));
+        HIPCHK(ctx, hipMemcpyAsync(pd.host, b.counters, kCtrBytes, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(pd.host) + kCtrBytes, b.status, nimg * 4, hipMemcpyDeviceToHost, s));
         pd.timing = timing;
         pd.fancy = fancy;
         pd.blocks = double(P.total_blocks);
@@ -1058,7 +1062,7 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
     const uint32_t nimg = pd.nimg;
     if (nimg) {
         const unsigned long long* ctr = static_cast<const unsigned long long*>(pd.host);
-        const uint32_t* status = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pd.host) + 32);
+        const uint32_t* status = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pd.host) + kNumCounters * 8);
         for (uint32_t i = 0; i < nimg; i++)
             if (status[i]) pd.pst[size_t(pd.item_of_img[i] - pd.lo)] = JD_ERR_CORRUPT;
         if (ctx->host_timing)
@@ -1107,6 +1111,11 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
         S.blocks += blocks;
         S.segments += nsegd;
         S.subsequences += nsubd;
+        S.redo_pieces += double(ctr[kCtrRedo]);
+        S.fix_intervals += double(ctr[kCtrFixIntervals]);
+        S.fix_rounds += double(ctr[kCtrFixRounds]);
+        S.fix_rewalks += double(ctr[kCtrFixRewalks]);
+        S.fix_early += double(ctr[kCtrFixEarly]);
     }
     for (int i = pd.lo; i < pd.hi; i++) {
         const jd_status st = pd.pst[size_t(i - pd.lo)];
@@ -1202,9 +1211,13 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_SPARE_PIECES")) ctx->spare_pieces = std::strtoll(e, nullptr, 0);
     if (const char* e = std::getenv("JD_FIXED_PIECES")) ctx->fixed_pieces = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_PIECE_OVERLAP_BITS")) ctx->piece_overlap = std::strtoll(e, nullptr, 0);
+    if (const char* e = std::getenv("JD_MIN_PIECE_BITS")) {  // a power of two in [64, kPieceBits]
+        const long long v = std::strtoll(e, nullptr, 0);
+        if (v >= 64 && v <= kPieceBits && (v & (v - 1)) == 0) ctx->min_piece_bits = uint32_t(v);
+    }
     if (const char* e = std::getenv("JD_STAGE_NT")) ctx->stage_nt = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_H2D_SERIAL")) ctx->h2d_serial = std::strtoll(e, nullptr, 0) != 0;
-    if (const char* e = std::getenv("JD_ASYNC_DEPTH")) ctx->async_depth = std::strtoll(e, nullptr, 0) == 2 ? 2 : 1;
+    ctx->async_depth = (ctx->flags & JD_FLAG_ASYNC_DEPTH2) ? 2 : 1;  // an explicit opt-in
     if (const char* e = std::getenv("JD_STAGE_CHUNK_MB")) {
         const long long mb = std::strtoll(e, nullptr, 0);
         ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);

@@ -33,8 +33,9 @@ JD_FLAG_FORCE_SYNC = 2
 JD_FLAG_FORCE_LANES = 4
 JD_FLAG_FANCY_UPSAMPLING = 8
 JD_FLAG_FULL_PIECES = 16
+JD_FLAG_ASYNC_DEPTH2 = 32
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES, "full": JD_FLAG_FULL_PIECES}
-JD_ABI_VERSION = 6
+JD_ABI_VERSION = 7
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece", "k_redo", "k_chain",
                 "k_gather", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
@@ -75,7 +76,9 @@ class _Stats(ctypes.Structure):
                 ("images", ctypes.c_double), ("pixels", ctypes.c_double), ("ecs_bytes", ctypes.c_double),
                 ("blocks", ctypes.c_double), ("segments", ctypes.c_double), ("subsequences", ctypes.c_double),
                 ("host_ms", ctypes.c_double * 4), ("h2d_bytes", ctypes.c_double),
-                ("h2d_registered_bytes", ctypes.c_double)]
+                ("h2d_registered_bytes", ctypes.c_double), ("redo_pieces", ctypes.c_double),
+                ("fix_intervals", ctypes.c_double), ("fix_rounds", ctypes.c_double), ("fix_rewalks", ctypes.c_double),
+                ("fix_early", ctypes.c_double)]
 
 
 # Every symbol include/jd.h and include/jd_test.h declare (checked by tests/test_abi.py).
@@ -253,9 +256,12 @@ class Decoder:
     (cuda-decoder/src/parser.cu:324-358, 577-700) as a context object."""
 
     def __init__(self, device: int = 0, timing: bool = False, parse_threads: int = 0, path: str = "auto",
-                 fancy: bool = False):
+                 fancy: bool = False, async_depth: int = 1):
         """fancy=True: libjpeg's triangular chroma upsampling instead of replication
-        (JD_FLAG_FANCY_UPSAMPLING; an option beyond the reference, see include/jd.h)."""
+        (JD_FLAG_FANCY_UPSAMPLING; an option beyond the reference, see include/jd.h).
+        async_depth=2: pipelined calls leave two batches in flight (JD_FLAG_ASYNC_DEPTH2)."""
+        if async_depth not in (1, 2):
+            raise ValueError("async_depth: 1 or 2")
         self.lib = load_library()
         abi = self.lib.jd_abi_version()
         if abi != JD_ABI_VERSION:
@@ -264,8 +270,8 @@ class Decoder:
             warnings.warn(f"libjdamd ABI {abi} != {JD_ABI_VERSION}: loaded anyway (JDAMD_ALLOW_ABI_MISMATCH=1)")
         self._arenas = {}  # pointer -> registered numpy arena (kept alive while registered)
         self.ctx = ctypes.c_void_p()
-        opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path] | (JD_FLAG_FANCY_UPSAMPLING if fancy else 0),
-                     parse_threads)
+        opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path] | (JD_FLAG_FANCY_UPSAMPLING if fancy else 0) |
+                     (JD_FLAG_ASYNC_DEPTH2 if async_depth == 2 else 0), parse_threads)
         st = self.lib.jd_ctx_create(ctypes.byref(self.ctx), device, ctypes.byref(opts))
         if st != JD_OK:
             raise JDError(st, "jd_ctx_create")
@@ -428,6 +434,10 @@ class Decoder:
             "host_ms": {"parse": s.host_ms[0], "plan": s.host_ms[1], "stage_inputs": s.host_ms[2],
                         "wait": s.host_ms[3]},
             "h2d_bytes": s.h2d_bytes, "h2d_registered_bytes": s.h2d_registered_bytes,
+            # speculative decode: k_redo's re-walks; intervals k_chain_fix / k_chain_big fixed, their
+            # rounds, re-walked pieces, early stops
+            "redo_pieces": s.redo_pieces, "fix_intervals": s.fix_intervals, "fix_rounds": s.fix_rounds,
+            "fix_rewalks": s.fix_rewalks, "fix_early": s.fix_early,
         }
 
     def device_bytes(self):

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define JD_ABI_VERSION 6
+#define JD_ABI_VERSION 7
 
 typedef enum jd_status {
     JD_OK = 0,
@@ -59,6 +59,11 @@ typedef struct jd_ctx jd_ctx;
  * libjpeg's triangular "fancy" filter for 2x1, 2x2 and 1x2 ratios (closer to libjpeg-turbo /
  * Pillow output; an option beyond the reference, which has no subsampled chroma at all). */
 #define JD_FLAG_FANCY_UPSAMPLING 8u
+/* jd_decode_batch_async leaves two batches in flight instead of one: a call collects the batch
+ * launched two calls before it, so results[], rgb and jpeg_dev buffers of batch k stay in use until
+ * call k + 2 returns (or jd_decode_wait).  Measured 3-4 % slower on the bench configs (DESIGN.md
+ * §4.5); an explicit opt-in because it changes when a caller may reuse those buffers. */
+#define JD_FLAG_ASYNC_DEPTH2 32u
 
 typedef struct jd_opts {
     unsigned flags;
@@ -137,7 +142,7 @@ jd_status jd_decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* r
  * uploaded by an H2D on that slot's stream, which overlaps the other slot's kernels.  results[],
  * the rgb buffers and the jpeg_dev buffers must stay valid and unused by other calls until the
  * batch is collected: by the next jd_decode_batch_async call (the second next with
- * JD_ASYNC_DEPTH=2, which leaves two batches in flight), by a jd_decode_batch call, or by
+ * JD_FLAG_ASYNC_DEPTH2, which leaves two batches in flight), by a jd_decode_batch call, or by
  * jd_decode_wait; host jpeg buffers only until the call returns, unless they lie in a range
  * registered with jd_host_register (then until the batch is collected). */
 jd_status jd_decode_batch_async(jd_ctx* ctx, const jd_item* items, int n, jd_result* results,
@@ -198,6 +203,11 @@ typedef struct jd_stats {
     double host_ms[4];
     double h2d_bytes; /* host-memory input bytes uploaded */
     double h2d_registered_bytes; /* file bytes uploaded straight from registered ranges (no staging copy) */
+    /* speculative decode: pieces k_redo re-walked; intervals whose starts still
+     * disagreed after it (k_chain_fix / k_chain_big), their re-walk rounds and re-walked pieces, and
+     * the k_chain_big intervals that stopped early at a right piece with an error (corrupt data or
+     * trailing bytes) */
+    double redo_pieces, fix_intervals, fix_rounds, fix_rewalks, fix_early;
 } jd_stats;
 jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out);
 jd_status jd_reset_stats(jd_ctx* ctx);

@@ -202,14 +202,13 @@ def test_mutated_files_batch_matches_oracle_status_and_pixels():
 
 
 @pytest.mark.parametrize("depth", [1, 2])
-def test_async_depth_results_and_pixels(monkeypatch, depth):
-    """jd_decode_batch_async with one or two batches left in flight (JD_ASYNC_DEPTH): after call k
-    returns, batch k - depth is collected (its results filled); host-staged and device inputs
-    alternate, every image bit-exact after jd_decode_wait."""
-    monkeypatch.setenv("JD_ASYNC_DEPTH", str(depth))
+def test_async_depth_results_and_pixels(depth):
+    """jd_decode_batch_async with one or two batches left in flight (JD_FLAG_ASYNC_DEPTH2, an
+    explicit opt-in: ADVICE r05): after call k returns, batch k - depth is collected (its results
+    filled); host-staged and device inputs alternate, every image bit-exact after jd_decode_wait."""
     sets = [jd_synth.make_batch(6, 640 + 64 * k, 360, 90, ("4:2:0", "4:4:4", "4:2:2")[k % 3], k % 2, 0,
                                 seed0=9700 + 20 * k) for k in range(5)]
-    dec = jdamd.Decoder(0)
+    dec = jdamd.Decoder(0, async_depth=depth)
     try:
         runs = []
         for k, datas in enumerate(sets):

@@ -133,9 +133,9 @@ def test_dense_streams_without_spare_regions(monkeypatch, dense_batch, path):
 @pytest.mark.parametrize("overlap,spare", [("1024", "default"), ("256", "default"), ("64", "0")])
 def test_big_interval_rounds_vs_oracle(monkeypatch, overlap, spare):
     """One image without DRI in a batch of its own: a single interval of ~45 K 512-bit pieces, which
-    k_chain leaves to k_chain_big (wave-parallel re-walk rounds, then the counts by prefix sums).
-    A short warm-up makes runs of consecutive failed starts (several rounds); with a 64-bit warm-up
-    and no spare regions the runs outlast kFixRounds and the serial walk finishes the interval."""
+    k_chain leaves to k_chain_big (re-walk rounds, then the counts by prefix sums).  A short warm-up
+    makes runs of consecutive failed starts; with a 64-bit warm-up and no spare regions (no joins)
+    they are long, and each is re-walked by one lane in one round (there is no serial fallback)."""
     import bench
 
     (data,) = jd_synth.make_images(bench.ref444_jobs([bench.REF_SIZES.index(2000)], 95), workers=1)
@@ -150,6 +150,86 @@ def test_big_interval_rounds_vs_oracle(monkeypatch, overlap, spare):
         nsub = int((dec.debug_fetch("sub_seg") != 0xFFFFFFFF).sum())
         assert nsub > 4096  # one interval of thousands of pieces (kBigInterval = 256)
         assert np.array_equal(out, ref)
+        s = dec.stats()
+        assert s["redo_pieces"] > 0 and s["fix_early"] == 0  # (a valid image: no early stop)
+    finally:
+        dec.close()
+
+
+def _decode_timed(dec, data, reps=3):
+    """(pixels, best wall time in s) of `reps` blocking decodes after one untimed decode (pools)."""
+    import time
+    out = dec.decode(data)
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = dec.decode(data)
+        best = min(best, time.perf_counter() - t0)
+    return out, best
+
+
+def test_big_interval_short_pieces_bounded(monkeypatch):
+    """the geometry of round 5's silent latency run (r05ac, a variant build):
+    256-bit pieces with a 768-bit warm-up on the 2 000 x 2 000 4:4:4 q95 image, ~136 K pieces in
+    one interval, most speculative starts wrong.  k_chain_big then stopped after 32 rounds and one
+    lane walked the whole interval.  Now every run of disagreeing pieces is re-walked by one lane in
+    a round: parity with the oracle, the rounds counted (jd_stats), and a wall bound."""
+    import bench
+
+    (data,) = jd_synth.make_images(bench.ref444_jobs([bench.REF_SIZES.index(2000)], 95), workers=1)
+    st, ref = jdoracle.decode(data)
+    assert st == 0
+    monkeypatch.setenv("JD_MIN_PIECE_BITS", "256")
+    monkeypatch.setenv("JD_PIECE_OVERLAP_BITS", "768")
+    dec = jdamd.Decoder(0)
+    try:
+        dec.reset_stats()
+        out, wall = _decode_timed(dec, data)
+        nsub = int((dec.debug_fetch("sub_seg") != 0xFFFFFFFF).sum())
+        s = dec.stats()
+        per = {k: s[k] / s["batches"] for k in ("redo_pieces", "fix_intervals", "fix_rounds", "fix_rewalks", "fix_early")}
+        print(f"\n2000^2 4:4:4 q95, 256-bit pieces, 768-bit warm-up: {nsub} pieces, {wall * 1e3:.2f} ms, per decode {per}")
+        assert nsub > 80_000
+        assert np.array_equal(out, ref)
+        assert per["fix_early"] == 0
+        assert wall < 0.020
+    finally:
+        dec.close()
+
+
+@pytest.mark.parametrize("damage", ["ones", "truncate"])
+def test_big_interval_corrupt_bounded(monkeypatch, damage):
+    """a corrupt image without DRI in a batch of its own (one interval of tens of
+    thousands of short pieces).  Past the damage no start agrees with anything, so k_chain_big's
+    rounds would chase garbage; they stop at the first right piece with an error instead.  The
+    status must be the oracle's, and the decode must stay within a wall bound."""
+    import bench
+
+    (data,) = jd_synth.make_images(bench.ref444_jobs([bench.REF_SIZES.index(2000)], 95), workers=1)
+    h = jdamd.parse(data)
+    b = bytearray(data)
+    if damage == "ones":  # 256 one-bits (stuffed FF bytes) mid-scan: no Huffman code is all ones
+        m = h.ecs_offset + (len(b) - h.ecs_offset) // 2
+        b[m:m + 64] = b"\xff\x00" * 32
+    else:  # the scan cut at two thirds, EOI appended
+        b = b[: h.ecs_offset + 2 * (len(b) - h.ecs_offset) // 3] + b"\xff\xd9"
+    data = bytes(b)
+    st, _ = jdoracle.decode(data)
+    monkeypatch.setenv("JD_PIECE_OVERLAP_BITS", "256")  # many failed starts
+    dec = jdamd.Decoder(0)
+    try:
+        import time
+        _, status = dec.decode_batch([data])  # (pools)
+        assert status == [st] and st == jdamd.JD_ERR_CORRUPT
+        dec.reset_stats()
+        t0 = time.perf_counter()
+        _, status = dec.decode_batch([data])
+        wall = time.perf_counter() - t0
+        s = dec.stats()
+        print(f"\ncorrupt ({damage}): {wall * 1e3:.2f} ms, rounds {s['fix_rounds']:.0f}, early stops {s['fix_early']:.0f}, "
+              f"re-walks {s['fix_rewalks']:.0f} + {s['redo_pieces']:.0f}")
+        assert status == [st]
+        assert wall < 0.050
     finally:
         dec.close()
 

@@ -251,6 +251,19 @@ def test_piece_decode_emulation_matches_oracle(golden):
     assert rescans > 0  # the verification/re-scan path was exercised
 
 
+def test_piece_decode_pieces_shorter_than_an_mcu():
+    """Pieces shorter than an MCU (4:4:4 q98 MCUs take hundreds of bits): a piece in whose share no
+    MCU begins is empty (its end is its start, the next piece's start), so the chain still agrees
+    and the decode is unchanged (jd_kernels.hip walk_piece, the `W.start >= W.stop_at` case)."""
+    import jd_synth
+
+    data = jd_synth.encode(jd_synth.synth_pixels(96, 64, 3), 98, "4:4:4")
+    ref, _ = jd_trace.emulate(data, 8192, 4096)
+    for piece, overlap in [(64, 128), (200, 0), (32, 32)]:
+        blocks, _ = jd_trace.emulate(data, piece, overlap)
+        assert blocks == ref, (piece, overlap)
+
+
 def test_corrupt_and_unsupported_statuses():
     with open(os.path.join(ROOT, "tests", "golden", "ref", "5_200x200.jpg"), "rb") as f:
         d = f.read()

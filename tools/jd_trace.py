@@ -262,7 +262,7 @@ def _walk_scan(t, pattern, val, total, bits, start, warm_to, stop_at):
     counting = warm_to == start
     m_start = start if counting else None
     mcus = ents = 0
-    if counting and start + 8 > bits:  # starts at the data end: an empty piece
+    if counting and (start + 8 > bits or start >= stop_at):  # at the data end / past its share: empty
         return start, start, 0, 0
     while True:
         r = _symbol(t, pattern, val, total, p, bi, k)
@@ -276,7 +276,7 @@ def _walk_scan(t, pattern, val, total, bits, start, warm_to, stop_at):
             bi = (bi + 1) % len(pattern)
         if not counting and mcu_end and p >= warm_to:
             counting, m_start = True, p
-            if p + 8 > bits:
+            if p + 8 > bits or p >= stop_at:  # no MCU begins in the piece's share: empty
                 return m_start, p, 0, 0
         elif counting and mcu_end:
             mcus += 1
