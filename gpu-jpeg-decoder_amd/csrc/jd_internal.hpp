@@ -318,7 +318,7 @@ struct BatchDev {
     uint32_t piece_bits, piece_overlap;
     uint32_t piece_plan;          // k_pieceplan: resident piece lanes (0: use piece_bits as is)
     uint32_t* seg_ent;            // k_subplan: first region word of each segment's pieces (image-relative)
-    uint32_t* img_pool;           // k_subplan: next free region word of each image (re-walk regions)
+    unsigned long long* img_pool; // k_subplan: next free region word of each image (re-walk regions; 64-bit: never wraps)
     uint32_t no_pool;             // 1: re-walks always write over their own region (tests, JD_SPARE_PIECES=0)
     uint32_t* piece_bit;          // first bit of the piece (an MCU boundary; kNoPiece: none found)
     uint32_t* piece_end;          // first MCU boundary at/after the piece's nominal end (or data end)

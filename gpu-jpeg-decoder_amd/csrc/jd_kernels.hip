@@ -879,7 +879,7 @@ __device__ void subplan_image(const BatchDev& b, uint32_t img, int lane) {
         run += uint32_t(__shfl(int(incl), 63, 64));
         wrun += uint32_t(__shfl(int(wincl), 63, 64));
     }
-    if (lane == 0) b.img_pool[img] = wrun;
+    if (lane == 0) b.img_pool[img] = wrun;  // (64-bit)
 }
 __global__ __launch_bounds__(64) void k_subplan(BatchDev b) {
     JD_PRIO_SHORT();
@@ -1697,13 +1697,9 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
         stail = pj >> 24;
         tot = cp[kCpMax];
         const uint32_t img = b.seg_img[s];
-        const uint32_t cap = b.imgs[img].entry_cap;
-        // (the cursor is only advanced while it is below the cap: many rounds of re-walks would
-        // otherwise wrap it past 2^32 and hand out regions that overlap the image's pieces)
-        const uint32_t a = (b.no_pool || __hip_atomic_load(&b.img_pool[img], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cap)
-                               ? 0xFFFFFFFFu
-                               : atomicAdd(&b.img_pool[img], P.rw);
-        if (uint64_t(a) + P.rw <= cap) base = a;
+        // (a 64-bit cursor: many rounds of re-walks cannot wrap it into the image's own pieces)
+        const unsigned long long a = b.no_pool ? 0ull : atomicAdd(&b.img_pool[img], (unsigned long long)P.rw);
+        if (!b.no_pool && a + P.rw <= b.imgs[img].entry_cap) base = uint32_t(a);
         else ncp = 0;  // in place
     }
 #pragma unroll
@@ -1743,19 +1739,19 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
 }
 
 // Lane per piece: re-walk, all at once, every piece whose speculative start disagrees with its
-// predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images)
-// while that predecessor itself agrees with its own: starting from that end is then exact when the
-// predecessor is right.  A piece whose predecessor disagrees too waits for the next round: re-walked
-// from an end that is likely wrong, it would come out wrong, and its successor re-walked from it
-// next (r06 measured that cascade: with most starts failed, k_chain_big then needed thousands of
-// rounds).  Up to kRedoRounds rounds per workgroup, each only while some lane of the workgroup still
-// has work; a lane's predecessor may belong to another workgroup, whose rounds run at the same time,
-// so what is left, k_chain finds.  A run of r failed starts takes r rounds.
+// predecessor's end (about 0.6 % of 8192-bit pieces with a 4096-bit overlap on the bench images).
+// Starting from that end is exact when the predecessor is right; a predecessor re-walked in the same
+// round mostly joins its speculative walk and keeps its end, and otherwise the piece disagrees again.
+// Small batches (LT: short pieces, where runs of failed starts are common) go on for up to
+// kRedoRounds rounds, each only while some lane of the workgroup still has work, and from the second
+// round re-walk only a piece whose predecessor now agrees with its own (re-walked from an end that
+// is likely wrong, it would come out wrong again).  A lane's predecessor may belong to another
+// workgroup, whose rounds run at the same time, so what is left, k_chain finds.
 // LT: the table set staged in LDS (small batches, BatchDev::big_chain or small_fold: the re-walks'
 // lookups are a serial chain, ~1 us each from global memory); else read from global memory, so the
 // workgroups need little LDS and fit beside the other batch's big kernels.
 constexpr uint32_t kRedoRoundsLT = 16;  // small batches: short pieces, runs of failed starts are common
-constexpr uint32_t kRedoRoundsBig = 2;  // large batches: the second round takes the rare double failure
+constexpr uint32_t kRedoRoundsBig = 1;  // large batches: double failures are rare (k_chain finds them)
 template <bool LT>
 __global__ __launch_bounds__(kRedoThreads, (!LT && kRewalkDirect) ? 8 : 1) void k_redo(BatchDev b) {
     JD_PRIO_CRIT();
@@ -1786,7 +1782,7 @@ __global__ __launch_bounds__(kRedoThreads, (!LT && kRewalkDirect) ? 8 : 1) void 
         return pd;
     };
     if (__ballot(dis) == 0) return;  // wave-uniform (one wave per workgroup)
-    bool need = dis && !pred_dis(false);
+    bool need = dis;  // the first round: every disagreeing start (most predecessors re-walked with it join their speculative walk and keep their end)
     uint64_t needm = __ballot(need);
     // the piece workgroup (kPieceThreads lanes, one table set) this one is part of
     const TableSet& ts = b.tablesets[b.wg_tableset[(blockIdx.x * kRedoThreads) / kPieceThreads]];
@@ -1796,7 +1792,7 @@ __global__ __launch_bounds__(kRedoThreads, (!LT && kRewalkDirect) ? 8 : 1) void 
     }
     SegInfo S;
     PieceGeo P{0u, 1u, 0u, 0u, 0u};
-    if (valid) {
+    if (kRedoRounds > 1 ? valid : need) {  // (one round: only the lanes with a re-walk)
         seg_info(b, s, S);
         P = piece_geo(b, S, s, u);
     } else {

@@ -864,7 +864,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         const size_t o_sns = reserve(end, nseg * 4);
         const size_t o_subseg = reserve(end, nsub * 4);
         const size_t o_segent = reserve(end, nseg * 4);
-        const size_t o_pool = reserve(end, size_t(nimg) * 4);
+        const size_t o_pool = reserve(end, size_t(nimg) * 8);
         const size_t o_cand = reserve(end, size_t(nimg) * 16 * 4);
         const size_t o_ibase = reserve(end, size_t(nimg) * 4);
         size_t o_piece[9];
@@ -897,7 +897,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.seg_cstart = reinterpret_cast<uint32_t*>(base + o_cstart);
         b.seg_cend = reinterpret_cast<uint32_t*>(base + o_cend);
         b.seg_ent = reinterpret_cast<uint32_t*>(base + o_segent);
-        b.img_pool = reinterpret_cast<uint32_t*>(base + o_pool);
+        b.img_pool = reinterpret_cast<unsigned long long*>(base + o_pool);
         b.nseg = uint32_t(nseg);
         b.seg_sub_base = reinterpret_cast<uint32_t*>(base + o_ssb);
         b.seg_nsub = reinterpret_cast<uint32_t*>(base + o_sns);
