@@ -170,10 +170,12 @@ def _decode_timed(dec, data, reps=3):
 
 def test_big_interval_short_pieces_bounded(monkeypatch):
     """the geometry of round 5's silent latency run (r05ac, a variant build):
-    256-bit pieces with a 768-bit warm-up on the 2 000 x 2 000 4:4:4 q95 image, ~136 K pieces in
-    one interval, most speculative starts wrong.  k_chain_big then stopped after 32 rounds and one
-    lane walked the whole interval.  Now every run of disagreeing pieces is re-walked by one lane in
-    a round: parity with the oracle, the rounds counted (jd_stats), and a wall bound."""
+    256-bit pieces with a 768-bit warm-up on the 2 000 x 2 000 4:4:4 q95 image, ~90 K pieces in one
+    interval.  Its cause: a 4:4:4 q95 MCU takes ~450 bits, more than a piece, and a piece in whose
+    share no MCU begins walked one MCU anyway, so nearly every start after it disagreed and
+    k_chain_big, after 32 rounds, left the interval to one lane.  Such a piece is now empty, and
+    k_chain_big has no serial fallback: parity with the oracle, the rounds counted (jd_stats), and a
+    wall bound."""
     import bench
 
     (data,) = jd_synth.make_images(bench.ref444_jobs([bench.REF_SIZES.index(2000)], 95), workers=1)
@@ -192,6 +194,7 @@ def test_big_interval_short_pieces_bounded(monkeypatch):
         assert nsub > 80_000
         assert np.array_equal(out, ref)
         assert per["fix_early"] == 0
+        assert per["fix_rounds"] <= 32
         assert wall < 0.020
     finally:
         dec.close()
