@@ -961,6 +961,9 @@ def main():
             "per_rank": per_rank_table(allc, args.steps),
             "device_memory": {"decoder_pools_peak_GB": dec.device_bytes()[1] / 1e9,
                               "torch_peak_GB": torch.cuda.max_memory_allocated(dev) / 1e9,
+                              "pools": "optimistic (default; an image that overflows one is decoded again "
+                                       "with worst-case pools: include/jd.h JD_FLAG_WORST_CASE_POOLS)",
+                              "retried_images_timed": st_overlap["retried_images"],
                               "note": "rank 0: the library's grow-only pools (two in-flight slots) and the "
                                       "bench's own input/output buffers"},
             "cpu_baseline": cpu,

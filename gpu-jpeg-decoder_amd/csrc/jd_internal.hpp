@@ -137,8 +137,10 @@ struct alignas(16) ImgDesc {
     uint32_t entry_cap;               // AC-entry slots of this image (entry indices are image-relative):
                                       // its pieces' regions, then spare regions for re-walks
     uint64_t entry_base;              // first AC-entry slot of this image in BatchDev::entries
-    uint32_t rw_div;                  // fewest walk bits per region word (jd_plan.cpp region_divisor)
-    uint32_t rsv_[3];
+    uint32_t rw_div;                  // walk bits per region word the regions are sized for (region_words):
+                                      // jd_plan.cpp region_divisor (worst case) or kOptRegionDiv
+    uint32_t rw_slack;                // region words per piece beyond plen / rw_div (region_words)
+    uint32_t rsv_[2];
 };
 static_assert(sizeof(ImgDesc) % 16 == 0, "ImgDesc must stay 16-byte aligned");
 
@@ -208,6 +210,7 @@ constexpr int kScanThreads = 256;
 constexpr int kScanBytesPerThread = 64;
 constexpr int kScanChunk = kScanThreads * kScanBytesPerThread;
 constexpr int kScanCap = kScanChunk / 2;  // a break takes 2 bytes: a chunk cannot hold more
+constexpr uint32_t kBrkSlack = 16;        // optimistic break slots beyond the batch's most intervals
 static_assert(kScanChunk <= 16384, "Break: 14-bit chunk offsets and drop counts");
 
 #ifndef JD_CP_MAX
@@ -243,13 +246,21 @@ constexpr uint32_t kTailErr = kNoError - 15u;
 // straddles the piece's end (<= 10 blocks x 64) and one window round past the data end (<= 272), see
 // jd_kernels.hip walk_piece, whose region guard stops a walk (as an error) before it could overrun.
 constexpr uint32_t kRegionSlack = 1040;
+// Optimistic regions (the default plan): sized for kOptRegionDiv walk bits per word
+// (C2's streams average 13), with a slack of the image's own largest MCU (64 words a block) plus one
+// window round (kRoundItemsMax).  A walk whose region fills up stops at the region guard and flags
+// its image kStOverflow; the host then decodes that image again with the worst-case plan
+// (jd_runtime.cpp run_retries), so a dense stream costs time, never correctness.
+constexpr uint32_t kOptRegionDiv = 8u;
+constexpr uint32_t kRoundItemsMax = 152u;  // >= jd_kernels.hip kRoundItems (static_assert there)
+JD_HD inline uint32_t opt_region_slack(uint32_t bpm) { return 64u * bpm + kRoundItemsMax + 8u; }
 // Entry quads are stored in pairs (32 bytes, one HBM write granule) into 32-byte aligned regions:
 // a lane's region line stays open for ~60 walk iterations and is written back piecemeal when the
 // L2 (4 MB per XCD, ~32 K lanes each streaming into their own lines) evicts it, each 16-byte quad
 // costing a 32-byte write (C2: k_piece WRITE_SIZE 3.98 -> 2.30 GB per launch).
 constexpr uint32_t kRegionAlign = 8u;  // words
-JD_HD inline uint32_t region_words(uint32_t plen, uint32_t div = 2u) {
-    return ((plen + div - 1u) / div + kRegionSlack + kRegionAlign - 1u) & ~(kRegionAlign - 1u);
+JD_HD inline uint32_t region_words(uint32_t plen, uint32_t div = 2u, uint32_t slack = kRegionSlack) {
+    return ((plen + div - 1u) / div + slack + kRegionAlign - 1u) & ~(kRegionAlign - 1u);
 }
 
 constexpr int kIdctThreads = 64;      // one wave per IDCT/colour tile
@@ -271,6 +282,9 @@ constexpr uint32_t kFancyRowsPerWg = kFancyH * kFancyBands;
 constexpr uint32_t kStCorrupt = 1u;     // bad code / overrun / DC range
 constexpr uint32_t kStRstMissing = 2u;  // fewer RST markers than intervals
 constexpr uint32_t kStRstOrder = 4u;    // RSTn numbering wrong
+constexpr uint32_t kStOverflow = 8u;    // an optimistic pool was too small for the image (a piece region,
+                                        // or a chunk's break list before the ECS end): decode it again
+                                        // with the worst-case plan (jd_runtime.cpp run_retries)
 
 // Per IDCT/colour tile: k_dc_sum's aggregate (sums of the DC differences of components 0..2 after
 // the tile's last interval start, flag = it has one), which k_dc_scan turns into the components'
@@ -343,7 +357,11 @@ struct BatchDev {
     uint32_t* chunk_nbrk;         // breaks per chunk
     uint32_t* chunk_drops;        // stuffed zero bytes per chunk
     uint32_t* chunk_coff;         // un-stuffed offset of each chunk's first byte
-    Break* chunk_brk;             // kScanCap per chunk
+    Break* chunk_brk;             // brk_cap per chunk
+    uint32_t brk_cap;             // break slots per chunk: kScanCap (worst case), or the batch's most
+                                  // restart intervals + kBrkSlack (every RSTn and the EOI of a valid
+                                  // stream; k_index flags kStOverflow when a chunk before the ECS end
+                                  // held more)
     // outputs
     BlockInfo* blocks;
     uint32_t* entries;

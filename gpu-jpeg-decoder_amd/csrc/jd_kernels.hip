@@ -228,7 +228,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     if (nbrk && interior) {
         // walk the break bits only, in the words that hold one (a word without a break in any lane
         // of the wave costs two instructions); their masks recomputed as in the count pass
-        Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
+        Break* out = b.chunk_brk + size_t(im.chunk_base + c) * b.brk_cap;
+        const uint32_t cap = b.brk_cap;  // (breaks past it are counted, not stored: k_index)
 #pragma unroll
         for (int q = 0; q < 16; q++) {
             if (__any((brkw >> q) & 1u)) {
@@ -252,13 +253,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
                     const uint32_t nbv = k < 3u ? (wc >> (8u * (k + 1u))) & 0xFFu : (q < 15 ? wn & 0xFFu : nextb);
                     const uint32_t dd = d + __builtin_popcount(dm & ((1u << bit) - 1u));
                     const uint32_t is_term = (nbv & 0xF8u) == 0xD0u ? 0u : 1u;
-                    out[off++] = brk_make(threadIdx.x * uint32_t(kScanBytesPerThread) + 4u * q + k, dd, is_term);
+                    if (off < cap) out[off] = brk_make(threadIdx.x * uint32_t(kScanBytesPerThread) + 4u * q + k, dd, is_term);
+                    off++;
                     bm &= bm - 1u;
                 }
             }
         }
     } else if (nbrk) {  // edge threads: byte by byte
-        Break* out = b.chunk_brk + size_t(im.chunk_base + c) * kScanCap;
+        Break* out = b.chunk_brk + size_t(im.chunk_base + c) * b.brk_cap;
         uint32_t d = drop_before;
         reload64(t0, fend, w);
 #pragma unroll 1
@@ -271,12 +273,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
             d += (inr && a > lo && by == 0x00u && pb == 0xFFu) ? 1u : 0u;
             if (inr && a + 1 < fend && by == 0xFFu && nb != 0x00u && nb != 0xFFu) {
                 const uint32_t is_term = (nb & 0xF8u) == 0xD0u ? 0u : 1u;
-                out[off++] = brk_make(threadIdx.x * uint32_t(kScanBytesPerThread) + uint32_t(i), d, is_term);
+                if (off < b.brk_cap) out[off] = brk_make(threadIdx.x * uint32_t(kScanBytesPerThread) + uint32_t(i), d, is_term);
+                off++;
             }
         }
     }
     if (threadIdx.x == 0) {
-        b.chunk_nbrk[im.chunk_base + c] = tot_brk;
+        b.chunk_nbrk[im.chunk_base + c] = tot_brk;  // (all of them: k_index reads at most brk_cap)
         b.chunk_drops[im.chunk_base + c] = tot_drop;
     }
 }
@@ -338,22 +341,34 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
     const uint32_t cb = im.chunk_base, nch = im.nchunks, nseg = im.nseg, sb = im.seg_base;
     const int lane = threadIdx.x;
 
-    // pass A: first terminating marker
-    uint32_t term = 0xFFFFFFFFu;
+    // pass A: first terminating marker.  A chunk may hold more breaks than its brk_cap slots (the
+    // optimistic cap: the batch's most intervals + kBrkSlack); those past the cap were counted, not
+    // stored, and they come after the stored ones in stream order.  They are harmless when the chunk
+    // starts after the first terminator or stored one itself (every later break is ignored); else
+    // the image is flagged kStOverflow and decoded again with kScanCap slots per chunk.
+    const uint32_t cap = b.brk_cap;
+    uint32_t term = 0xFFFFFFFFu, ovf_from = 0xFFFFFFFFu;
     for (uint32_t c0 = 0; c0 < nch; c0 += 64) {
         const uint32_t c = c0 + lane;
         if (c < nch) {
-            const uint32_t n = b.chunk_nbrk[cb + c];
-            const Break* br = b.chunk_brk + size_t(cb + c) * kScanCap;
+            const uint32_t nt = b.chunk_nbrk[cb + c], n = min(nt, cap);
+            const Break* br = b.chunk_brk + size_t(cb + c) * cap;
+            bool has_term = false;
             for (uint32_t j = 0; j < n; j++)
                 if (brk_term(br[j])) {
                     term = min(term, a0 + c * uint32_t(kScanChunk) + brk_rel(br[j]));
+                    has_term = true;
                     break;
                 }
+            if (nt > cap && !has_term) ovf_from = min(ovf_from, a0 + c * uint32_t(kScanChunk));
         }
     }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) term = min(term, uint32_t(__shfl_xor(int(term), d, 64)));
+    for (int d = 32; d >= 1; d >>= 1) {
+        term = min(term, uint32_t(__shfl_xor(int(term), d, 64)));
+        ovf_from = min(ovf_from, uint32_t(__shfl_xor(int(ovf_from), d, 64)));
+    }
+    if (ovf_from < term && lane == 0) atomicOr(&b.status[ii], kStOverflow);
 
     // pass B: offsets and segment boundaries
     uint32_t drops_run = 0, marks_run = 0;
@@ -363,8 +378,8 @@ __global__ __launch_bounds__(64) void k_index(BatchDev b) {
         const uint32_t c = c0 + lane;
         const bool vc = c < nch;
         const uint32_t drops = vc ? b.chunk_drops[cb + c] : 0u;
-        const uint32_t nbrk = vc ? b.chunk_nbrk[cb + c] : 0u;
-        const Break* br = b.chunk_brk + size_t(cb + c) * kScanCap;
+        const uint32_t nbrk = vc ? min(b.chunk_nbrk[cb + c], cap) : 0u;
+        const Break* br = b.chunk_brk + size_t(cb + c) * cap;
         uint32_t nmark = 0;
         const uint32_t cpos0 = a0 + c * uint32_t(kScanChunk);  // file offset of the chunk's first byte
         for (uint32_t j = 0; j < nbrk; j++) nmark += (!brk_term(br[j]) && cpos0 + brk_rel(br[j]) < term) ? 1u : 0u;
@@ -637,7 +652,8 @@ struct SegInfo {
     uintptr_t last;    // last mapped 16-byte chunk of the image's un-stuffed region
     uint32_t ent0;     // first region word of the interval's pieces (image-relative, k_subplan)
     uint32_t pattern, bpm;
-    uint32_t rw_div;   // the image's region divisor (region_words)
+    uint32_t rw_div;   // the image's region divisor and slack (region_words)
+    uint32_t rw_slack;
     uint32_t* eimg;    // the image's AC entries (BatchDev::entries + ImgDesc::entry_base)
 };
 
@@ -666,6 +682,7 @@ __device__ __forceinline__ void seg_info(const BatchDev& b, uint32_t s, SegInfo&
     S.pattern = im.block_pattern;
     S.bpm = im.bpm;
     S.rw_div = im.rw_div;
+    S.rw_slack = im.rw_slack;
 }
 
 // Nominal piece length of an interval cut into npc pieces: equal shares of its bits (at most
@@ -682,6 +699,7 @@ __device__ __forceinline__ void seg_invalid(const BatchDev& b, SegInfo& S) {
     S.pattern = 0;
     S.bpm = 1;
     S.rw_div = 2;
+    S.rw_slack = kRegionSlack;
 }
 
 __device__ __forceinline__ void stage_luts(const BatchDev& b, const TableSet& ts, HuffLut* s_lut, int nthreads) {
@@ -844,7 +862,7 @@ __device__ void subplan_image(const BatchDev& b, uint32_t img, int lane) {
             const uint32_t cs = b.seg_cstart[s], ce = max(cs, b.seg_cend[s]);
             const uint32_t bits = (ce - cs) * 8;
             n = pieces_of(bits, piece_bits);
-            w = n * region_words((bits + n - 1u) / n, im.rw_div);
+            w = n * region_words((bits + n - 1u) / n, im.rw_div, im.rw_slack);
         }
         const uint32_t incl = wave_incl_scan(n), wincl = wave_incl_scan(w);
         const uint32_t off = run + incl - n;
@@ -854,7 +872,7 @@ __device__ void subplan_image(const BatchDev& b, uint32_t img, int lane) {
             b.seg_nsub[s] = n;
             b.seg_ent[s] = wrun + wincl - w;
         }
-        // (wrun <= entry_cap by construction: ECS bits / rw_div + kRegionSlack + 4 words per piece)
+        // (wrun <= entry_cap by construction: ECS bits / rw_div + rw_slack + 4 words per piece)
         const uint32_t m = min(64u, im.nseg - k0);
         for (uint32_t j = 0; j < m; j++) {
             const uint32_t oj = uint32_t(__builtin_amdgcn_readlane(int(off), int(j)));
@@ -907,6 +925,7 @@ static_assert((kRareEvery & (kRareEvery - 1u)) == 0u, "kRareEvery: a power of tw
 // items (entries + block records) one window round can add: every item takes >= 2 bits
 constexpr uint32_t kRoundItems = (kWin * 8 + 31) / 2 + 4;
 static_assert(kRegionSlack >= 640 + kRoundItems + 2, "region slack: straddling MCU + one round past the data");
+static_assert(kRoundItems <= kRoundItemsMax, "opt_region_slack: one round past a region's fill");
 
 constexpr int kRingWords = 8;  // per-lane ring of two entry quads (16-byte aligned)
 // Block records staged four at a time in a per-lane LDS ring and stored as one 16-byte quad (a
@@ -1162,6 +1181,7 @@ struct PWalk {
     uint32_t* reg;
     uint32_t rw;
     uint32_t m_start, m_end, mcus, ents, emcu, ncp, join, tail;
+    uint32_t ovf;               // the region guard stopped the walk (optimistic regions: kStOverflow)
     unsigned long long* stats;  // JD_PSTAT builds
 };
 
@@ -1257,6 +1277,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     // into registers when complete and stored together with the odd quad after it (32 bytes: one
     // HBM write granule); block records go four at a time through their own ring.
     uint32_t fq = 0;  // quads stored so far (regions start on a quad)
+    uint32_t ovf = 0;
     uint32_t st_wit = 0, st_lit = 0, st_rare = 0, st_rare_w = 0, st_rounds = 0, st_mend_w = 0, st_sym = 0;
     // block record k goes to ring word 3 - (k & 3), so that the ring reads as the records' memory
     // order (descending from rec_top); group fr (records 4fr .. 4fr + 3) is stored when complete,
@@ -1452,10 +1473,12 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
             }
             active = false;
         }
-        if (active && (ent2 + 2u) / 4u + blk / kBlkStep + kRoundItems > W.rw) {  // never for a valid stream (region bound)
+        if (active && (ent2 + 2u) / 4u + blk / kBlkStep + kRoundItems > W.rw) {  // worst-case regions: never for a
+                                                                                    // valid stream (region bound)
             m_end = R.bit();
             emcu = min(emcu, mcus);
             active = false;
+            ovf = 1u;
         }
         if (JD_PSTAT) {
             st_wit += wave_max_u32(it);
@@ -1485,6 +1508,7 @@ __device__ __forceinline__ void walk_piece(const SegInfo& S, const uint32_t* s_l
     W.ncp = ncp;
     W.join = join;
     W.tail = errs >> 1;
+    W.ovf = ovf;
     if (JD_PSTAT && KIND == kSpec && W.stats) {
         const uint32_t v[10] = {st_wit, 0u, wave_sum_u32(st_lit), 0u, wave_sum_u32(st_rare),
                                 wave_max_u32(st_rare_w), st_rounds, 1u, wave_max_u32(st_mend_w), wave_sum_u32(st_sym)};
@@ -1589,7 +1613,7 @@ __device__ __forceinline__ PieceGeo piece_geo(const BatchDev& b, const SegInfo& 
     P.j = u - b.seg_sub_base[s];
     P.npc = b.seg_nsub[s];
     P.plen = piece_len(S, P.npc);
-    P.rw = region_words(P.plen, S.rw_div);
+    P.rw = region_words(P.plen, S.rw_div, S.rw_slack);
     P.own = S.ent0 + P.j * P.rw;
     return P;
 }
@@ -1626,6 +1650,7 @@ __device__ __forceinline__ void spec_piece(const BatchDev& b, const SegInfo& S, 
     const uint32_t none[kCpMax] = {};
     walk_piece<kSpec>(S, luts, dcp, acp, row, ring, rring, live, W, cp, max(1u, P.plen / kCpMax), none);
     if (!valid) return;
+    if (W.ovf) atomicOr(&b.status[b.seg_img[b.sub_seg[u]]], kStOverflow);  // (the host decodes it again)
     if (!live) {  // as a warm-up that runs past the data: no piece, an error at its first MCU
         W.m_start = kNoPiece;
         W.m_end = sync_end;
@@ -1712,6 +1737,7 @@ __device__ uint32_t redo_piece(const BatchDev& b, const SegInfo& S, const PieceG
     W.rw = P.rw;
     walk_piece<kRedo, GL, DR>(S, s_lutw, dcp, acp, row, ring, rring, need, W, cp, 0xFFFFFFFFu, cpb);
     if (!need) return 0;
+    if (W.ovf) atomicOr(&b.status[b.seg_img[s]], kStOverflow);
     uint32_t end = W.m_end, mcus = W.mcus, ents = W.ents, emcu = W.emcu, tail = W.tail;
     if (W.join) {  // (checkpoints lie before the last byte: the tail, if any, is the speculative walk's)
         const CpRec c = cp[W.join - 1];

@@ -64,7 +64,7 @@ uint32_t region_divisor(const ParsedJpeg& pj) {
 
 // Fills d (everything but the piece ranges) for item it; pure function of the header + bases.
 void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uint64_t out_addr, const PlanImg& pi,
-               ImgDesc& d) {
+               ImgDesc& d, bool worst) {
     const jd_header& h = pj.hdr;
     memset(&d, 0, sizeof(d));
     d.jpeg = dev_addr;
@@ -124,7 +124,9 @@ void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uin
     d.nchunks = pi.nchunks;  // scan chunks over [align16(file + ecs_off), file + len)
     d.chunk_base = pi.chunk_base;
     d.comp = pi.comp;  // offset for now; rebased onto the pool in launch_batch
-    d.rw_div = region_divisor(pj);
+    const RegionSizing rs = region_sizing(pj, worst);
+    d.rw_div = rs.div;
+    d.rw_slack = rs.slack;
 }
 
 

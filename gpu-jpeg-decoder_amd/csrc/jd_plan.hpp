@@ -26,16 +26,26 @@ inline uint64_t piece_slots(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bi
     return (ecs_bytes * 8 + piece_bits - 1) / piece_bits + nseg;
 }
 inline uint64_t entry_words(uint64_t ecs_bytes, uint32_t nseg, uint32_t piece_bits, int64_t spare_pieces = -1,
-                            uint32_t div = 2u) {
+                            uint32_t div = 2u, uint32_t slack = kRegionSlack) {
     const uint64_t bits = ecs_bytes * 8, slots = piece_slots(ecs_bytes, nseg, piece_bits);
     uint64_t spare = (piece_bits >= bits) ? 0 : (piece_bits >= 4096 ? slots / 16 + 8 : slots);
     if (spare_pieces >= 0) spare = uint64_t(spare_pieces);  // JD_SPARE_PIECES (tests: in-place re-walks)
-    return bits / div + 4 + slots * (kRegionSlack + 8) +
-           spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)), div);
+    return bits / div + 4 + slots * (slack + 8) +
+           spare * region_words(uint32_t(std::min<uint64_t>(piece_bits, bits)), div, slack);
 }
 // Fewest walk bits per region word any block or entry of the image can take, from its Huffman
 // tables (in [2, 8]; 2 holds for any tables): the divisor of its piece regions (region_words).
 uint32_t region_divisor(const ParsedJpeg& pj);
+// The divisor and slack an image's regions are planned with: the worst case (region_divisor,
+// kRegionSlack: no valid stream can fill them), or the optimistic default (kOptRegionDiv and the
+// image's largest MCU: a denser stream overflows, is flagged and is decoded again with the worst case).
+struct RegionSizing {
+    uint32_t div, slack;
+};
+inline RegionSizing region_sizing(const ParsedJpeg& pj, bool worst) {
+    if (worst) return {region_divisor(pj), kRegionSlack};
+    return {std::max(region_divisor(pj), kOptRegionDiv), opt_region_slack(uint32_t(pj.hdr.blocks_per_mcu))};
+}
 inline uint32_t image_segments(const jd_header& h) {
     const uint64_t nmcu = uint64_t(h.mcux) * h.mcuy;
     return h.restart_interval ? uint32_t((nmcu + h.restart_interval - 1) / h.restart_interval) : 1u;
@@ -60,9 +70,9 @@ inline uint32_t adaptive_piece_bits(uint64_t ecs_bits, uint32_t pmin = kMinPiece
 // div: the image's region divisor.
 constexpr uint64_t kMaxImageEntryWords = 0x7FFFFF00ull;
 inline bool image_fits(uint64_t ecs_bytes, const jd_header& h, uint32_t pmin, uint32_t pmax, int64_t spare_pieces = -1,
-                       uint32_t div = 2u) {
+                       uint32_t div = 2u, uint32_t slack = kRegionSlack) {
     for (uint64_t p = pmin;; p *= 2) {
-        if (entry_words(ecs_bytes, image_segments(h), uint32_t(p), spare_pieces, div) > kMaxImageEntryWords) return false;
+        if (entry_words(ecs_bytes, image_segments(h), uint32_t(p), spare_pieces, div, slack) > kMaxImageEntryWords) return false;
         if (p >= pmax) return true;
     }
 }
@@ -75,8 +85,9 @@ struct PlanImg {
     uint32_t seg_base, nseg, chunk_base, nchunks;
 };
 
-// Fills d (everything but the piece ranges) for item it; pure function of the header + bases.
+// Fills d (everything but the piece ranges) for item it; pure function of the header + bases
+// (worst: worst-case region sizing, region_sizing).
 void fill_desc(const ParsedJpeg& pj, const jd_item& item, uint64_t dev_addr, uint64_t out_addr, const PlanImg& pi,
-               ImgDesc& d);
+               ImgDesc& d, bool worst);
 
 }  // namespace jd

@@ -188,6 +188,14 @@ struct Pending {
     bool timing = false, fancy = false;
     double blocks = 0, pixels = 0, ecs = 0, nsub = 0, nseg = 0, chunks = 0, tiles = 0, piece_bits = 0, piece_overlap = 0;
     double t_plan = 0, t_upload = 0;
+    // what a retry needs (run_retries): the items, their parsed headers and device bytes (dev_addr:
+    // the caller's jpeg_dev, or the slot's copy of a host input, which stays until the slot's next
+    // launch, i.e. past this batch's collection at async depth 1), and whether the plan was the worst case
+    std::vector<jd_item> items;
+    std::vector<ParsedJpeg> parsed;
+    std::vector<uint64_t> dev_addr;
+    int rgb_on_device = 1;
+    bool worst = false;
 };
 // launch records (>= the async depth + 2: a record is reused 4 launches later)
 constexpr int kNumPending = 4;
@@ -226,6 +234,20 @@ struct jd_ctx {
     uint64_t max_batch_entries = 0;     // AC-entry slots per launched sub-batch (JD_MAX_BATCH_ENTRIES)
     int max_batch_images = 0;           // items per launched sub-batch (JD_MAX_BATCH_IMAGES)
     int64_t spare_pieces = -1;          // spare re-walk regions per image (JD_SPARE_PIECES; -1: default)
+    // Pools: optimistic by default (piece regions at kOptRegionDiv bits per word, break lists of the
+    // batch's most intervals); an image that overflows one is decoded again with the worst-case plan
+    // (run_retries).  worst: the plan being built is the worst case (a retry, or every batch with
+    // JD_FLAG_WORST_CASE_POOLS); brk_cap_force: JD_BRK_CAP (tests: break slots per chunk of
+    // optimistic plans, to force the break-list overflow).
+    bool worst = false, worst_always = false;
+    uint32_t brk_cap_force = 0;
+    struct Retry {
+        jd_item item;
+        ParsedJpeg pj;
+        jd_result* res;
+        int rgb_on_device;
+    };
+    std::vector<Retry> retry;  // overflowed images of collected batches, not yet decoded again
     int64_t piece_overlap = -1;         // warm-up bits (JD_PIECE_OVERLAP_BITS; -1: default)
     uint32_t min_piece_bits = kMinPieceBits;  // small batches' shortest pieces (JD_MIN_PIECE_BITS: a test knob)
     bool fixed_pieces = false;          // JD_FIXED_PIECES: keep the host's piece size (no k_pieceplan)
@@ -250,6 +272,7 @@ struct jd_ctx {
     uint64_t last_blocks = 0, last_entries = 0;
     std::vector<uint64_t> last_entry_base;  // per image (jd_debug_fetch 20)
     std::vector<uint32_t> last_rw_div;      // per image (jd_debug_fetch 21)
+    std::vector<uint32_t> last_rw_slack;    // per image (jd_debug_fetch 22)
     uint64_t dev_bytes = 0, dev_peak = 0;   // device pool bytes held now / at most (jd_device_bytes)
 };
 
@@ -368,7 +391,7 @@ struct Plan {
     std::vector<uint32_t> img_order;  // images in table-set order (k_pieceplan's dense allocation)
     uint32_t piece_bits = kPieceBits, piece_overlap = kPieceOverlap;
     std::vector<uint32_t> chain_seg, chain_wg_tableset;  // k_chain lanes, grouped by table set
-    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0;
+    uint32_t total_chunks = 0, max_chunks = 0, max_tiles = 0, total_tiles = 0, max_slots = 1, nsub = 0, brk_cap = kScanCap;
     uint64_t total_blocks = 0, total_entry_cap = 0, comp_bytes = 0;
     double pixels = 0, ecs_bytes = 0;
     std::vector<uint32_t> mode_imgs;  // images grouped by sampling layout (k_idct_color<M>)
@@ -393,8 +416,9 @@ int batch_split(jd_ctx* ctx, int lo, int n, const jd_item* items) {
         if (hi - lo >= ctx->max_batch_images) break;
         if (ctx->pst[hi] != JD_OK) continue;
         const jd_header& h = ctx->parsed[hi].hdr;
-        const uint64_t w = entry_words(items[hi].len - h.ecs_offset, image_segments(h), kPieceBits, -1,
-                                       region_divisor(ctx->parsed[hi]));
+        // (at async depth 2 a batch with host inputs is planned with worst-case pools: launch_batch)
+        const RegionSizing rs = region_sizing(ctx->parsed[hi], ctx->worst || ctx->worst_always || ctx->async_depth == 2);
+        const uint64_t w = entry_words(items[hi].len - h.ecs_offset, image_segments(h), kPieceBits, -1, rs.div, rs.slack);
         if (hi > lo && cap + w > limit) break;
         cap += w;
     }
@@ -402,7 +426,7 @@ int batch_split(jd_ctx* ctx, int lo, int n, const jd_item* items) {
 }
 
 jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const std::vector<uint64_t>& dev_addr,
-                     const std::vector<uint64_t>& out_addr, Plan& P) {
+                     const std::vector<uint64_t>& out_addr, bool worst, Plan& P) {
     const auto tb0 = std::chrono::steady_clock::now();
     auto tbms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(); };
     // 1. sequential: table sets and quant tables (de-duplicated across the batch), bases
@@ -427,7 +451,9 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
                               : (ctx->flags & JD_FLAG_FULL_PIECES) ? kPieceBits
                                                                    : adaptive_piece_bits(ecs_img * 8, ctx->min_piece_bits);
         const bool forced = (ctx->flags & (JD_FLAG_FORCE_SYNC | JD_FLAG_FORCE_LANES | JD_FLAG_FULL_PIECES)) != 0;
-        if (!image_fits(ecs_img, h, pmin, forced ? pmin : kPieceBits, ctx->spare_pieces, region_divisor(pj))) {
+        // (the worst-case plan must fit: an optimistic one may be retried with it)
+        const RegionSizing rs = region_sizing(pj, true);
+        if (!image_fits(ecs_img, h, pmin, forced ? pmin : kPieceBits, ctx->spare_pieces, rs.div, rs.slack)) {
             ctx->pst[it] = JD_ERR_CAPACITY;
             continue;
         }
@@ -535,7 +561,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             const PlanImg& pi = pim[i];
             const ParsedJpeg& pj = ctx->parsed[pi.item];
             ImgDesc& d = P.imgs[i];
-            fill_desc(pj, items[pi.item], dev_addr[pi.item], out_addr[pi.item], pi, d);
+            fill_desc(pj, items[pi.item], dev_addr[pi.item], out_addr[pi.item], pi, d, worst);
             P.item_of_img[i] = pi.item;
             for (uint32_t k = 0; k < d.nseg; k++) P.seg_img[d.seg_base + k] = uint32_t(i);
         }
@@ -588,7 +614,7 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
             d.sub_base = uint32_t(sub);
             d.sub_cap = uint32_t(piece_slots(d.len - d.ecs_off, d.nseg, P.piece_bits));
             d.entry_base = entry_cursor;
-            const uint64_t words = entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces, d.rw_div);
+            const uint64_t words = entry_words(d.len - d.ecs_off, d.nseg, P.piece_bits, ctx->spare_pieces, d.rw_div, d.rw_slack);
             if (words > kMaxImageEntryWords) return JD_ERR_CAPACITY;  // image_fits checked every piece size
             d.entry_cap = uint32_t(words);
             entry_cursor += align_up(size_t(d.entry_cap), kRegionAlign);
@@ -605,6 +631,12 @@ jd_status build_plan(jd_ctx* ctx, const jd_item* items, int lo, int hi, const st
     P.nsub = uint32_t(sub);
 
     P.total_entry_cap = entry_cursor;
+    // break slots per scan chunk: every RSTn and the EOI of a valid stream fit in the batch's most
+    // intervals + kBrkSlack (k_index flags a chunk before the ECS end that held more)
+    uint32_t most_seg = 0;
+    for (const ImgDesc& d : P.imgs) most_seg = std::max(most_seg, d.nseg);
+    P.brk_cap = worst ? uint32_t(kScanCap) : std::min<uint32_t>(kScanCap, most_seg + kBrkSlack);
+    if (!worst && ctx->brk_cap_force) P.brk_cap = std::min<uint32_t>(P.brk_cap, ctx->brk_cap_force);
     return JD_OK;
 }
 
@@ -799,8 +831,12 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     std::unique_ptr<Range> rng(new Range("jd_plan"));
     const auto tp0 = std::chrono::steady_clock::now();
     auto tms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count(); };
+    // Optimistic pools unless this is a retry (or the caller asked for worst-case pools), or a batch
+    // with host inputs at async depth 2: the slot's copy of them may be replaced by its next launch
+    // before this batch is collected, and a retry would have nothing to read.
+    const bool worst = ctx->worst || ctx->worst_always || (ctx->async_depth == 2 && in_bytes + reg_bytes > 0);
     Plan P;
-    jd_status st = build_plan(ctx, items, lo, hi, dev_addr, out_addr, P);
+    jd_status st = build_plan(ctx, items, lo, hi, dev_addr, out_addr, worst, P);
     const double t_plan = tms();
     if (st != JD_OK) return st;
     st = sync_luts(ctx);
@@ -880,7 +916,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         HIPCHK(ctx, hipMemcpyAsync(sl.d_plan.p, sl.plan_host, upload, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipEventRecord(sl.plan_done, s));
         sl.plan_recorded = true;
-        HIPCHK(ctx, ensure_dev(ctx, sl.d_brk, std::max<size_t>(16, size_t(P.total_chunks) * kScanCap * sizeof(Break))));
+        HIPCHK(ctx, ensure_dev(ctx, sl.d_brk, std::max<size_t>(16, size_t(P.total_chunks) * P.brk_cap * sizeof(Break))));
         HIPCHK(ctx, ensure_dev(ctx, sl.d_blocks, std::max<size_t>(16, P.total_blocks * sizeof(BlockInfo))));
         HIPCHK(ctx, ensure_dev(ctx, sl.d_entries, P.total_entry_cap * 4 + 64));  // +64: 16-byte over-reads
 
@@ -948,6 +984,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         b.chunk_drops = reinterpret_cast<uint32_t*>(base + o_drops);
         b.chunk_coff = reinterpret_cast<uint32_t*>(base + o_coff);
         b.chunk_brk = static_cast<Break*>(sl.d_brk.p);
+        b.brk_cap = P.brk_cap;
         b.blocks = static_cast<BlockInfo*>(sl.d_blocks.p);
         b.entries = static_cast<uint32_t*>(sl.d_entries.p);
         b.entries_cap = (sl.d_entries.cap - 64) / 4;  // last 64 B: padding for 16-byte over-reads
@@ -975,9 +1012,11 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
         ctx->last_entries = P.total_entry_cap;
         ctx->last_entry_base.resize(P.imgs.size());
         ctx->last_rw_div.resize(P.imgs.size());
+        ctx->last_rw_slack.resize(P.imgs.size());
         for (size_t i = 0; i < P.imgs.size(); i++) {
             ctx->last_entry_base[i] = P.imgs[i].entry_base;
             ctx->last_rw_div[i] = P.imgs[i].rw_div;
+            ctx->last_rw_slack[i] = P.imgs[i].rw_slack;
         }
         const bool timing = (ctx->flags & JD_FLAG_TIMING) != 0;
         const double t_upload = tms();
@@ -1042,6 +1081,16 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
             pd.host_copies.push_back({reinterpret_cast<uint64_t>(items[i].rgb), out_addr[i],
                                       uint64_t(ctx->parsed[i].hdr.width) * ctx->parsed[i].hdr.height * 3});
     }
+    pd.worst = worst;
+    pd.rgb_on_device = rgb_on_device;
+    if (!worst) {  // (a worst-case batch is never retried)
+        pd.items.assign(items + lo, items + hi);
+        pd.dev_addr.assign(dev_addr.begin() + lo, dev_addr.begin() + hi);
+        if (lo == 0 && size_t(hi) == ctx->parsed.size())
+            std::swap(pd.parsed, ctx->parsed);  // (the call's last use of them: parse_all refills ctx->parsed)
+        else
+            pd.parsed.assign(ctx->parsed.begin() + lo, ctx->parsed.begin() + hi);
+    }
     HIPCHK(ctx, hipEventRecord(pd.done, s));
     pd.active = true;
     pd.seq = ctx->seq++;
@@ -1063,8 +1112,16 @@ jd_status finish_batch(jd_ctx* ctx, Pending& pd) {
     if (nimg) {
         const unsigned long long* ctr = static_cast<const unsigned long long*>(pd.host);
         const uint32_t* status = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pd.host) + kNumCounters * 8);
-        for (uint32_t i = 0; i < nimg; i++)
-            if (status[i]) pd.pst[size_t(pd.item_of_img[i] - pd.lo)] = JD_ERR_CORRUPT;
+        for (uint32_t i = 0; i < nimg; i++) {
+            if (!status[i]) continue;
+            const size_t k = size_t(pd.item_of_img[i] - pd.lo);
+            pd.pst[k] = JD_ERR_CORRUPT;  // (until a retry decodes it)
+            if ((status[i] & kStOverflow) && !pd.worst) {  // an optimistic pool was too small: decode it again
+                jd_item it = pd.items[k];
+                it.jpeg_dev = reinterpret_cast<const uint8_t*>(pd.dev_addr[k]);
+                ctx->retry.push_back(jd_ctx::Retry{it, pd.parsed[k], pd.results + pd.lo + k, pd.rgb_on_device});
+            }
+        }
         if (ctx->host_timing)
             std::fprintf(stderr, "host plan %.3f upload %.3f wait %.3f ms\n", pd.t_plan, pd.t_upload,
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count());
@@ -1151,6 +1208,49 @@ jd_status collect_until(jd_ctx* ctx, int keep) {
 // Collects every launched batch, oldest first.
 jd_status finish_all(jd_ctx* ctx) { return collect_until(ctx, 0); }
 
+// Decodes again, with worst-case pools, the images of collected batches that overflowed an
+// optimistic one (kStOverflow), and fills their results.  Every batch is collected first (the
+// retries use both slots' scratch), so a retry costs the pipeline's overlap once.  The images'
+// parsed headers and device bytes were kept with their batch (Pending), so nothing is read from the
+// caller's host buffers, which may have been reused since.
+jd_status run_retries(jd_ctx* ctx, void* hip_stream) {
+    if (ctx->worst) return JD_OK;  // (a retry's own batches are never retried)
+    while (!ctx->retry.empty()) {
+        jd_status st = finish_all(ctx);  // (may add retries)
+        if (st != JD_OK) return st;
+        std::vector<jd_ctx::Retry> r;
+        r.swap(ctx->retry);
+        for (int mode = 0; mode < 2; mode++) {
+            std::vector<size_t> idx;
+            for (size_t j = 0; j < r.size(); j++)
+                if ((r[j].rgb_on_device != 0) == (mode != 0)) idx.push_back(j);
+            if (idx.empty()) continue;
+            const int m = int(idx.size());
+            std::vector<jd_item> items(static_cast<size_t>(m));
+            std::vector<jd_result> res(static_cast<size_t>(m));
+            ctx->parsed.resize(size_t(m));
+            ctx->pst.assign(size_t(m), JD_OK);
+            for (int j = 0; j < m; j++) {
+                items[size_t(j)] = r[idx[size_t(j)]].item;
+                ctx->parsed[size_t(j)] = r[idx[size_t(j)]].pj;
+            }
+            ctx->worst = true;
+            for (int lo = 0; lo < m && st == JD_OK;) {
+                const int hi = batch_split(ctx, lo, m, items.data());
+                hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->slots[ctx->slot].stream;
+                st = launch_batch(ctx, items.data(), lo, hi, res.data(), mode, s);
+                if (st == JD_OK) st = finish_all(ctx);
+                lo = hi;
+            }
+            ctx->worst = false;
+            if (st != JD_OK) return st;
+            for (int j = 0; j < m; j++) *r[idx[size_t(j)]].res = res[size_t(j)];
+            ctx->stats.retried_images += double(m);
+        }
+    }
+    return JD_OK;
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -1218,6 +1318,9 @@ jd_status jd_ctx_create(jd_ctx** out, int hip_device, const jd_opts* opts) {
     if (const char* e = std::getenv("JD_STAGE_NT")) ctx->stage_nt = std::strtoll(e, nullptr, 0) != 0;
     if (const char* e = std::getenv("JD_H2D_SERIAL")) ctx->h2d_serial = std::strtoll(e, nullptr, 0) != 0;
     ctx->async_depth = (ctx->flags & JD_FLAG_ASYNC_DEPTH2) ? 2 : 1;  // an explicit opt-in
+    ctx->worst_always = (ctx->flags & JD_FLAG_WORST_CASE_POOLS) != 0;
+    if (const char* e = std::getenv("JD_WORST_CASE_POOLS")) ctx->worst_always = ctx->worst_always || std::strtoll(e, nullptr, 0) != 0;
+    if (const char* e = std::getenv("JD_BRK_CAP")) ctx->brk_cap_force = uint32_t(std::strtoul(e, nullptr, 0));
     if (const char* e = std::getenv("JD_STAGE_CHUNK_MB")) {
         const long long mb = std::strtoll(e, nullptr, 0);
         ctx->stage_chunk = mb > 0 ? size_t(mb) << 20 : ~size_t(0);
@@ -1400,7 +1503,11 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
         if (st != JD_OK) return st;
         lo = hi;
     }
-    return async ? JD_OK : finish_all(ctx);
+    if (!async) {
+        const jd_status st = finish_all(ctx);
+        if (st != JD_OK) return st;
+    }
+    return run_retries(ctx, hip_stream);
 }
 }  // namespace
 
@@ -1416,7 +1523,9 @@ jd_status jd_decode_batch_async(jd_ctx* ctx, const jd_item* items, int n, jd_res
 jd_status jd_decode_wait(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
     if (hipSetDevice(ctx->device) != hipSuccess) return JD_ERR_HIP;
-    return finish_all(ctx);
+    const jd_status st = finish_all(ctx);
+    if (st != JD_OK) return st;
+    return run_retries(ctx, const_cast<void*>(ctx->last_stream));
 }
 
 jd_status jd_decode(jd_ctx* ctx, const uint8_t* jpeg, size_t len, uint8_t* rgb, int rgb_on_device, int* width,
@@ -1565,6 +1674,10 @@ jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* dst, size_t cap, size_t* n
         case 21:  // per image of the last batch: ImgDesc::rw_div (u32), host copy
             *nbytes = ctx->last_rw_div.size() * 4;
             if (dst) memcpy(dst, ctx->last_rw_div.data(), std::min(*nbytes, cap));
+            return JD_OK;
+        case 22:  // per image of the last batch: ImgDesc::rw_slack (u32), host copy
+            *nbytes = ctx->last_rw_slack.size() * 4;
+            if (dst) memcpy(dst, ctx->last_rw_slack.data(), std::min(*nbytes, cap));
             return JD_OK;
         default: return JD_ERR_INVALID_ARG;
     }

@@ -34,8 +34,9 @@ JD_FLAG_FORCE_LANES = 4
 JD_FLAG_FANCY_UPSAMPLING = 8
 JD_FLAG_FULL_PIECES = 16
 JD_FLAG_ASYNC_DEPTH2 = 32
+JD_FLAG_WORST_CASE_POOLS = 64
 PATHS = {"auto": 0, "sync": JD_FLAG_FORCE_SYNC, "lanes": JD_FLAG_FORCE_LANES, "full": JD_FLAG_FULL_PIECES}
-JD_ABI_VERSION = 7
+JD_ABI_VERSION = 8
 JD_NUM_KERNELS = 11
 KERNEL_NAMES = ["k_scan", "k_index", "k_compact", "k_subplan", "k_piece", "k_redo", "k_chain",
                 "k_gather", "k_dc_pred", "k_idct_color", "k_colour_fancy"]
@@ -78,7 +79,7 @@ class _Stats(ctypes.Structure):
                 ("host_ms", ctypes.c_double * 4), ("h2d_bytes", ctypes.c_double),
                 ("h2d_registered_bytes", ctypes.c_double), ("redo_pieces", ctypes.c_double),
                 ("fix_intervals", ctypes.c_double), ("fix_rounds", ctypes.c_double), ("fix_rewalks", ctypes.c_double),
-                ("fix_early", ctypes.c_double)]
+                ("fix_early", ctypes.c_double), ("retried_images", ctypes.c_double)]
 
 
 # Every symbol include/jd.h and include/jd_test.h declare (checked by tests/test_abi.py).
@@ -256,10 +257,12 @@ class Decoder:
     (cuda-decoder/src/parser.cu:324-358, 577-700) as a context object."""
 
     def __init__(self, device: int = 0, timing: bool = False, parse_threads: int = 0, path: str = "auto",
-                 fancy: bool = False, async_depth: int = 1):
+                 fancy: bool = False, async_depth: int = 1, worst_case_pools: bool = False):
         """fancy=True: libjpeg's triangular chroma upsampling instead of replication
         (JD_FLAG_FANCY_UPSAMPLING; an option beyond the reference, see include/jd.h).
-        async_depth=2: pipelined calls leave two batches in flight (JD_FLAG_ASYNC_DEPTH2)."""
+        async_depth=2: pipelined calls leave two batches in flight (JD_FLAG_ASYNC_DEPTH2).
+        worst_case_pools=True: device pools sized for the densest stream the tables allow, so no
+        image is ever decoded twice (JD_FLAG_WORST_CASE_POOLS; about twice the device memory)."""
         if async_depth not in (1, 2):
             raise ValueError("async_depth: 1 or 2")
         self.lib = load_library()
@@ -271,7 +274,8 @@ class Decoder:
         self._arenas = {}  # pointer -> registered numpy arena (kept alive while registered)
         self.ctx = ctypes.c_void_p()
         opts = _Opts((JD_FLAG_TIMING if timing else 0) | PATHS[path] | (JD_FLAG_FANCY_UPSAMPLING if fancy else 0) |
-                     (JD_FLAG_ASYNC_DEPTH2 if async_depth == 2 else 0), parse_threads)
+                     (JD_FLAG_ASYNC_DEPTH2 if async_depth == 2 else 0) |
+                     (JD_FLAG_WORST_CASE_POOLS if worst_case_pools else 0), parse_threads)
         st = self.lib.jd_ctx_create(ctypes.byref(self.ctx), device, ctypes.byref(opts))
         if st != JD_OK:
             raise JDError(st, "jd_ctx_create")
@@ -438,6 +442,8 @@ class Decoder:
             # rounds, re-walked pieces, early stops
             "redo_pieces": s.redo_pieces, "fix_intervals": s.fix_intervals, "fix_rounds": s.fix_rounds,
             "fix_rewalks": s.fix_rewalks, "fix_early": s.fix_early,
+            # images decoded again with worst-case pools after overflowing an optimistic one
+            "retried_images": s.retried_images,
         }
 
     def device_bytes(self):
@@ -459,7 +465,8 @@ class Decoder:
                     "piece_mcu0": (12, np.uint32, 1), "piece_abase": (13, np.uint32, 1),
                     "piece_cp": (14, np.uint32, 36), "stamps": (15, np.uint64, 8), "piece_emcu": (16, np.uint32, 1),
                     "piece_amcu": (17, np.uint32, 1), "piece_join": (18, np.uint32, 1), "seg_ent": (19, np.uint32, 1),
-                    "entry_base": (20, np.uint64, 1), "rw_div": (21, np.uint32, 1)}
+                    "entry_base": (20, np.uint64, 1), "rw_div": (21, np.uint32, 1),
+                    "rw_slack": (22, np.uint32, 1)}
 
     def debug_fetch(self, name: str) -> np.ndarray:
         """Internal array of the most recent batch (white-box tests and debugging)."""

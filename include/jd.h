@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define JD_ABI_VERSION 7
+#define JD_ABI_VERSION 8
 
 typedef enum jd_status {
     JD_OK = 0,
@@ -64,6 +64,15 @@ typedef struct jd_ctx jd_ctx;
  * call k + 2 returns (or jd_decode_wait).  Measured 3-4 % slower on the bench configs (DESIGN.md
  * §4.5); an explicit opt-in because it changes when a caller may reuse those buffers. */
 #define JD_FLAG_ASYNC_DEPTH2 32u
+/* Device pools.  By default a batch's scratch is sized for the data it is likely to hold: piece
+ * regions of sparse coefficients for 8 walk bits per 32-bit word (real streams take 10-14) and
+ * scan break lists for the batch's restart intervals.  An image that overflows one is decoded again
+ * with worst-case pools before its batch is reported (jd_stats.retried_images): the results are the
+ * same, the pools about half as large.  This flag plans every batch with worst-case pools (no retry
+ * can happen; about twice the device memory).  At async depth 2 a batch with host-memory inputs is
+ * always planned with worst-case pools (its inputs' device copy does not outlive its slot's next
+ * launch, which precedes its collection). */
+#define JD_FLAG_WORST_CASE_POOLS 64u
 
 typedef struct jd_opts {
     unsigned flags;
@@ -208,6 +217,9 @@ typedef struct jd_stats {
      * the k_chain_big intervals that stopped early at a right piece with an error (corrupt data or
      * trailing bytes) */
     double redo_pieces, fix_intervals, fix_rounds, fix_rewalks, fix_early;
+    /* images decoded again with worst-case pools after overflowing an optimistic one
+     * (JD_FLAG_WORST_CASE_POOLS) */
+    double retried_images;
 } jd_stats;
 jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out);
 jd_status jd_reset_stats(jd_ctx* ctx);

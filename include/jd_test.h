@@ -38,6 +38,7 @@ jd_status jd_test_copy_peak(jd_ctx* ctx, const void* src_dev, void* dst_dev, siz
  *       16 piece_emcu, 17 piece_amcu, 18 piece_join (u32 per piece slot), 19 seg_ent (u32 per
  *       segment), 20 entry_base (u64 per image: first 32-bit word of its AC-entry region),
  *       21 rw_div (u32 per image: walk bits per piece-region word, jd_internal.hpp region_words).
+ *       22 rw_slack (u32 per image: region words per piece beyond plen / rw_div, region_words).
  *       *nbytes receives the array size; at most cap bytes are copied. */
 jd_status jd_debug_fetch(jd_ctx* ctx, int what, void* host_dst, size_t cap, size_t* nbytes);
 

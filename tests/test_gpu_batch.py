@@ -27,13 +27,19 @@ import jd_synth  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def region_words(plen, div=2):
-    """jd_internal.hpp region_words: one piece's AC-entry region in 32-bit words (div: the image's
-    jd_plan.cpp region_divisor; 4 for the Annex K tables, tests/test_sanitize.py)."""
-    return ((plen + div - 1) // div + 1040 + 7) & ~7  # kRegionAlign: 8 words
+def region_words(plen, div=2, slack=1040):
+    """jd_internal.hpp region_words: one piece's AC-entry region in 32-bit words (div, slack: the
+    image's jd_plan.hpp region_sizing; worst case: 4 and 1040 for the Annex K tables)."""
+    return ((plen + div - 1) // div + slack + 7) & ~7  # kRegionAlign: 8 words
 
 
-def entry_words(data, h, piece_bits=16384, spare=None, div=2):
+def opt_sizing(h):
+    """jd_plan.hpp region_sizing of the default (optimistic) plan: kOptRegionDiv and
+    opt_region_slack (the image's largest MCU + kRoundItemsMax + 8)."""
+    return {"div": 8, "slack": 64 * h.blocks_per_mcu + 152 + 8}
+
+
+def entry_words(data, h, piece_bits=16384, spare=None, div=2, slack=1040):
     """jd_plan.hpp entry_words: the AC-entry words one image reserves (its pieces' regions and the
     spare regions of re-walks), from its entropy-coded bytes and restart intervals."""
     bits = (len(data) - h.ecs_offset) * 8
@@ -42,7 +48,7 @@ def entry_words(data, h, piece_bits=16384, spare=None, div=2):
     slots = -(-bits // piece_bits) + nseg
     if spare is None:
         spare = 0 if piece_bits >= bits else (slots // 16 + 8 if piece_bits >= 4096 else slots)
-    return bits // div + 4 + slots * (1040 + 8) + spare * region_words(min(piece_bits, bits), div)
+    return bits // div + 4 + slots * (slack + 8) + spare * region_words(min(piece_bits, bits), div, slack)
 
 
 def _device_batch(dec, datas):
@@ -72,10 +78,10 @@ def test_mixed_batch_tail_beyond_2_32_entry_words(monkeypatch):
     n = 1024
     datas = jd_synth.make_batch(n, 1920, 1080, mixed=True, seed0=500000)
     hdrs0 = [jdamd.parse(d) for d in datas]
-    # Annex K tables: region divisor 4 (tests/test_sanitize.py)
-    natural = sum(entry_words(d, h, div=4) for d, h in zip(datas, hdrs0))
+    # the default plan's optimistic regions (jd_plan.hpp region_sizing)
+    natural = sum(entry_words(d, h, **opt_sizing(h)) for d, h in zip(datas, hdrs0))
     pad = max(0, (3 << 32) // 2 - natural) // n  # total ~1.5 x 2^32 words (~26 GB of entry pool)
-    monkeypatch.setenv("JD_SPARE_PIECES", str(pad // region_words(16384, 4) + 16))
+    monkeypatch.setenv("JD_SPARE_PIECES", str(pad // region_words(16384, **opt_sizing(hdrs0[0])) + 16))
     dec = jdamd.Decoder(0)
     try:
         hosts, hdrs, din, dout, offs, ooffs = _device_batch(dec, datas)
@@ -102,7 +108,8 @@ def test_forced_split_host_inputs_and_outputs(monkeypatch):
     pool; each must be collected before the next is launched."""
     datas = jd_synth.make_batch(24, 640, 480, 90, "4:2:0", 1, 0, seed0=7000)
     datas += jd_synth.make_batch(12, 800, 600, 75, "4:4:4", 0, 0, seed0=8000)
-    per = entry_words(datas[0], jdamd.parse(datas[0]), div=4)  # batch_split's estimate (Annex K tables)
+    h0 = jdamd.parse(datas[0])
+    per = entry_words(datas[0], h0, **opt_sizing(h0))  # batch_split's estimate (the default plan)
     monkeypatch.setenv("JD_MAX_BATCH_ENTRIES", str(per * 14))  # ~14 images of the first kind
     dec = jdamd.Decoder(0)
     try:

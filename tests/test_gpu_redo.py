@@ -115,9 +115,11 @@ def dense_batch():
 @pytest.mark.parametrize("path", ["auto", "sync", "lanes", "full"])
 def test_dense_streams_without_spare_regions(monkeypatch, dense_batch, path):
     """Flat (DC-only) and long-code images on every piece geometry with JD_SPARE_PIECES=0 (re-walks
-    over their own regions): bit-exact, and the re-tabled images planned with region divisor 8."""
+    over their own regions), with worst-case pools (tests/test_gpu_pools.py: the default optimistic
+    ones): bit-exact, and the re-tabled images planned with region divisor 8."""
     datas, refs = dense_batch
     monkeypatch.setenv("JD_SPARE_PIECES", "0")
+    monkeypatch.setenv("JD_WORST_CASE_POOLS", "1")
     dec = jdamd.Decoder(0, path=path)
     try:
         outs, status = dec.decode_batch(datas)

@@ -51,8 +51,9 @@ def test_intervals_and_piece_starts(sync_decoder, name):
     pab = sync_decoder.debug_fetch("piece_abase")
     pjoin = sync_decoder.debug_fetch("piece_join")
     sent = sync_decoder.debug_fetch("seg_ent")
-    div = int(sync_decoder.debug_fetch("rw_div")[0])  # jd_plan.cpp region_divisor of the image
-    assert 2 <= div <= 8
+    div = int(sync_decoder.debug_fetch("rw_div")[0])  # jd_plan.hpp region_sizing of the image
+    slack = int(sync_decoder.debug_fetch("rw_slack")[0])
+    assert 2 <= div <= 8 and slack <= 1040
     errs = []
     for s, seg in enumerate(truth):
         if (int(ce[s]) - int(cs[s])) * 8 != seg["bits"]:
@@ -63,7 +64,7 @@ def test_intervals_and_piece_starts(sync_decoder, name):
             errs.append(f"seg {s}: pieces gpu {nsub[s]} want {want_n}")
             continue
         plen = -(-seg["bits"] // want_n)
-        rw = ((plen + div - 1) // div + 1040 + 7) // 8 * 8  # jd_internal.hpp region_words (kRegionAlign 8)
+        rw = ((plen + div - 1) // div + slack + 7) // 8 * 8  # jd_internal.hpp region_words (kRegionAlign 8)
         starts = {b: (m, e) for m, (b, e) in enumerate(seg["starts"])}
         nm = 0
         for j in range(want_n):

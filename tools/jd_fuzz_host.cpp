@@ -35,14 +35,17 @@ static int plan_one(const uint8_t* buf, size_t len, const ParsedJpeg& pj, ImgDes
     delete lut;
     if (!ok) return JD_ERR_CORRUPT;
     const uint64_t ecs = len - h.ecs_offset;
-    if (!image_fits(ecs, h, adaptive_piece_bits(ecs * 8), kPieceBits, -1, region_divisor(pj))) return JD_ERR_CAPACITY;
+    const RegionSizing opt = region_sizing(pj, false), worst = region_sizing(pj, true);
+    if (!image_fits(ecs, h, adaptive_piece_bits(ecs * 8), kPieceBits, -1, worst.div, worst.slack)) return JD_ERR_CAPACITY;
+    (void)image_fits(ecs, h, adaptive_piece_bits(ecs * 8), kPieceBits, -1, opt.div, opt.slack);
     PlanImg pi{};
     pi.nseg = image_segments(h);
     pi.nchunks = uint32_t((len - (h.ecs_offset & ~uint64_t(15)) + kScanChunk - 1) / kScanChunk);
     (void)piece_slots(ecs, pi.nseg, kPieceBits);
-    (void)entry_words(ecs, pi.nseg, kPieceBits);
+    (void)entry_words(ecs, pi.nseg, kPieceBits, -1, opt.div, opt.slack);
     jd_item item{buf, nullptr, len, nullptr};
-    fill_desc(pj, item, 0x100000000ull, 0x200000000ull, pi, d);
+    fill_desc(pj, item, 0x100000000ull, 0x200000000ull, pi, d, false);  // the default (optimistic) plan
+    fill_desc(pj, item, 0x100000000ull, 0x200000000ull, pi, d, true);   // the retry's: reported (rw_div)
     return 0;
 }
 
