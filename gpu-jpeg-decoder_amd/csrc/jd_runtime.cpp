@@ -1623,7 +1623,8 @@ jd_status jd_memcpy_d2h(jd_ctx* ctx, void* dst, const void* src, size_t n) {
 
 jd_status jd_synchronize(jd_ctx* ctx) {
     if (!ctx) return JD_ERR_INVALID_ARG;
-    const jd_status st = finish_all(ctx);
+    jd_status st = finish_all(ctx);
+    if (st == JD_OK) st = run_retries(ctx, const_cast<void*>(ctx->last_stream));  // (collected batches' overflows)
     if (st != JD_OK) return st;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return JD_OK;

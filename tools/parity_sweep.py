@@ -41,6 +41,13 @@ def make_image(args):
     p = args
     gray = p["ss"] == "gray"
     px = jd_synth.synth_pixels(p["w"], p["h"], p["seed"], gray)
+    if p.get("flat"):  # flat areas (DC-only blocks): the densest streams, which overflow the default
+                       # plan's optimistic piece regions at long pieces (jd_runtime.cpp run_retries)
+        rng = np.random.default_rng(p["seed"] ^ 0xF1A7)
+        cell = int(rng.integers(8, 129))
+        gh, gw = -(-p["h"] // cell), -(-p["w"] // cell)
+        grid = rng.integers(0, 256, (gh, gw) if gray else (gh, gw, 3), dtype=np.uint8)
+        px = np.ascontiguousarray(np.repeat(np.repeat(grid, cell, 0), cell, 1)[: p["h"], : p["w"]])
     enc = p.get("enc", "jdenc")  # jdenc | pil | pil-opt
     data = jd_synth.encode(px, p["q"], "4:4:4" if gray else p["ss"], p["rows"], p["blocks"],
                            optimize=enc == "pil-opt", encoder="jdenc" if enc == "jdenc" else "pil")
@@ -74,7 +81,7 @@ def draw(rng, seed, pil=False):
     rows, blocks = (0, 0) if r < 0.4 else ((int(rng.integers(1, 4)), 0) if r < 0.7 else (0, int(rng.integers(1, 12))))
     d = {"seed": int(seed), "w": w, "h": h, "ss": LAYOUTS[int(rng.integers(0, len(LAYOUTS)))],
          "q": int(rng.choice([20, 35, 50, 75, 90, 95, 100])), "rows": rows, "blocks": blocks,
-         "flips": int(rng.integers(1, 4)) if rng.random() < 0.2 else 0}
+         "flips": int(rng.integers(1, 4)) if rng.random() < 0.2 else 0, "flat": bool(rng.random() < 0.15)}
     if pil:
         e = rng.random()
         d["enc"] = "jdenc" if e < 0.6 or d["ss"] == "4:4:0" else ("pil" if e < 0.75 else "pil-opt")
@@ -130,9 +137,10 @@ def main():
             it += 1
             print(f"batch {it} ({path}): {n_img} images, {n_ok} decoded, {n_bad_status} corrupt (status equal), "
                   f"{len(fails)} mismatches", flush=True)
+    retried = {p: d.stats()["retried_images"] for p, d in decs.items()}
     for d in decs.values():
         d.close()
-    res = {"images": n_img, "decoded_equal_or_checked": n_ok, "corrupt_status_checked": n_bad_status,
+    res = {"retried_images": retried, "images": n_img, "decoded_equal_or_checked": n_ok, "corrupt_status_checked": n_bad_status,
            "batches": it, "mismatches": fails, "seed": a.seed, "minutes": a.minutes, "fancy": a.fancy, "pil": a.pil,
            "paths": paths}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
