@@ -174,6 +174,7 @@ struct Slot {
 struct Pending {
     bool active = false;
     uint64_t seq = 0;                           // launch order
+    int slot = 0;                               // the slot it runs on
     jd_result* results = nullptr;
     int lo = 0, hi = 0;
     std::vector<jd_status> pst;                 // per item lo..hi: host-side status
@@ -1094,6 +1095,7 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     HIPCHK(ctx, hipEventRecord(pd.done, s));
     pd.active = true;
     pd.seq = ctx->seq++;
+    pd.slot = ctx->slot;
     staging.s = nullptr;  // the slot's done event now covers the copies
     ctx->slot ^= 1;
     return JD_OK;
@@ -1209,15 +1211,25 @@ jd_status collect_until(jd_ctx* ctx, int keep) {
 jd_status finish_all(jd_ctx* ctx) { return collect_until(ctx, 0); }
 
 // Decodes again, with worst-case pools, the images of collected batches that overflowed an
-// optimistic one (kStOverflow), and fills their results.  Every batch is collected first (the
-// retries use both slots' scratch), so a retry costs the pipeline's overlap once.  The images'
-// parsed headers and device bytes were kept with their batch (Pending), so nothing is read from the
-// caller's host buffers, which may have been reused since.
+// optimistic one (kStOverflow), and fills their results.  The retry runs as synchronous batches
+// on the next launch's slot, which holds no batch at async depth 1 (the collected ones ran there),
+// while the other slot's batch keeps running; otherwise every batch is collected first.  The
+// images' parsed headers and device bytes were kept with their batch (Pending), so nothing is read
+// from the caller's host buffers, which may have been reused since.
 jd_status run_retries(jd_ctx* ctx, void* hip_stream) {
     if (ctx->worst) return JD_OK;  // (a retry's own batches are never retried)
     while (!ctx->retry.empty()) {
-        jd_status st = finish_all(ctx);  // (may add retries)
+        int active = 0;
+        bool next_busy = false;
+        for (const Pending& pd : ctx->pend)
+            if (pd.active) {
+                active++;
+                next_busy = next_busy || pd.slot == ctx->slot;
+            }
+        jd_status st = JD_OK;
+        if (active > 1 || next_busy) st = finish_all(ctx);  // (may add retries)
         if (st != JD_OK) return st;
+        const int keep_slot = ctx->slot;
         std::vector<jd_ctx::Retry> r;
         r.swap(ctx->retry);
         for (int mode = 0; mode < 2; mode++) {
@@ -1237,11 +1249,13 @@ jd_status run_retries(jd_ctx* ctx, void* hip_stream) {
             ctx->worst = true;
             for (int lo = 0; lo < m && st == JD_OK;) {
                 const int hi = batch_split(ctx, lo, m, items.data());
+                ctx->slot = keep_slot;
                 hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->slots[ctx->slot].stream;
                 st = launch_batch(ctx, items.data(), lo, hi, res.data(), mode, s);
-                if (st == JD_OK) st = finish_all(ctx);
+                if (st == JD_OK) st = finish_batch(ctx, ctx->pend[(ctx->seq - 1) % kNumPending]);
                 lo = hi;
             }
+            ctx->slot = keep_slot;  // (the other slot's batch, if any, stays the older one in flight)
             ctx->worst = false;
             if (st != JD_OK) return st;
             for (int j = 0; j < m; j++) *r[idx[size_t(j)]].res = res[size_t(j)];
