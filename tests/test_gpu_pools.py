@@ -178,3 +178,31 @@ def test_optimistic_pools_smaller_than_worst_case():
         finally:
             dec.close()
     assert peaks[False] <= 0.7 * peaks[True], peaks
+
+
+def test_synchronize_runs_pending_retries():
+    """jd_synchronize collects a pipelined batch and decodes its overflowed images again before it
+    returns, like jd_decode_wait."""
+    import torch
+
+    datas = [_flat(1920, 1080, "4:2:0", 0, 99), jd_synth.encode(jd_synth.synth_pixels(640, 480, 90), 90, "4:2:0", 1)]
+    hdrs = [jdamd.parse(d) for d in datas]
+    ooffs, otot = [], 0
+    for h in hdrs:
+        ooffs.append(otot)
+        otot += (h.width * h.height * 3 + 255) // 256 * 256
+    dec = jdamd.Decoder(0, path="full")
+    try:
+        out = torch.zeros(otot, dtype=torch.uint8, device="cuda:0")
+        hosts = [np.frombuffer(d, np.uint8).copy() for d in datas]
+        bt = dec.make_batch(hosts, [None] * len(datas), [out.data_ptr() + o for o in ooffs])
+        dec.decode_prepared(bt, pipelined=True)
+        dec.synchronize()
+        assert [r.status for r in bt[1]] == [0, 0]
+        assert dec.stats()["retried_images"] == 1
+        flat = out.cpu().numpy()
+        for i, (d, h) in enumerate(zip(datas, hdrs)):
+            got = flat[ooffs[i]:ooffs[i] + h.width * h.height * 3].reshape(h.height, h.width, 3)
+            assert np.array_equal(got, jdoracle.decode(d)[1]), i
+    finally:
+        dec.close()
