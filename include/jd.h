@@ -218,7 +218,8 @@ typedef struct jd_stats {
      * trailing bytes) */
     double redo_pieces, fix_intervals, fix_rounds, fix_rewalks, fix_early;
     /* images decoded again with worst-case pools after overflowing an optimistic one
-     * (JD_FLAG_WORST_CASE_POOLS) */
+     * (JD_FLAG_WORST_CASE_POOLS); the retry's batch counts in batches, images, pixels and the
+     * kernel figures like any other */
     double retried_images;
 } jd_stats;
 jd_status jd_get_stats(jd_ctx* ctx, jd_stats* out);
