@@ -657,6 +657,7 @@ size_t reserve(size_t& end, size_t bytes) {
 }
 
 jd_status finish_batch(jd_ctx* ctx, Pending& pd);
+jd_status run_retries(jd_ctx* ctx, void* hip_stream);
 
 // Grow-only pinned buffer of a pending slot (the slot is idle when this is called).
 hipError_t ensure_pinned(void*& p, size_t& cap, size_t bytes) {
@@ -693,7 +694,8 @@ jd_status launch_batch(jd_ctx* ctx, const jd_item* items, int lo, int hi, jd_res
     Slot& sl = ctx->slots[ctx->slot];
     Pending& pd = ctx->pend[ctx->seq % kNumPending];
     if (pd.active) {  // (the async depth keeps fewer batches in flight: normally collected already)
-        const jd_status fst = finish_batch(ctx, pd);
+        jd_status fst = finish_batch(ctx, pd);
+        if (fst == JD_OK) fst = run_retries(ctx, s);  // (before this launch reuses a slot)
         if (fst != JD_OK) return fst;
     }
     // The slot's previous batch (launched two calls ago) may still run: its device scratch is
@@ -1211,14 +1213,22 @@ jd_status collect_until(jd_ctx* ctx, int keep) {
 jd_status finish_all(jd_ctx* ctx) { return collect_until(ctx, 0); }
 
 // Decodes again, with worst-case pools, the images of collected batches that overflowed an
-// optimistic one (kStOverflow), and fills their results.  The retry runs as synchronous batches
-// on the next launch's slot, which holds no batch at async depth 1 (the collected ones ran there),
-// while the other slot's batch keeps running; otherwise every batch is collected first.  The
-// images' parsed headers and device bytes were kept with their batch (Pending), so nothing is read
-// from the caller's host buffers, which may have been reused since.
+// optimistic one (kStOverflow), and fills their results.  Called right after every collection
+// point, before anything else is launched: the retry reads a host input's copy in its slot's
+// device input pool, which the slot's next launch would replace.  The retry runs as synchronous
+// batches on the next launch's slot, which holds no batch at async depth 1 (the collected ones ran
+// there), while the other slot's batch keeps running; otherwise every batch is collected first.
+// The images' parsed headers and device bytes were kept with their batch (Pending), so nothing is
+// read from the caller's host buffers, which may have been reused since; the caller's own parse
+// results (decode_batch's further sub-batches) are kept aside meanwhile.
 jd_status run_retries(jd_ctx* ctx, void* hip_stream) {
-    if (ctx->worst) return JD_OK;  // (a retry's own batches are never retried)
-    while (!ctx->retry.empty()) {
+    if (ctx->worst || ctx->retry.empty()) return JD_OK;  // (a retry's own batches are never retried)
+    std::vector<ParsedJpeg> keep_parsed;
+    std::vector<jd_status> keep_pst;
+    keep_parsed.swap(ctx->parsed);
+    keep_pst.swap(ctx->pst);
+    jd_status st = JD_OK;
+    while (st == JD_OK && !ctx->retry.empty()) {
         int active = 0;
         bool next_busy = false;
         for (const Pending& pd : ctx->pend)
@@ -1226,13 +1236,12 @@ jd_status run_retries(jd_ctx* ctx, void* hip_stream) {
                 active++;
                 next_busy = next_busy || pd.slot == ctx->slot;
             }
-        jd_status st = JD_OK;
         if (active > 1 || next_busy) st = finish_all(ctx);  // (may add retries)
-        if (st != JD_OK) return st;
+        if (st != JD_OK) break;
         const int keep_slot = ctx->slot;
         std::vector<jd_ctx::Retry> r;
         r.swap(ctx->retry);
-        for (int mode = 0; mode < 2; mode++) {
+        for (int mode = 0; mode < 2 && st == JD_OK; mode++) {
             std::vector<size_t> idx;
             for (size_t j = 0; j < r.size(); j++)
                 if ((r[j].rgb_on_device != 0) == (mode != 0)) idx.push_back(j);
@@ -1257,12 +1266,14 @@ jd_status run_retries(jd_ctx* ctx, void* hip_stream) {
             }
             ctx->slot = keep_slot;  // (the other slot's batch, if any, stays the older one in flight)
             ctx->worst = false;
-            if (st != JD_OK) return st;
+            if (st != JD_OK) break;
             for (int j = 0; j < m; j++) *r[idx[size_t(j)]].res = res[size_t(j)];
             ctx->stats.retried_images += double(m);
         }
     }
-    return JD_OK;
+    ctx->parsed.swap(keep_parsed);
+    ctx->pst.swap(keep_pst);
+    return st;
 }
 
 }  // namespace
@@ -1488,14 +1499,16 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
     // Without a caller stream each slot runs on its own stream; a caller stream orders both slots.
     // Switching streams first collects the pending batches.
     if (hip_stream != ctx->last_stream) {
-        const jd_status st = finish_all(ctx);
+        jd_status st = finish_all(ctx);
+        if (st == JD_OK) st = run_retries(ctx, const_cast<void*>(ctx->last_stream));  // (on their own stream)
         if (st != JD_OK) return st;
         ctx->last_stream = hip_stream;
     }
     // The output pool is shared by the slots: with host outputs, collect first, and collect every
     // sub-batch before launching the next.  Host inputs are staged per slot and pipeline.
     if (!rgb_on_device) {
-        const jd_status st = finish_all(ctx);
+        jd_status st = finish_all(ctx);
+        if (st == JD_OK) st = run_retries(ctx, hip_stream);
         if (st != JD_OK) return st;
         async = false;
     }
@@ -1514,14 +1527,16 @@ jd_status decode_batch(jd_ctx* ctx, const jd_item* items, int n, jd_result* resu
         // for); otherwise collect this sub-batch before the next one reuses the staging and
         // output pools
         st = collect_until(ctx, async ? ctx->async_depth : 0);
+        if (st == JD_OK) st = run_retries(ctx, hip_stream);  // (before the next sub-batch reuses a slot)
         if (st != JD_OK) return st;
         lo = hi;
     }
     if (!async) {
-        const jd_status st = finish_all(ctx);
+        jd_status st = finish_all(ctx);
+        if (st == JD_OK) st = run_retries(ctx, hip_stream);
         if (st != JD_OK) return st;
     }
-    return run_retries(ctx, hip_stream);
+    return JD_OK;
 }
 }  // namespace
 

@@ -206,3 +206,67 @@ def test_synchronize_runs_pending_retries():
             assert np.array_equal(got, jdoracle.decode(d)[1]), i
     finally:
         dec.close()
+
+
+def _async_host_batch(dec, datas):
+    """A pipelined batch of host-staged inputs with device outputs; the caller's host bytes are
+    clobbered once the call returns (only the slot's device copy can produce the pixels)."""
+    import torch
+
+    hdrs = [jdamd.parse(d) for d in datas]
+    ooffs, otot = [], 0
+    for h in hdrs:
+        ooffs.append(otot)
+        otot += (h.width * h.height * 3 + 255) // 256 * 256
+    out = torch.zeros(otot, dtype=torch.uint8, device="cuda:0")
+    hosts = [np.frombuffer(d, np.uint8).copy() for d in datas]
+    bt = dec.make_batch(hosts, [None] * len(datas), [out.data_ptr() + o for o in ooffs])
+    dec.decode_prepared(bt, pipelined=True)
+    for h in hosts:
+        h[:] = 0
+    return bt, out, hdrs, ooffs, hosts
+
+
+def _check_async(bt, out, hdrs, ooffs, datas):
+    assert [r.status for r in bt[1]] == [0] * len(datas)
+    flat = out.cpu().numpy()
+    for i, (d, h) in enumerate(zip(datas, hdrs)):
+        got = flat[ooffs[i]:ooffs[i] + h.width * h.height * 3].reshape(h.height, h.width, 3)
+        assert np.array_equal(got, jdoracle.decode(d)[1]), i
+
+
+def test_retry_before_a_host_output_call_reuses_the_slot():
+    """A pipelined batch with an overflowing host-staged image, then a blocking call with host
+    outputs: that call collects the pipelined batch first, and its retry must run before the
+    call's own launch reuses a slot (and its device input pool)."""
+    a = [_flat(1920, 1080, "4:2:0", 0, 11), _flat(1024, 768, "4:4:4", 0, 222)]
+    b = [_flat(1280, 720, "4:2:0", 0, 66), jd_synth.encode(jd_synth.synth_pixels(640, 480, 91), 90, "4:2:0", 1)]
+    dec = jdamd.Decoder(0, path="full")
+    try:
+        ka = _async_host_batch(dec, a)
+        outs, status = dec.decode_batch(b)  # host outputs
+        assert status == [0, 0]
+        for d, o in zip(b, outs):
+            assert np.array_equal(o, jdoracle.decode(d)[1])
+        _check_async(*ka[:4], a)
+        assert dec.stats()["retried_images"] >= 3
+    finally:
+        dec.close()
+
+
+def test_retry_between_sub_batches(monkeypatch):
+    """A pipelined call split into sub-batches (JD_MAX_BATCH_IMAGES=2): a sub-batch collected
+    inside the call is retried before the next sub-batch reuses its slot."""
+    monkeypatch.setenv("JD_MAX_BATCH_IMAGES", "2")
+    sets = [[_flat(1920, 1080, "4:2:0", 0, 17 + 40 * k), _flat(1024, 768, "4:4:4", 0, 5 + 30 * k),
+             jd_synth.encode(jd_synth.synth_pixels(800, 600, 93 + k), 90, "4:2:0", 1),
+             _flat(1280, 720, "4:2:2", 0, 150 + 20 * k), _flat(640, 480, "4:2:0", 0, 77 + k)] for k in range(2)]
+    dec = jdamd.Decoder(0, path="full")
+    try:
+        runs = [_async_host_batch(dec, s) for s in sets]
+        dec.wait()
+        for (bt, out, hdrs, ooffs, _), s in zip(runs, sets):
+            _check_async(bt, out, hdrs, ooffs, s)
+        assert dec.stats()["retried_images"] >= 6
+    finally:
+        dec.close()
