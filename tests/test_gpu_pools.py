@@ -270,3 +270,25 @@ def test_retry_between_sub_batches(monkeypatch):
         assert dec.stats()["retried_images"] >= 6
     finally:
         dec.close()
+
+
+def test_large_batch_overflow_retried():
+    """A batch large enough for the device piece plan (k_pieceplan: full-size pieces grown to fill
+    the resident lanes, k_chain_fix, LDS-free re-walk tables) with flat images among C2-shaped
+    ones: the flat images overflow their regions, are retried, and every image is bit-exact."""
+    datas = jd_synth.make_batch(224, 1920, 1080, 90, "4:2:0", 1, 0, seed0=12000)
+    flats = [_flat(1920, 1080, "4:2:0", 0, 9 + 29 * k) for k in range(4)] + \
+            [_flat(1920, 1080, "4:4:4", 1, 200 - 31 * k) for k in range(4)]
+    for k, f in enumerate(flats):
+        datas.insert(17 + 25 * k, f)
+    dec = jdamd.Decoder(0, timing=True)
+    try:
+        outs, status = dec.decode_batch(datas)
+        assert status == [0] * len(datas)
+        st = dec.stats()
+        assert st["retried_images"] >= 4, st["retried_images"]  # at least the 4:2:0 flat images
+        for i, (d, o) in enumerate(zip(datas, outs)):
+            if d in flats or i % 16 == 0:
+                assert np.array_equal(o, jdoracle.decode(d)[1]), i
+    finally:
+        dec.close()
