@@ -3930,10 +3930,20 @@ __device__ __forceinline__ DcPred load_dcpred(const BatchDev& b, const ImgDesc& 
 
 // One wave per tile; grid: tiles x the batch's images of sampling layout M (b.mode_imgs).  (Two
 // tiles per wave, the second's BlockInfo loaded up front, took 3.7 instead of 2.9 ms: DESIGN.md §8.)
+// JD_IDCT_PRIO (experiment builds): a wave issues its descriptor, BlockInfo and entry loads at
+// raised priority, then drops to 0 for the DC prediction, IDCT and colour, so that a newly started
+// wave's loads go out ahead of the older waves' arithmetic.
+#ifndef JD_IDCT_PRIO
+#define JD_IDCT_PRIO 0
+#endif
+#ifndef JD_IDCT_PRIO_LATE
+#define JD_IDCT_PRIO_LATE 0  // (experiment builds) the reverse: priority raised once the loads are out
+#endif
 template <int M>
 __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDev b) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kIdctBufWords];
     __shared__ __attribute__((aligned(16))) int s_qz[kQzWords];
+    if (JD_IDCT_PRIO) __builtin_amdgcn_s_setprio(JD_IDCT_PRIO);
     const uint32_t lane = threadIdx.x, img = b.mode_imgs[b.mode_off[M] + blockIdx.y], tile = blockIdx.x;
     const ImgDesc& im = b.imgs[img];
     if (tile >= im.tiles_x * im.tiles_y) return;
@@ -3947,6 +3957,8 @@ __global__ __launch_bounds__(kIdctThreads, JD_IDCT_LB) void k_idct_color(BatchDe
     const EntryRange R = entry_range(b, im, bi, L.have);
     uint4 E[kPreQuads];
     load_entry_quads(R, E);
+    if (JD_IDCT_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (JD_IDCT_PRIO_LATE) __builtin_amdgcn_s_setprio(JD_IDCT_PRIO_LATE);
     const int dc_pred = tile_dc_predict(G, L, bi, dcin, lane);
     JD_STAMP_AT(1);
     __syncthreads();
