@@ -176,7 +176,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
     const bool interior = t0 >= lo && t0 + 64 < fend;
     // interior thread: exact per-byte masks (high bit of each byte lane), one word at a time with
     // the neighbours' masks carried
-    //   drop : 00 preceded by FF       brk : FF followed by neither 00 nor FF
+    //   drop : 00 preceded by FF       brk : FF followed by neither 00 nor FF, or FF 00 preceded
+    //                                        by FF (a run of FFs that ends in 00 is no stuffing but a
+    //                                        marker at its first FF: the oracle's reader stops there,
+    //                                        jdoracle.c br_fetch; never in a valid stream)
     // Only which words hold a break (brkw) and the stuffed zeros before each word (cum, a byte per
     // word) are kept for the break walk below, which recomputes the masks of those words alone:
     // keeping both masks of all 16 words took 84 VGPRs, so only one workgroup per CU fitted beside
@@ -189,12 +192,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
         uint32_t ff_cur, nz_cur;
         uint32_t zero_cur = scan_masks(w[0], ff_cur, nz_cur);
         const uint32_t nznext = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;  // byte after it
+        const uint32_t znext = (nextb == 0x00u) ? 0x80u : 0u;
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = 0;
+            uint32_t ff_nx = 0, nz_nx = nznext, zero_nx = znext;
             if (q < 15) zero_nx = scan_masks(w[q + 1], ff_nx, nz_nx);
-            const uint32_t dm = zero_cur & __builtin_amdgcn_alignbit(ff_cur, ff_prev, 24);  // (ff_cur << 8) | (ff_prev >> 24)
-            const uint32_t bm = ff_cur & __builtin_amdgcn_alignbit(nz_nx, nz_cur, 8);     // (nz_cur >> 8) | (nz_nx << 24)
+            const uint32_t ffb = __builtin_amdgcn_alignbit(ff_cur, ff_prev, 24);  // byte before is FF: (ff_cur << 8) | (ff_prev >> 24)
+            const uint32_t dm = zero_cur & ffb;
+            const uint32_t bm = ff_cur & (__builtin_amdgcn_alignbit(nz_nx, nz_cur, 8) |  // (nz_cur >> 8) | (nz_nx << 24)
+                                          (__builtin_amdgcn_alignbit(zero_nx, zero_cur, 8) & ffb));
             cum[q >> 2] = (q & 3) ? (cum[q >> 2] | (ndrop << (8 * (q & 3)))) : ndrop;
             ndrop += __builtin_popcount(dm);
             nbrk += __builtin_popcount(bm);
@@ -219,7 +225,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
             const uintptr_t a = t0 + i;
             const bool inr = a >= lo && a < fend;
             ndrop += (inr && a > lo && by == 0x00u && pb == 0xFFu) ? 1u : 0u;
-            nbrk += (inr && a + 1 < fend && by == 0xFFu && nb != 0x00u && nb != 0xFFu) ? 1u : 0u;
+            nbrk += (inr && a + 1 < fend && by == 0xFFu &&
+                     ((nb != 0x00u && nb != 0xFFu) || (nb == 0x00u && a > lo && pb == 0xFFu))) ? 1u : 0u;
         }
     }
     uint32_t tot_drop, tot_brk;
@@ -241,11 +248,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
                 const uint32_t wp = q > 0 ? *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(aq - 4) : 0u;
                 const uint32_t wn = q < 15 ? *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(aq + 4) : 0u;
                 uint32_t ff, nz, ffp = (prevb == 0xFFu) ? 0x80000000u : 0u, nzp, ffn, nzn = (nextb != 0x00u && nextb != 0xFFu) ? 0x80u : 0u;
+                uint32_t zn = (nextb == 0x00u) ? 0x80u : 0u;
                 const uint32_t zero = scan_masks(wc, ff, nz);
                 if (q > 0) (void)scan_masks(wp, ffp, nzp);
-                if (q < 15) (void)scan_masks(wn, ffn, nzn);
-                const uint32_t dm = zero & __builtin_amdgcn_alignbit(ff, ffp, 24);
-                uint32_t bm = ff & __builtin_amdgcn_alignbit(nzn, nz, 8);
+                if (q < 15) zn = scan_masks(wn, ffn, nzn);
+                const uint32_t ffb = __builtin_amdgcn_alignbit(ff, ffp, 24);
+                const uint32_t dm = zero & ffb;
+                uint32_t bm = ff & (__builtin_amdgcn_alignbit(nzn, nz, 8) | (__builtin_amdgcn_alignbit(zn, zero, 8) & ffb));
                 const uint32_t d = drop_before + ((cum[q >> 2] >> (8 * (q & 3))) & 0xFFu);
                 while (bm) {
                     const uint32_t bit = __builtin_ctz(bm);  // 7, 15, 23 or 31: byte k = bit >> 3
@@ -271,7 +280,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(BatchDev b) {
             const uintptr_t a = t0 + i;
             const bool inr = a >= lo && a < fend;
             d += (inr && a > lo && by == 0x00u && pb == 0xFFu) ? 1u : 0u;
-            if (inr && a + 1 < fend && by == 0xFFu && nb != 0x00u && nb != 0xFFu) {
+            if (inr && a + 1 < fend && by == 0xFFu && ((nb != 0x00u && nb != 0xFFu) || (nb == 0x00u && a > lo && pb == 0xFFu))) {
                 const uint32_t is_term = (nb & 0xF8u) == 0xD0u ? 0u : 1u;
                 if (off < b.brk_cap) out[off] = brk_make(threadIdx.x * uint32_t(kScanBytesPerThread) + uint32_t(i), d, is_term);
                 off++;

@@ -390,11 +390,15 @@ def test_mcu_inside_the_last_byte(decoder, params):
 #    walk, which had hit a garbage code before synchronising and a real one after the joined
 #    checkpoint: the real one must count (status corrupt; redo_piece, per-checkpoint errors);
 #  - 16045274: a flip turns the chroma DC table's first symbol into 16 (DC size 16, decoded by the
-#    reference and the oracle: jd_internal.hpp lut_entry).
+#    reference and the oracle: jd_internal.hpp lut_entry);
+#  - 64114030 (round 6, a flat-area image): a flip turns the byte before a stuffed FF 00 into FF,
+#    and the run FF FF 00 is a marker at its first FF, where the oracle's reader stops (status
+#    corrupt: the interval overruns it and no RSTn follows; jd_kernels.hip k_scan).
 @pytest.mark.parametrize("params", [
     {"seed": 16033655, "w": 74, "h": 179, "ss": "gray", "q": 35, "rows": 0, "blocks": 2, "flips": 1},
     {"seed": 16038946, "w": 366, "h": 10, "ss": "gray", "q": 100, "rows": 0, "blocks": 0, "flips": 1},
     {"seed": 16045274, "w": 11, "h": 68, "ss": "4:4:4", "q": 90, "rows": 0, "blocks": 0, "flips": 3},
+    {"seed": 64114030, "w": 318, "h": 183, "ss": "gray", "q": 75, "rows": 0, "blocks": 9, "flips": 1, "flat": True},
 ])
 def test_sweep_cases_every_path(params):
     import parity_sweep
